@@ -1,0 +1,223 @@
+/*
+ * mi_sim.h — C ABI of libmi_sim.so, the MI355X-native replacement for the closed
+ * PhysX GPU articulation pipeline + the task-layer TorchScript kernels that sit behind
+ * OmniIsaacGymEnvs' VecEnvBase / RLTask for the Humanoid, Ant and Cartpole tasks.
+ *
+ * Every entry point replaces one call site of the reference (file:line under
+ * tzmhuang/OmniIsaacGymEnvs v1.1.0, omniisaacgymenvs/...). The reference binds these from
+ * Python; the binding a maintainer would add is the ctypes stub in INTEGRATION.md
+ * (our own binding: omniisaacgymenvs_amd/native.py).
+ *
+ * Conventions
+ *  - Return 0 (MI_OK) on success, a negative MI_E_* code on failure; the message is in
+ *    mi_last_error() (thread-local). No C++ exception crosses this ABI.
+ *  - Ownership: an mi_sim owns ALL physics state (struct-of-arrays in device memory).
+ *    Every other buffer is caller-owned (PyTorch tensors); the library never frees or
+ *    retains them past the call.
+ *  - Pointers: tensor arguments are DEVICE pointers on the sim's device, row-major
+ *    [N, ...] exactly like the reference's torch buffers. `model`, `params`, `env_origins`,
+ *    `dof_limits` and task parameter structs are HOST pointers.
+ *  - Dtypes are those of the reference buffers: f32 state/obs/reward, int64 reset_buf /
+ *    progress_buf / reset indices, int32 effort indices.
+ *  - Streams: `stream` is a hipStream_t passed as void* (torch's current stream); every
+ *    call is stream-ordered and none blocks the host except create/destroy/info.
+ *  - A handle is not re-entrant: one host thread at a time.
+ */
+#ifndef MI_SIM_H
+#define MI_SIM_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define MI_ABI_VERSION 1
+
+enum {
+    MI_OK = 0,
+    MI_E_NULL = -1,    /* null pointer where a buffer is required            */
+    MI_E_SHAPE = -2,   /* size / count out of range                          */
+    MI_E_HIP = -3,     /* HIP runtime error                                  */
+    MI_E_MODEL = -4,   /* model description rejected                         */
+    MI_E_ARG = -5,     /* bad enum / parameter value                         */
+    MI_E_NODEV = -6,   /* no GPU / bad device id                             */
+    MI_E_STATE = -7    /* call out of order (e.g. task not configured)       */
+};
+
+/* Task kinds: which fused task kernels run on top of the physics. */
+enum { MI_TASK_CARTPOLE = 0, MI_TASK_ANT = 1, MI_TASK_HUMANOID = 2 };
+
+/* Dynamics kinds. */
+enum {
+    MI_DYN_ARTICULATION = 0, /* floating/fixed-base tree, CRBA + tree-LTDL + PGS contacts  */
+    MI_DYN_CARTPOLE = 1      /* analytic 2-DOF cart-pole (prismatic cart + hinge pole)      */
+};
+
+enum { MI_JOINT_HINGE = 0, MI_JOINT_SLIDE = 1 };
+enum { MI_GEOM_SPHERE = 0, MI_GEOM_CAPSULE = 1 };
+
+/*
+ * Compiled model description (host arrays). Produced from an MJCF-subset file by
+ * omniisaacgymenvs_amd/robots/model.py; replaces the USD articulation the reference
+ * pulls from Nucleus (robots/articulations/humanoid.py:57, ant.py:57, cartpole.py:56).
+ *
+ * Links: link 0 is the root. For a floating root (root_free=1) its 6 DOFs are the root
+ * linear (x,y,z, world) and angular (x,y,z, world) velocities; they are NOT part of the
+ * joint DOF vector the task sees. Links 1..L-1 each carry exactly ONE joint DOF
+ * (multi-DOF MJCF bodies are chains of massless 1-DOF links) in BFS order, and
+ * parent[l] < l. Joint DOF j belongs to link j+1.
+ */
+typedef struct mi_model_desc {
+    int32_t dyn_kind;        /* MI_DYN_*                                             */
+    int32_t root_free;       /* 1: floating base (free joint), 0: fixed base         */
+    int32_t num_links;       /* L, incl. root link 0                                 */
+    int32_t num_geoms;       /* G contact geoms                                      */
+    int32_t num_sensors;     /* S force sensors                                      */
+    int32_t num_pairs;       /* self-collision geom pairs (may be 0)                 */
+    const int32_t* parent;   /* [L]   parent link (-1 for root)                      */
+    const int32_t* jtype;    /* [L]   MI_JOINT_* (ignored for link 0)                */
+    const float* axis;       /* [L,3] joint axis in the link's joint frame (unit)    */
+    const float* pos;        /* [L,3] joint-frame origin in the parent link frame    */
+    const float* quat;       /* [L,4] joint-frame rotation wrt parent frame (wxyz)   */
+    const float* mass;       /* [L]                                                  */
+    const float* com;        /* [L,3] centre of mass in link frame                   */
+    const float* inertia;    /* [L,6] about com, link frame: xx yy zz xy xz yz       */
+    const float* lower;      /* [L]   joint limits (rad or m); lower>=upper: unlimited */
+    const float* upper;      /* [L]                                                  */
+    const float* damping;    /* [L]   joint viscous damping (implicit)               */
+    const float* armature;   /* [L]   joint armature (added to M diagonal)           */
+    const int32_t* geom_link;/* [G]                                                  */
+    const int32_t* geom_type;/* [G]   MI_GEOM_*                                      */
+    const float* geom_p0;    /* [G,3] sphere centre / capsule end 0, link frame      */
+    const float* geom_p1;    /* [G,3] capsule end 1 (ignored for spheres)            */
+    const float* geom_radius;/* [G]                                                  */
+    const int32_t* sensor_link; /* [S] force sensor body                              */
+    const float* sensor_pos; /* [S,3] sensor site in link frame (wrench reference)   */
+    const int32_t* pairs;    /* [P,2] self-collision geom pairs                      */
+    /* analytic cart-pole parameters (dyn_kind == MI_DYN_CARTPOLE)                   */
+    float cart_mass, pole_mass, pole_com, pole_inertia, cart_damping, pole_damping;
+} mi_model_desc;
+
+/* Scene / solver parameters — the task YAML `sim:` + `physx:` surface
+ * (cfg/task/Humanoid.yaml:34-63, utils/config_utils/default_scene_params.py:30-112). */
+typedef struct mi_sim_params {
+    float dt;                       /* sim.dt                                         */
+    float gravity[3];               /* sim.gravity                                    */
+    int32_t solver_iterations;      /* physx.solver_position_iteration_count (+vel)   */
+    float contact_offset;           /* physx.contact_offset                           */
+    float rest_offset;              /* physx.rest_offset                              */
+    float friction;                 /* default_physics_material.dynamic_friction      */
+    float max_depenetration_velocity;
+    float erp;                      /* position-error reduction per substep (0..1)    */
+    int32_t enable_self_collisions; /* <Actor>.enable_self_collisions                 */
+    float max_angular_velocity;     /* rad/s, PhysX default 5729.58 deg/s             */
+} mi_sim_params;
+
+/* Task-layer parameters (cfg/task/{Humanoid,Ant,Cartpole}.yaml `env:` + task
+ * constants from tasks/shared/locomotion.py:147-171, tasks/humanoid.py:81-112,
+ * tasks/ant.py:79-86, tasks/cartpole.py:54-62). */
+typedef struct mi_task_params {
+    int32_t task_kind;              /* MI_TASK_*                                      */
+    int32_t num_obs;                /* O                                              */
+    int32_t num_actions;            /* A                                              */
+    float clip_actions, clip_obs;   /* env.clipActions / env.clipObservations (inf)   */
+    float max_episode_length;       /* env.episodeLength (cartpole: 500)              */
+    /* locomotion */
+    float power_scale, heading_weight, up_weight, actions_cost, energy_cost;
+    float dof_vel_scale, angular_velocity_scale, contact_force_scale;
+    float joints_at_limit_cost, death_cost, termination_height, alive_reward_scale;
+    float task_dt;                  /* locomotion.py:163, 1/60                         */
+    float target[3];                /* locomotion.py:161, (1000,0,0)                   */
+    float init_root_pos[3];         /* spawn translation, env frame                   */
+    float init_root_quat[4];        /* wxyz                                           */
+    float dof_pos_noise, dof_vel_noise; /* locomotion.py:120,124: 0.2, 0.1            */
+    const float* joint_gears;       /* [A] host                                       */
+    const float* motor_effort_ratio;/* [A] host                                       */
+    const float* init_dof_pos;      /* [D] host                                       */
+    /* cartpole */
+    float reset_dist, max_push_effort;
+} mi_task_params;
+
+typedef struct mi_sim mi_sim;
+
+/* --- lifecycle: replaces World/SimulationContext + GridCloner + ArticulationView init
+ *     (tasks/base/rl_task.py:109-131, utils/task_util.py:70) ---------------------------- */
+int mi_sim_create(const mi_model_desc* model, const mi_sim_params* params, int32_t num_envs,
+                  int64_t env_id_offset, int32_t device_id, const float* env_origins /*[N,3]*/,
+                  uint64_t seed, mi_sim** out);
+int mi_sim_destroy(mi_sim* sim);
+/* ArticulationView.num_dof / count / get_dof_limits (humanoid.py:110, ant.py:81) */
+int mi_sim_info(const mi_sim* sim, int32_t* num_envs, int32_t* num_dof, int32_t* num_links,
+                int32_t* num_sensors, float* dof_limits /*[D,2] host or NULL*/);
+
+/* --- ArticulationView tensor API (call sites locomotion.py:81-89,114,130-134) -------- */
+int mi_get_root_state(mi_sim* sim, float* pos /*[N,3]*/, float* quat /*[N,4] wxyz*/,
+                      float* vel /*[N,6] lin,ang*/, void* stream);
+int mi_get_dof_state(mi_sim* sim, float* q /*[N,D]*/, float* qd /*[N,D]*/, void* stream);
+int mi_get_sensor_wrench(mi_sim* sim, float* out /*[N,S,6]*/, void* stream);
+int mi_set_dof_efforts(mi_sim* sim, const float* eff /*[n,D]*/, const int32_t* idx /*[n]|NULL*/,
+                       int32_t n, void* stream);
+int mi_set_dof_state(mi_sim* sim, const float* q /*[n,D]|NULL*/, const float* qd /*[n,D]|NULL*/,
+                     const int64_t* idx /*[n]|NULL*/, int32_t n, void* stream);
+int mi_set_root_state(mi_sim* sim, const float* pos /*[n,3]|NULL*/, const float* quat /*[n,4]|NULL*/,
+                      const float* vel /*[n,6]|NULL*/, const int64_t* idx /*[n]|NULL*/, int32_t n,
+                      void* stream);
+
+/* --- physics step: World.step x controlFrequencyInv (envs/vec_env_rlgames.py:64-66) --- */
+int mi_sim_step(mi_sim* sim, int32_t substeps, void* stream);
+
+/* --- fused task kernels ---------------------------------------------------------------- */
+int mi_task_configure(mi_sim* sim, const mi_task_params* tp);
+/* LocomotionTask.pre_physics_step / CartpoleTask.pre_physics_step
+ * (locomotion.py:103-145, cartpole.py:101-134): mask-driven reset_idx for every env with
+ * reset_buf != 0 (no host sync), actions_out = actions, efforts = actions*gear*power. */
+int mi_task_pre_step(mi_sim* sim, const float* actions /*[N,A]*/, int64_t* reset_buf,
+                     int64_t* progress_buf, float* potentials, float* prev_potentials,
+                     float* actions_out /*[N,A]|NULL*/, void* stream);
+/* reset_idx(env_ids) with explicit indices (locomotion.py:116-145, cartpole.py:114-134) */
+int mi_task_reset_idx(mi_sim* sim, const int64_t* env_ids, int32_t n, int64_t* reset_buf,
+                      int64_t* progress_buf, float* potentials, float* prev_potentials,
+                      void* stream);
+/* RLTask.post_physics_step (rl_task.py:231-251): progress += 1, get_observations,
+ * calculate_metrics, is_done — one kernel (locomotion.py:80-101,173-321,
+ * humanoid.py:116-127, ant.py:88-95, cartpole.py:80-99,143-162). */
+int mi_task_post_step(mi_sim* sim, const float* actions /*[N,A]*/, float* obs /*[N,O]*/,
+                      float* rew /*[N]*/, int64_t* reset_buf, int64_t* progress_buf,
+                      float* potentials, float* prev_potentials, void* stream);
+/* The three task methods RLTask.post_physics_step calls, as separate kernels
+ * (rl_task.py:244-250) for tasks that override some of them in torch:
+ * get_observations (locomotion.py:80-101 / cartpole.py:80-99) writes obs + potentials,
+ * calculate_metrics (locomotion.py:173-178 / cartpole.py:143-153) reads obs,
+ * is_done (locomotion.py:180-183 / cartpole.py:155-162) reads obs[:,0] and progress_buf. */
+int mi_task_observations(mi_sim* sim, const float* actions /*[N,A]*/, float* obs /*[N,O]*/,
+                         float* potentials, float* prev_potentials, void* stream);
+int mi_task_metrics(mi_sim* sim, const float* actions, const float* obs, float* rew,
+                    const float* potentials, const float* prev_potentials, void* stream);
+int mi_task_is_done(mi_sim* sim, const float* obs, int64_t* reset_buf, const int64_t* progress_buf,
+                    void* stream);
+/* VecEnvRLGames.step (vec_env_rlgames.py:56-78) minus the Python: clamp actions,
+ * pre_physics_step, `substeps` physics steps, post_physics_step and _process_data's obs
+ * clamp, in ONE kernel launch. obs_task (unclamped task.obs_buf) may be NULL. */
+int mi_env_step(mi_sim* sim, const float* actions /*[N,A]*/, int32_t substeps,
+                float* obs_out /*[N,O] clamped*/, float* obs_task /*[N,O]|NULL*/,
+                float* rew /*[N]*/, int64_t* reset_buf, int64_t* progress_buf,
+                float* potentials, float* prev_potentials, float* actions_out /*[N,A]|NULL*/,
+                void* stream);
+
+/* --- utilities --------------------------------------------------------------------- */
+/* U(lo,hi) Philox4x32-10 actions for the random-policy driver (scripts/random_policy.py:57),
+ * keyed on (seed, env_id_offset + env, step). */
+int mi_fill_uniform(mi_sim* sim, float* out /*[N,cols]*/, int32_t cols, uint64_t seed,
+                    uint64_t step, float lo, float hi, void* stream);
+/* Per-env reset counters (the Philox counter of the reset noise stream) -> host [N]. */
+int mi_get_reset_count(mi_sim* sim, uint32_t* out /*[N] host*/);
+/* Number of env-steps whose physics produced a non-finite state and were forced to reset. */
+int mi_sim_nan_count(mi_sim* sim, int64_t* count);
+int mi_abi_version(void);
+const char* mi_last_error(void);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* MI_SIM_H */

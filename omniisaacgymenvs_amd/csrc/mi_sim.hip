@@ -1,0 +1,668 @@
+// mi_sim.hip — kernels + C ABI of libmi_sim.so (include/mi_sim.h), gfx950.
+//
+// Round-1 mapping: one lane per env, `block` lanes per workgroup (default 64 = one wave).
+// The fused env step (mi_env_step) is ONE launch per VecEnvRLGames.step: mask-driven reset,
+// action clamp + efforts, controlFrequencyInv physics substeps, obs / reward / done and the
+// VecEnv obs clamp, with the per-env solver workspace resident in L2 / MALL between phases.
+#include <hip/hip_runtime.h>
+
+#include <cmath>
+#include <cstdarg>
+#include <cstdio>
+#include <cstring>
+#include <string>
+#include <vector>
+
+#include "mi_artic.hpp"
+#include "mi_device.hpp"
+#include "mi_task.hpp"
+
+using namespace mi;
+
+// ---------------------------------------------------------------------------------------
+// errors
+// ---------------------------------------------------------------------------------------
+static thread_local std::string g_err;
+
+static int fail(int code, const char* fmt, ...) {
+    char buf[512];
+    va_list ap;
+    va_start(ap, fmt);
+    vsnprintf(buf, sizeof buf, fmt, ap);
+    va_end(ap);
+    g_err = buf;
+    return code;
+}
+
+#define HIP_TRY(expr)                                                                    \
+    do {                                                                                 \
+        hipError_t e_ = (expr);                                                          \
+        if (e_ != hipSuccess)                                                            \
+            return fail(MI_E_HIP, "%s: %s (%s:%d)", #expr, hipGetErrorString(e_), __FILE__, \
+                        __LINE__);                                                       \
+    } while (0)
+
+#define LAUNCH_CHECK()                                                                   \
+    do {                                                                                 \
+        hipError_t e_ = hipGetLastError();                                               \
+        if (e_ != hipSuccess) return fail(MI_E_HIP, "launch: %s", hipGetErrorString(e_)); \
+    } while (0)
+
+// ---------------------------------------------------------------------------------------
+// handle
+// ---------------------------------------------------------------------------------------
+struct mi_sim {
+    int device = 0;
+    int N = 0;
+    int block = 64;
+    DevModel dm{};
+    DevState ds{};
+    SimP sp{};
+    DevTask tp{};
+    bool task_ok = false;
+    std::vector<float> lower, upper;  // host copy for mi_sim_info
+    std::vector<void*> allocs;
+};
+
+static int dev_alloc(mi_sim* s, void** p, size_t bytes) {
+    if (bytes == 0) bytes = 16;
+    HIP_TRY(hipMalloc(p, bytes));
+    s->allocs.push_back(*p);
+    HIP_TRY(hipMemset(*p, 0, bytes));
+    return MI_OK;
+}
+
+template <typename T>
+static int upload(mi_sim* s, const T* host, size_t count, const T** out) {
+    void* p = nullptr;
+    int rc = dev_alloc(s, &p, count * sizeof(T));
+    if (rc) return rc;
+    if (count && host) HIP_TRY(hipMemcpy(p, host, count * sizeof(T), hipMemcpyHostToDevice));
+    *out = (const T*)p;
+    return MI_OK;
+}
+
+static inline dim3 grid_for(const mi_sim* s, int n) { return dim3((n + s->block - 1) / s->block); }
+
+// ---------------------------------------------------------------------------------------
+// kernels
+// ---------------------------------------------------------------------------------------
+__device__ __forceinline__ void physics_env(const DevModel& m, const DevState& st, const SimP& p,
+                                            int i, int substeps) {
+    if (m.dyn == MI_DYN_CARTPOLE) {
+        const int N = st.N;
+        float x = st.q[i], th = st.q[N + i], xd = st.qd[i], thd = st.qd[N + i];
+        const float F0 = st.eff[i], F1 = st.eff[N + i];
+        for (int s = 0; s < substeps; ++s) cartpole_substep(m, p, x, th, xd, thd, F0, F1);
+        st.q[i] = x; st.q[N + i] = th; st.qd[i] = xd; st.qd[N + i] = thd;
+        if (!(isfinite(x) && isfinite(th) && isfinite(xd) && isfinite(thd))) st.nan_flag[i] = 1;
+    } else {
+        for (int s = 0; s < substeps; ++s) artic_substep(m, st, p, i);
+    }
+}
+
+__global__ void k_sim_step(DevModel m, DevState st, SimP p, int substeps) {
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= st.N) return;
+    physics_env(m, st, p, i, substeps);
+}
+
+__global__ void k_pre_step(DevModel m, DevState st, DevTask tp, const float* actions,
+                           int64_t* reset_buf, int64_t* progress_buf, float* pot, float* prev,
+                           float* actions_out) {
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= st.N) return;
+    task_pre_env(m, st, tp, i, actions, reset_buf, progress_buf, pot, prev, actions_out, false);
+}
+
+// locomotion post for one env from a row buffer R (unclamped obs row). act = actions row.
+__device__ __forceinline__ void loco_post(const DevModel& m, const DevState& st, const DevTask& tp,
+                                          int i, const float* act, float act_clip, float* R,
+                                          float* rew, int64_t* reset_buf, int64_t* progress_buf,
+                                          float* pot, float* prev) {
+    const int64_t progress = progress_buf[i] + 1;                 // rl_task.py:242
+    loco_obs_env(m, st, tp, i, act, act_clip, R, pot, prev);      // get_observations
+    const float* ca = R + 12 + 2 * m.D + 6 * m.S;                 // task.actions (clamped)
+    rew[i] = loco_reward(tp, m.D, R, ca, pot[i], prev[i]);        // calculate_metrics
+    reset_buf[i] = nan_guard(st, i, loco_done(tp, R[0], reset_buf[i], progress));  // is_done
+    progress_buf[i] = progress;
+}
+
+__device__ __forceinline__ void cartpole_post(const DevState& st, const DevTask& tp, int i, float* R,
+                                              float* rew, int64_t* reset_buf,
+                                              int64_t* progress_buf) {
+    const int64_t progress = progress_buf[i] + 1;
+    cartpole_obs_env(st, i, R);
+    rew[i] = cartpole_reward(tp, R);
+    reset_buf[i] = nan_guard(st, i, cartpole_done(tp, R, progress));
+    progress_buf[i] = progress;
+}
+
+// RLTask.post_physics_step (rl_task.py:231-251) for the built-in tasks, one launch
+__global__ void k_post_step(DevModel m, DevState st, DevTask tp, const float* actions, float* obs,
+                            float* rew, int64_t* reset_buf, int64_t* progress_buf, float* pot,
+                            float* prev) {
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= st.N) return;
+    float* R = obs + (size_t)tp.O * i;
+    if (tp.kind == MI_TASK_CARTPOLE)
+        cartpole_post(st, tp, i, R, rew, reset_buf, progress_buf);
+    else
+        loco_post(m, st, tp, i, actions + (size_t)tp.A * i, INFINITY, R, rew, reset_buf,
+                  progress_buf, pot, prev);
+}
+
+// the three task methods as separate kernels, for tasks that override some of them
+__global__ void k_observations(DevModel m, DevState st, DevTask tp, const float* actions,
+                               float* obs, float* pot, float* prev) {
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= st.N) return;
+    float* R = obs + (size_t)tp.O * i;
+    if (tp.kind == MI_TASK_CARTPOLE)
+        cartpole_obs_env(st, i, R);
+    else
+        loco_obs_env(m, st, tp, i, actions + (size_t)tp.A * i, INFINITY, R, pot, prev);
+}
+__global__ void k_metrics(DevModel m, DevState st, DevTask tp, const float* actions,
+                          const float* obs, float* rew, const float* pot, const float* prev) {
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= st.N) return;
+    const float* R = obs + (size_t)tp.O * i;
+    rew[i] = tp.kind == MI_TASK_CARTPOLE
+                 ? cartpole_reward(tp, R)
+                 : loco_reward(tp, m.D, R, actions + (size_t)tp.A * i, pot[i], prev[i]);
+}
+__global__ void k_is_done(DevState st, DevTask tp, const float* obs, int64_t* reset_buf,
+                          const int64_t* progress_buf) {
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= st.N) return;
+    const float* R = obs + (size_t)tp.O * i;
+    const int64_t d = tp.kind == MI_TASK_CARTPOLE
+                          ? cartpole_done(tp, R, progress_buf[i])
+                          : loco_done(tp, R[0], reset_buf[i], progress_buf[i]);
+    reset_buf[i] = nan_guard(st, i, d);
+}
+
+__global__ void k_env_step(DevModel m, DevState st, SimP p, DevTask tp, const float* actions,
+                           int substeps, float* obs_out, float* obs_task, float* rew,
+                           int64_t* reset_buf, int64_t* progress_buf, float* pot, float* prev,
+                           float* actions_out) {
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= st.N) return;
+    // 1. VecEnvRLGames.step:57 action clamp + pre_physics_step (reset_idx, efforts)
+    task_pre_env(m, st, tp, i, actions, reset_buf, progress_buf, pot, prev, actions_out, true);
+    // 2. controlFrequencyInv x World.step
+    physics_env(m, st, p, i, substeps);
+    // 3. post_physics_step into the unclamped row, then _process_data's obs clamp
+    const int O = tp.O;
+    float* R = (obs_task ? obs_task : obs_out) + (size_t)O * i;
+    if (tp.kind == MI_TASK_CARTPOLE)
+        cartpole_post(st, tp, i, R, rew, reset_buf, progress_buf);
+    else
+        loco_post(m, st, tp, i, actions + (size_t)tp.A * i, tp.clip_actions, R, rew, reset_buf,
+                  progress_buf, pot, prev);
+    const float co = tp.clip_obs;
+    float* OUT = obs_out + (size_t)O * i;
+    if (obs_task) {
+        for (int k = 0; k < O; ++k) OUT[k] = clampf(R[k], -co, co);
+    } else if (co < INFINITY) {
+        for (int k = 0; k < O; ++k) OUT[k] = clampf(OUT[k], -co, co);
+    }
+}
+
+__global__ void k_reset_idx(DevModel m, DevState st, DevTask tp, const int64_t* ids, int n,
+                            int64_t* reset_buf, int64_t* progress_buf, float* pot, float* prev) {
+    const int t = blockIdx.x * blockDim.x + threadIdx.x;
+    if (t >= n) return;
+    const int64_t i = ids ? ids[t] : t;
+    if (i < 0 || i >= st.N) return;
+    task_reset_env(m, st, tp, (int)i, pot, prev);
+    if (reset_buf) reset_buf[i] = 0;
+    if (progress_buf) progress_buf[i] = 0;
+}
+
+// SoA [C][N] <-> row-major [N,C] (gather / scatter with optional indices)
+__global__ void k_soa_to_rows(const float* src, int N, int C, float* dst) {
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= N) return;
+    for (int c = 0; c < C; ++c) dst[(size_t)i * C + c] = src[(size_t)c * N + i];
+}
+template <typename IDX>
+__global__ void k_rows_to_soa(const float* src, int n, int C, const IDX* idx, int N, float* dst) {
+    const int t = blockIdx.x * blockDim.x + threadIdx.x;
+    if (t >= n) return;
+    const int64_t i = idx ? (int64_t)idx[t] : t;
+    if (i < 0 || i >= N) return;
+    for (int c = 0; c < C; ++c) dst[(size_t)c * N + i] = src[(size_t)t * C + c];
+}
+
+__global__ void k_init_state(DevState st, int D) {
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= st.N) return;
+    const int N = st.N;
+    for (int k = 0; k < 3; ++k) st.root_pos[(size_t)k * N + i] = st.origins[(size_t)k * N + i];
+    st.root_quat[i] = 1.0f;
+}
+
+__global__ void k_fill_uniform(int N, int64_t off, float* out, int cols, uint64_t seed,
+                               uint64_t step, float lo, float hi) {
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= N) return;
+    const uint64_t gid = (uint64_t)(off + i);
+    const float w = hi - lo;
+    float u[4];
+    for (int c = 0; c < cols; ++c) {
+        if ((c & 3) == 0) uniform4(seed, gid, (uint32_t)step, (uint32_t)(c >> 2), 1, u);
+        out[(size_t)i * cols + c] = w * u[c & 3] + lo;
+    }
+}
+
+// ---------------------------------------------------------------------------------------
+// C ABI
+// ---------------------------------------------------------------------------------------
+extern "C" {
+
+int mi_abi_version(void) { return MI_ABI_VERSION; }
+const char* mi_last_error(void) { return g_err.c_str(); }
+
+int mi_sim_create(const mi_model_desc* md, const mi_sim_params* prm, int32_t N, int64_t off,
+                  int32_t device_id, const float* env_origins, uint64_t seed, mi_sim** out) {
+    if (!md || !prm || !out || !env_origins) return fail(MI_E_NULL, "mi_sim_create: null argument");
+    *out = nullptr;
+    if (N <= 0) return fail(MI_E_SHAPE, "num_envs must be > 0 (got %d)", N);
+    const int L = md->num_links;
+    if (L < 1 || L - 1 > MI_MAXA) return fail(MI_E_MODEL, "num_links %d out of range [1,%d]", L, MI_MAXA + 1);
+    if (md->dyn_kind != MI_DYN_ARTICULATION && md->dyn_kind != MI_DYN_CARTPOLE)
+        return fail(MI_E_ARG, "bad dyn_kind %d", md->dyn_kind);
+    if (md->dyn_kind == MI_DYN_CARTPOLE && L != 3)
+        return fail(MI_E_MODEL, "cart-pole dynamics needs exactly 2 joints");
+    if (!md->parent || !md->jtype || !md->axis || !md->pos || !md->quat || !md->mass || !md->com ||
+        !md->inertia || !md->lower || !md->upper || !md->damping || !md->armature)
+        return fail(MI_E_NULL, "model arrays must not be null");
+    if (md->num_geoms < 0 || md->num_sensors < 0 || md->num_pairs < 0)
+        return fail(MI_E_MODEL, "negative counts");
+    if (md->num_geoms && (!md->geom_link || !md->geom_type || !md->geom_p0 || !md->geom_p1 || !md->geom_radius))
+        return fail(MI_E_NULL, "geom arrays must not be null");
+    if (md->num_sensors && (!md->sensor_link || !md->sensor_pos))
+        return fail(MI_E_NULL, "sensor arrays must not be null");
+    for (int l = 1; l < L; ++l)
+        if (md->parent[l] < 0 || md->parent[l] >= l)
+            return fail(MI_E_MODEL, "parent[%d]=%d must be in [0,%d)", l, md->parent[l], l);
+    for (int g = 0; g < md->num_geoms; ++g)
+        if (md->geom_link[g] < 0 || md->geom_link[g] >= L) return fail(MI_E_MODEL, "geom_link[%d] out of range", g);
+    for (int s = 0; s < md->num_sensors; ++s)
+        if (md->sensor_link[s] < 0 || md->sensor_link[s] >= L) return fail(MI_E_MODEL, "sensor_link[%d] out of range", s);
+    int ndev = 0;
+    if (hipGetDeviceCount(&ndev) != hipSuccess || ndev == 0) return fail(MI_E_NODEV, "no HIP device visible");
+    if (device_id < 0 || device_id >= ndev) return fail(MI_E_NODEV, "device_id %d out of range (%d devices)", device_id, ndev);
+    HIP_TRY(hipSetDevice(device_id));
+
+    mi_sim* s = new mi_sim();
+    s->device = device_id;
+    s->N = N;
+    if (const char* b = getenv("MI_SIM_BLOCK")) {
+        int v = atoi(b);
+        if (v >= 1 && v <= 1024) s->block = v;
+    }
+    auto cleanup = [&](int rc) { mi_sim_destroy(s); return rc; };
+    DevModel& m = s->dm;
+    m.dyn = md->dyn_kind;
+    m.root_free = md->root_free ? 1 : 0;
+    m.L = L;
+    m.D = L - 1;
+    m.nr = m.root_free ? 6 : 0;
+    m.nv = m.nr + m.D;
+    m.G = md->num_geoms;
+    m.S = md->num_sensors;
+    if (m.nv > MI_MAXNV) return cleanup(fail(MI_E_MODEL, "too many dofs"));
+    // derived tables
+    std::vector<int> dof_parent(m.nv > 0 ? m.nv : 1), dof_link(m.nv > 0 ? m.nv : 1), pt_geom, pt_end;
+    for (int k = 0; k < m.nr; ++k) { dof_parent[k] = k - 1; dof_link[k] = 0; }
+    for (int l = 1; l < L; ++l) {
+        const int k = m.nr + l - 1, P = md->parent[l];
+        dof_parent[k] = P == 0 ? m.nr - 1 : m.nr + P - 1;
+        dof_link[k] = l;
+    }
+    for (int g = 0; g < m.G; ++g) {
+        pt_geom.push_back(g); pt_end.push_back(0);
+        if (md->geom_type[g] == MI_GEOM_CAPSULE) { pt_geom.push_back(g); pt_end.push_back(1); }
+    }
+    m.npts = (int)pt_geom.size();
+    m.max_rows = 3 * m.npts + m.D;
+    int rc = 0;
+#define UP(field, src, cnt) if ((rc = upload(s, src, (size_t)(cnt), &m.field))) return cleanup(rc)
+    UP(parent, md->parent, L); UP(jtype, md->jtype, L); UP(axis, md->axis, 3 * L);
+    UP(pos, md->pos, 3 * L); UP(quat, md->quat, 4 * L); UP(mass, md->mass, L);
+    UP(com, md->com, 3 * L); UP(inertia, md->inertia, 6 * L); UP(lower, md->lower, L);
+    UP(upper, md->upper, L); UP(damping, md->damping, L); UP(armature, md->armature, L);
+    UP(dof_parent, dof_parent.data(), dof_parent.size()); UP(dof_link, dof_link.data(), dof_link.size());
+    UP(geom_link, md->geom_link, m.G); UP(geom_p0, md->geom_p0, 3 * m.G);
+    UP(geom_p1, md->geom_p1, 3 * m.G); UP(geom_radius, md->geom_radius, m.G);
+    UP(pt_geom, pt_geom.data(), pt_geom.size()); UP(pt_end, pt_end.data(), pt_end.size());
+    UP(sensor_link, md->sensor_link, m.S); UP(sensor_pos, md->sensor_pos, 3 * m.S);
+#undef UP
+    m.cart_mass = md->cart_mass; m.pole_mass = md->pole_mass; m.pole_com = md->pole_com;
+    m.pole_inertia = md->pole_inertia; m.cart_damping = md->cart_damping;
+    m.pole_damping = md->pole_damping;
+    // workspace slots (articulation only)
+    int o = 0;
+    if (m.dyn == MI_DYN_ARTICULATION) {
+        const int nv = m.nv, R = m.max_rows;
+        m.o_R = o; o += 9 * L;
+        m.o_o = o; o += 3 * L;
+        m.o_aw = o;
+        m.o_Ic = o; o += 10 * L;
+        m.o_S = o; o += 6 * nv;
+        m.o_V = o; o += 6 * L;
+        m.o_A = o; o += 6 * L;
+        m.o_F = o; o += 6 * L;
+        m.o_M = o; o += nv * nv;
+        m.o_u = o; o += nv;
+        m.o_r = o; o += nv;
+        m.o_Jr = o; o += R * nv;
+        m.o_W = o; o += R * nv;
+        m.o_b = o; o += R;
+        m.o_lam = o; o += R;
+        m.o_Ad = o; o += R;
+        m.o_rk = o; o += R;
+        m.o_cp = o; o += 3 * m.npts;
+        m.o_cl = o; o += m.npts;
+    }
+    m.slots = o;
+    s->lower.assign(md->lower, md->lower + L);
+    s->upper.assign(md->upper, md->upper + L);
+    // params
+    s->sp.dt = prm->dt;
+    for (int k = 0; k < 3; ++k) s->sp.g[k] = prm->gravity[k];
+    s->sp.iters = prm->solver_iterations;
+    s->sp.contact_offset = prm->contact_offset;
+    s->sp.rest_offset = prm->rest_offset;
+    s->sp.friction = prm->friction;
+    s->sp.max_depen = prm->max_depenetration_velocity;
+    s->sp.erp = prm->erp;
+    s->sp.max_angvel = prm->max_angular_velocity;
+    // state
+    DevState& st = s->ds;
+    st.N = N;
+    st.off = off;
+    st.seed = seed;
+    const int D = m.D > 0 ? m.D : 1, S = m.S > 0 ? m.S : 1;
+    void* p = nullptr;
+#define AL(field, T, cnt) if ((rc = dev_alloc(s, &p, sizeof(T) * (size_t)(cnt)))) return cleanup(rc); st.field = (T*)p
+    AL(root_pos, float, 3 * N); AL(root_quat, float, 4 * N); AL(root_vel, float, 6 * N);
+    AL(q, float, (size_t)D * N); AL(qd, float, (size_t)D * N); AL(eff, float, (size_t)D * N);
+    AL(sens, float, (size_t)6 * S * N); AL(reset_count, uint32_t, N); AL(nan_flag, int32_t, N);
+    AL(nan_total, unsigned long long, 1);
+    AL(ws, float, (size_t)((N + 63) / 64) * 64 * (m.slots > 0 ? m.slots : 1));
+#undef AL
+    std::vector<float> org((size_t)3 * N);
+    for (int i = 0; i < N; ++i)
+        for (int k = 0; k < 3; ++k) org[(size_t)k * N + i] = env_origins[(size_t)3 * i + k];
+    const float* od = nullptr;
+    if ((rc = upload(s, org.data(), org.size(), &od))) return cleanup(rc);
+    st.origins = od;
+    hipLaunchKernelGGL(k_init_state, grid_for(s, N), dim3(s->block), 0, 0, st, m.D);
+    hipError_t e = hipDeviceSynchronize();
+    if (e != hipSuccess) return cleanup(fail(MI_E_HIP, "init: %s", hipGetErrorString(e)));
+    *out = s;
+    return MI_OK;
+}
+
+int mi_sim_destroy(mi_sim* s) {
+    if (!s) return MI_OK;
+    (void)hipSetDevice(s->device);
+    for (void* p : s->allocs) (void)hipFree(p);
+    delete s;
+    return MI_OK;
+}
+
+int mi_sim_info(const mi_sim* s, int32_t* num_envs, int32_t* num_dof, int32_t* num_links,
+                int32_t* num_sensors, float* dof_limits) {
+    if (!s) return fail(MI_E_NULL, "null sim");
+    if (num_envs) *num_envs = s->N;
+    if (num_dof) *num_dof = s->dm.D;
+    if (num_links) *num_links = s->dm.L;
+    if (num_sensors) *num_sensors = s->dm.S;
+    if (dof_limits)
+        for (int j = 0; j < s->dm.D; ++j) {
+            dof_limits[2 * j] = s->lower[j + 1];
+            dof_limits[2 * j + 1] = s->upper[j + 1];
+        }
+    return MI_OK;
+}
+
+#define STREAM(x) ((hipStream_t)(x))
+#define NEED(p) if (!(p)) return fail(MI_E_NULL, "%s: null %s", __func__, #p)
+
+int mi_get_root_state(mi_sim* s, float* pos, float* quat, float* vel, void* stream) {
+    NEED(s);
+    HIP_TRY(hipSetDevice(s->device));
+    const dim3 g = grid_for(s, s->N), b(s->block);
+    if (pos) hipLaunchKernelGGL(k_soa_to_rows, g, b, 0, STREAM(stream), s->ds.root_pos, s->N, 3, pos);
+    if (quat) hipLaunchKernelGGL(k_soa_to_rows, g, b, 0, STREAM(stream), s->ds.root_quat, s->N, 4, quat);
+    if (vel) hipLaunchKernelGGL(k_soa_to_rows, g, b, 0, STREAM(stream), s->ds.root_vel, s->N, 6, vel);
+    LAUNCH_CHECK();
+    return MI_OK;
+}
+
+int mi_get_dof_state(mi_sim* s, float* q, float* qd, void* stream) {
+    NEED(s);
+    HIP_TRY(hipSetDevice(s->device));
+    const dim3 g = grid_for(s, s->N), b(s->block);
+    if (q) hipLaunchKernelGGL(k_soa_to_rows, g, b, 0, STREAM(stream), s->ds.q, s->N, s->dm.D, q);
+    if (qd) hipLaunchKernelGGL(k_soa_to_rows, g, b, 0, STREAM(stream), s->ds.qd, s->N, s->dm.D, qd);
+    LAUNCH_CHECK();
+    return MI_OK;
+}
+
+int mi_get_sensor_wrench(mi_sim* s, float* out, void* stream) {
+    NEED(s); NEED(out);
+    HIP_TRY(hipSetDevice(s->device));
+    if (s->dm.S == 0) return MI_OK;
+    hipLaunchKernelGGL(k_soa_to_rows, grid_for(s, s->N), dim3(s->block), 0, STREAM(stream),
+                       s->ds.sens, s->N, 6 * s->dm.S, out);
+    LAUNCH_CHECK();
+    return MI_OK;
+}
+
+int mi_set_dof_efforts(mi_sim* s, const float* eff, const int32_t* idx, int32_t n, void* stream) {
+    NEED(s); NEED(eff);
+    if (n < 0 || n > s->N || (!idx && n != s->N)) return fail(MI_E_SHAPE, "mi_set_dof_efforts: bad n=%d", n);
+    HIP_TRY(hipSetDevice(s->device));
+    if (n == 0) return MI_OK;
+    hipLaunchKernelGGL(k_rows_to_soa<int32_t>, grid_for(s, n), dim3(s->block), 0, STREAM(stream),
+                       eff, n, s->dm.D, idx, s->N, s->ds.eff);
+    LAUNCH_CHECK();
+    return MI_OK;
+}
+
+int mi_set_dof_state(mi_sim* s, const float* q, const float* qd, const int64_t* idx, int32_t n,
+                     void* stream) {
+    NEED(s);
+    if (n < 0 || n > s->N || (!idx && n != s->N)) return fail(MI_E_SHAPE, "mi_set_dof_state: bad n=%d", n);
+    HIP_TRY(hipSetDevice(s->device));
+    if (n == 0) return MI_OK;
+    const dim3 g = grid_for(s, n), b(s->block);
+    if (q) hipLaunchKernelGGL(k_rows_to_soa<int64_t>, g, b, 0, STREAM(stream), q, n, s->dm.D, idx, s->N, s->ds.q);
+    if (qd) hipLaunchKernelGGL(k_rows_to_soa<int64_t>, g, b, 0, STREAM(stream), qd, n, s->dm.D, idx, s->N, s->ds.qd);
+    LAUNCH_CHECK();
+    return MI_OK;
+}
+
+int mi_set_root_state(mi_sim* s, const float* pos, const float* quat, const float* vel,
+                      const int64_t* idx, int32_t n, void* stream) {
+    NEED(s);
+    if (n < 0 || n > s->N || (!idx && n != s->N)) return fail(MI_E_SHAPE, "mi_set_root_state: bad n=%d", n);
+    HIP_TRY(hipSetDevice(s->device));
+    if (n == 0) return MI_OK;
+    const dim3 g = grid_for(s, n), b(s->block);
+    if (pos) hipLaunchKernelGGL(k_rows_to_soa<int64_t>, g, b, 0, STREAM(stream), pos, n, 3, idx, s->N, s->ds.root_pos);
+    if (quat) hipLaunchKernelGGL(k_rows_to_soa<int64_t>, g, b, 0, STREAM(stream), quat, n, 4, idx, s->N, s->ds.root_quat);
+    if (vel) hipLaunchKernelGGL(k_rows_to_soa<int64_t>, g, b, 0, STREAM(stream), vel, n, 6, idx, s->N, s->ds.root_vel);
+    LAUNCH_CHECK();
+    return MI_OK;
+}
+
+int mi_sim_step(mi_sim* s, int32_t substeps, void* stream) {
+    NEED(s);
+    if (substeps < 0 || substeps > 64) return fail(MI_E_ARG, "substeps %d out of range", substeps);
+    HIP_TRY(hipSetDevice(s->device));
+    hipLaunchKernelGGL(k_sim_step, grid_for(s, s->N), dim3(s->block), 0, STREAM(stream), s->dm,
+                       s->ds, s->sp, substeps);
+    LAUNCH_CHECK();
+    return MI_OK;
+}
+
+int mi_task_configure(mi_sim* s, const mi_task_params* t) {
+    NEED(s); NEED(t);
+    if (t->task_kind < MI_TASK_CARTPOLE || t->task_kind > MI_TASK_HUMANOID)
+        return fail(MI_E_ARG, "bad task_kind %d", t->task_kind);
+    const int D = s->dm.D;
+    if (t->task_kind == MI_TASK_CARTPOLE) {
+        if (s->dm.dyn != MI_DYN_CARTPOLE) return fail(MI_E_ARG, "cartpole task needs cart-pole dynamics");
+        if (t->num_actions != 1 || t->num_obs != 4) return fail(MI_E_SHAPE, "cartpole: A=1, O=4");
+    } else {
+        if (s->dm.dyn != MI_DYN_ARTICULATION || !s->dm.root_free)
+            return fail(MI_E_ARG, "locomotion needs a floating-base articulation");
+        if (t->num_actions != D) return fail(MI_E_SHAPE, "locomotion: num_actions %d != num_dof %d", t->num_actions, D);
+        if (t->num_obs != 12 + 3 * D + 6 * s->dm.S)
+            return fail(MI_E_SHAPE, "locomotion: num_obs %d != 12+3D+6S = %d", t->num_obs, 12 + 3 * D + 6 * s->dm.S);
+        if (!t->joint_gears || !t->motor_effort_ratio) return fail(MI_E_NULL, "gears / effort ratio required");
+    }
+    DevTask& d = s->tp;
+    d = DevTask{};
+    d.kind = t->task_kind; d.O = t->num_obs; d.A = t->num_actions;
+    d.clip_actions = t->clip_actions; d.clip_obs = t->clip_obs;
+    d.max_episode_length = t->max_episode_length;
+    d.power_scale = t->power_scale; d.heading_weight = t->heading_weight; d.up_weight = t->up_weight;
+    d.actions_cost = t->actions_cost; d.energy_cost = t->energy_cost;
+    d.dof_vel_scale = t->dof_vel_scale; d.angular_velocity_scale = t->angular_velocity_scale;
+    d.contact_force_scale = t->contact_force_scale; d.joints_at_limit_cost = t->joints_at_limit_cost;
+    d.death_cost = t->death_cost; d.termination_height = t->termination_height;
+    d.alive_reward_scale = t->alive_reward_scale; d.task_dt = t->task_dt;
+    for (int k = 0; k < 3; ++k) { d.target[k] = t->target[k]; d.init_root_pos[k] = t->init_root_pos[k]; }
+    for (int k = 0; k < 4; ++k) d.init_root_quat[k] = t->init_root_quat[k];
+    d.dof_pos_noise = t->dof_pos_noise; d.dof_vel_noise = t->dof_vel_noise;
+    d.reset_dist = t->reset_dist; d.max_push_effort = t->max_push_effort;
+    for (int j = 0; j < t->num_actions && j < MI_MAXA; ++j) {
+        d.gears[j] = t->joint_gears ? t->joint_gears[j] : 1.0f;
+        d.ratio[j] = t->motor_effort_ratio ? t->motor_effort_ratio[j] : 1.0f;
+    }
+    for (int j = 0; j < D && j < MI_MAXA; ++j) d.init_dof[j] = t->init_dof_pos ? t->init_dof_pos[j] : 0.0f;
+    s->task_ok = true;
+    return MI_OK;
+}
+
+#define NEED_TASK(s) if (!(s)->task_ok) return fail(MI_E_STATE, "%s: mi_task_configure not called", __func__)
+
+int mi_task_pre_step(mi_sim* s, const float* actions, int64_t* reset_buf, int64_t* progress_buf,
+                     float* potentials, float* prev_potentials, float* actions_out, void* stream) {
+    NEED(s); NEED_TASK(s); NEED(actions); NEED(reset_buf); NEED(progress_buf);
+    if (s->tp.kind != MI_TASK_CARTPOLE) { NEED(potentials); NEED(prev_potentials); }
+    HIP_TRY(hipSetDevice(s->device));
+    hipLaunchKernelGGL(k_pre_step, grid_for(s, s->N), dim3(s->block), 0, STREAM(stream), s->dm,
+                       s->ds, s->tp, actions, reset_buf, progress_buf, potentials, prev_potentials,
+                       actions_out);
+    LAUNCH_CHECK();
+    return MI_OK;
+}
+
+int mi_task_reset_idx(mi_sim* s, const int64_t* env_ids, int32_t n, int64_t* reset_buf,
+                      int64_t* progress_buf, float* potentials, float* prev_potentials, void* stream) {
+    NEED(s); NEED_TASK(s);
+    if (n < 0 || n > s->N || (!env_ids && n != s->N)) return fail(MI_E_SHAPE, "mi_task_reset_idx: bad n=%d", n);
+    HIP_TRY(hipSetDevice(s->device));
+    if (n == 0) return MI_OK;
+    hipLaunchKernelGGL(k_reset_idx, grid_for(s, n), dim3(s->block), 0, STREAM(stream), s->dm, s->ds,
+                       s->tp, env_ids, n, reset_buf, progress_buf, potentials, prev_potentials);
+    LAUNCH_CHECK();
+    return MI_OK;
+}
+
+int mi_task_post_step(mi_sim* s, const float* actions, float* obs, float* rew, int64_t* reset_buf,
+                      int64_t* progress_buf, float* potentials, float* prev_potentials, void* stream) {
+    NEED(s); NEED_TASK(s); NEED(obs); NEED(rew); NEED(reset_buf); NEED(progress_buf);
+    if (s->tp.kind != MI_TASK_CARTPOLE) { NEED(actions); NEED(potentials); NEED(prev_potentials); }
+    HIP_TRY(hipSetDevice(s->device));
+    hipLaunchKernelGGL(k_post_step, grid_for(s, s->N), dim3(s->block), 0, STREAM(stream), s->dm,
+                       s->ds, s->tp, actions, obs, rew, reset_buf, progress_buf, potentials,
+                       prev_potentials);
+    LAUNCH_CHECK();
+    return MI_OK;
+}
+
+int mi_task_observations(mi_sim* s, const float* actions, float* obs, float* potentials,
+                         float* prev_potentials, void* stream) {
+    NEED(s); NEED_TASK(s); NEED(obs);
+    if (s->tp.kind != MI_TASK_CARTPOLE) { NEED(actions); NEED(potentials); NEED(prev_potentials); }
+    HIP_TRY(hipSetDevice(s->device));
+    hipLaunchKernelGGL(k_observations, grid_for(s, s->N), dim3(s->block), 0, STREAM(stream), s->dm,
+                       s->ds, s->tp, actions, obs, potentials, prev_potentials);
+    LAUNCH_CHECK();
+    return MI_OK;
+}
+
+int mi_task_metrics(mi_sim* s, const float* actions, const float* obs, float* rew,
+                    const float* potentials, const float* prev_potentials, void* stream) {
+    NEED(s); NEED_TASK(s); NEED(obs); NEED(rew);
+    if (s->tp.kind != MI_TASK_CARTPOLE) { NEED(actions); NEED(potentials); NEED(prev_potentials); }
+    HIP_TRY(hipSetDevice(s->device));
+    hipLaunchKernelGGL(k_metrics, grid_for(s, s->N), dim3(s->block), 0, STREAM(stream), s->dm,
+                       s->ds, s->tp, actions, obs, rew, potentials, prev_potentials);
+    LAUNCH_CHECK();
+    return MI_OK;
+}
+
+int mi_task_is_done(mi_sim* s, const float* obs, int64_t* reset_buf, const int64_t* progress_buf,
+                    void* stream) {
+    NEED(s); NEED_TASK(s); NEED(obs); NEED(reset_buf); NEED(progress_buf);
+    HIP_TRY(hipSetDevice(s->device));
+    hipLaunchKernelGGL(k_is_done, grid_for(s, s->N), dim3(s->block), 0, STREAM(stream), s->ds,
+                       s->tp, obs, reset_buf, progress_buf);
+    LAUNCH_CHECK();
+    return MI_OK;
+}
+
+int mi_env_step(mi_sim* s, const float* actions, int32_t substeps, float* obs_out, float* obs_task,
+                float* rew, int64_t* reset_buf, int64_t* progress_buf, float* potentials,
+                float* prev_potentials, float* actions_out, void* stream) {
+    NEED(s); NEED_TASK(s); NEED(actions); NEED(obs_out); NEED(rew); NEED(reset_buf); NEED(progress_buf);
+    if (s->tp.kind != MI_TASK_CARTPOLE) { NEED(potentials); NEED(prev_potentials); }
+    if (substeps < 0 || substeps > 64) return fail(MI_E_ARG, "substeps %d out of range", substeps);
+    HIP_TRY(hipSetDevice(s->device));
+    hipLaunchKernelGGL(k_env_step, grid_for(s, s->N), dim3(s->block), 0, STREAM(stream), s->dm,
+                       s->ds, s->sp, s->tp, actions, substeps, obs_out, obs_task, rew, reset_buf,
+                       progress_buf, potentials, prev_potentials, actions_out);
+    LAUNCH_CHECK();
+    return MI_OK;
+}
+
+int mi_fill_uniform(mi_sim* s, float* out, int32_t cols, uint64_t seed, uint64_t step, float lo,
+                    float hi, void* stream) {
+    NEED(s); NEED(out);
+    if (cols <= 0) return fail(MI_E_SHAPE, "cols must be > 0");
+    HIP_TRY(hipSetDevice(s->device));
+    hipLaunchKernelGGL(k_fill_uniform, grid_for(s, s->N), dim3(s->block), 0, STREAM(stream), s->N,
+                       s->ds.off, out, cols, seed, step, lo, hi);
+    LAUNCH_CHECK();
+    return MI_OK;
+}
+
+int mi_get_reset_count(mi_sim* s, uint32_t* out) {
+    NEED(s); NEED(out);
+    HIP_TRY(hipSetDevice(s->device));
+    HIP_TRY(hipDeviceSynchronize());
+    HIP_TRY(hipMemcpy(out, s->ds.reset_count, sizeof(uint32_t) * s->N, hipMemcpyDeviceToHost));
+    return MI_OK;
+}
+
+int mi_sim_nan_count(mi_sim* s, int64_t* count) {
+    NEED(s); NEED(count);
+    HIP_TRY(hipSetDevice(s->device));
+    unsigned long long v = 0;
+    HIP_TRY(hipMemcpy(&v, s->ds.nan_total, sizeof v, hipMemcpyDeviceToHost));
+    *count = (int64_t)v;
+    return MI_OK;
+}
+
+}  // extern "C"

@@ -1,0 +1,227 @@
+"""Scene pieces the reference takes from closed Isaac Sim packages, rebuilt over libmi_sim.so:
+
+* :class:`GridCloner` — env-origin grid of omni.isaac.cloner (used at tasks/base/rl_task.py:92,
+  124-126). Restated from its public behaviour; the closed source is absent, so the exact
+  layout is unverified.
+* :class:`ArticulationView` — the omni.isaac.core tensor API the tasks call
+  (get_world_poses / get_velocities / get_joint_positions / get_joint_velocities /
+  set_* with indices / get_dof_limits / get_dof_index / _physics_view.get_force_sensor_forces,
+  call sites tasks/shared/locomotion.py:81-89,114,130-134, tasks/cartpole.py:81-82,112,
+  129-130,137-138). Every getter and setter is one HIP gather / scatter kernel on torch's
+  current stream; the physics state itself never leaves HBM.
+* :func:`Humanoid` / :func:`Ant` / :func:`Cartpole` — robot constructors
+  (robots/articulations/{humanoid,ant,cartpole}.py) returning compiled model descriptions.
+"""
+from __future__ import annotations
+
+import ctypes as C
+from typing import Optional
+
+import numpy as np
+import torch
+
+from .. import native as N
+from .model import CompiledModel, load_robot
+
+
+class GridCloner:
+    def __init__(self, spacing: float, num_per_row: int = -1):
+        self._spacing = float(spacing)
+        self._num_per_row = num_per_row
+
+    def get_clone_positions(self, num_clones: int, first: int = 0, count: Optional[int] = None) -> np.ndarray:
+        """[count, 3] origins of envs first..first+count-1 of a num_clones grid."""
+        count = num_clones - first if count is None else count
+        per_row = self._num_per_row if self._num_per_row > 0 else int(np.sqrt(num_clones))
+        num_rows = np.ceil(num_clones / per_row)
+        num_cols = np.ceil(num_clones / num_rows)
+        row_offset = 0.5 * self._spacing * (num_rows - 1)
+        col_offset = 0.5 * self._spacing * (num_cols - 1)
+        i = np.arange(first, first + count, dtype=np.float64)
+        row = np.floor(i / num_cols)
+        col = i - row * num_cols
+        x = row_offset - row * self._spacing
+        y = col * self._spacing - col_offset
+        return np.stack([x, y, np.zeros_like(x)], axis=1).astype(np.float32)
+
+
+def Humanoid() -> CompiledModel:
+    return load_robot("Humanoid")
+
+
+def Ant() -> CompiledModel:
+    return load_robot("Ant")
+
+
+def Cartpole() -> CompiledModel:
+    return load_robot("Cartpole")
+
+
+class _PhysicsView:
+    """``ArticulationView._physics_view`` (omni.physics.tensors) — force sensors only."""
+
+    def __init__(self, view: "ArticulationView"):
+        self._view = view
+
+    def get_force_sensor_forces(self) -> torch.Tensor:
+        v = self._view
+        out = torch.empty((v.count, v.num_sensors, 6), dtype=torch.float32, device=v.device)
+        if v.num_sensors:
+            N.check(N.lib().mi_get_sensor_wrench(v.handle, out.data_ptr(), v.stream()),
+                    "mi_get_sensor_wrench")
+        return out
+
+
+class ArticulationView:
+    """One articulation replicated over ``count`` envs, backed by one mi_sim handle."""
+
+    def __init__(self, model: CompiledModel, name: str = "view", prim_paths_expr: str = "",
+                 reset_xform_properties: bool = False):
+        self.model = model
+        self.name = name
+        self.prim_paths_expr = prim_paths_expr
+        self.handle = None
+        self.count = 0
+        self.device = None
+        self._desc = None
+        self._physics_view = _PhysicsView(self)
+
+    # ---- lifecycle (called by Scene.add / World) ----
+    def initialize(self, sim_params: "N.MiSimParams", num_envs: int, env_origins: np.ndarray,
+                   device: str, seed: int, env_id_offset: int = 0) -> None:
+        dev = torch.device(device)
+        if dev.type != "cuda":
+            raise N.NativeUnavailable(
+                f"sim_device={device!r}: libmi_sim.so runs on the GPU only (no CPU fallback)")
+        lib = N.lib()
+        self.device = dev
+        self.count = int(num_envs)
+        self.sim_params = sim_params
+        self._desc = self.model.to_desc()
+        origins = np.ascontiguousarray(env_origins, dtype=np.float32).reshape(self.count, 3)
+        h = C.c_void_p()
+        dev_index = dev.index if dev.index is not None else torch.cuda.current_device()
+        N.check(lib.mi_sim_create(self._desc.ref(), C.byref(sim_params), self.count,
+                                  int(env_id_offset), int(dev_index),
+                                  origins.ctypes.data, int(seed), C.byref(h)), "mi_sim_create")
+        self.handle = h.value
+        self.env_origins = origins
+
+    def close(self) -> None:
+        if self.handle:
+            N.lib().mi_sim_destroy(self.handle)
+            self.handle = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def stream(self) -> int:
+        return torch.cuda.current_stream(self.device).cuda_stream
+
+    # ---- sizes ----
+    @property
+    def num_dof(self) -> int:
+        return self.model.num_dof
+
+    @property
+    def num_sensors(self) -> int:
+        return self.model.num_sensors
+
+    @property
+    def dof_names(self):
+        return list(self.model.dof_names)
+
+    def get_dof_index(self, name: str) -> int:
+        return self.model.get_dof_index(name)
+
+    def get_dof_limits(self) -> torch.Tensor:
+        lim = torch.from_numpy(self.model.dof_limits())
+        return lim.unsqueeze(0).repeat(self.count, 1, 1).to(self.device)
+
+    # ---- getters ----
+    def _empty(self, *shape) -> torch.Tensor:
+        return torch.empty(shape, dtype=torch.float32, device=self.device)
+
+    def get_world_poses(self, indices=None, clone: bool = True):
+        pos, rot = self._empty(self.count, 3), self._empty(self.count, 4)
+        N.check(N.lib().mi_get_root_state(self.handle, pos.data_ptr(), rot.data_ptr(), None,
+                                          self.stream()), "mi_get_root_state")
+        if indices is not None:
+            return pos[indices.long()], rot[indices.long()]
+        return pos, rot
+
+    def get_velocities(self, indices=None, clone: bool = True) -> torch.Tensor:
+        vel = self._empty(self.count, 6)
+        N.check(N.lib().mi_get_root_state(self.handle, None, None, vel.data_ptr(), self.stream()),
+                "mi_get_root_state")
+        return vel if indices is None else vel[indices.long()]
+
+    def get_joint_positions(self, indices=None, clone: bool = True) -> torch.Tensor:
+        q = self._empty(self.count, self.num_dof)
+        N.check(N.lib().mi_get_dof_state(self.handle, q.data_ptr(), None, self.stream()),
+                "mi_get_dof_state")
+        return q if indices is None else q[indices.long()]
+
+    def get_joint_velocities(self, indices=None, clone: bool = True) -> torch.Tensor:
+        qd = self._empty(self.count, self.num_dof)
+        N.check(N.lib().mi_get_dof_state(self.handle, None, qd.data_ptr(), self.stream()),
+                "mi_get_dof_state")
+        return qd if indices is None else qd[indices.long()]
+
+    # ---- setters (indices: env ids, rows of the value tensors align with them) ----
+    @staticmethod
+    def _f32(t: Optional[torch.Tensor]) -> Optional[torch.Tensor]:
+        return None if t is None else t.to(torch.float32).contiguous()
+
+    def _idx64(self, indices) -> (Optional[torch.Tensor], int):
+        if indices is None:
+            return None, self.count
+        idx = torch.as_tensor(indices, device=self.device).to(torch.int64).contiguous()
+        return idx, int(idx.numel())
+
+    def set_joint_efforts(self, efforts: torch.Tensor, indices=None) -> None:
+        e = self._f32(efforts)
+        if indices is None:
+            idx, n = None, self.count
+        else:
+            idx = torch.as_tensor(indices, device=self.device).to(torch.int32).contiguous()
+            n = int(idx.numel())
+        N.check(N.lib().mi_set_dof_efforts(self.handle, e.data_ptr(),
+                                           None if idx is None else idx.data_ptr(), n,
+                                           self.stream()), "mi_set_dof_efforts")
+
+    def set_joint_positions(self, positions: torch.Tensor, indices=None) -> None:
+        q = self._f32(positions)
+        idx, n = self._idx64(indices)
+        N.check(N.lib().mi_set_dof_state(self.handle, q.data_ptr(), None, N.ptr(idx), n,
+                                         self.stream()), "mi_set_dof_state")
+
+    def set_joint_velocities(self, velocities: torch.Tensor, indices=None) -> None:
+        qd = self._f32(velocities)
+        idx, n = self._idx64(indices)
+        N.check(N.lib().mi_set_dof_state(self.handle, None, qd.data_ptr(), N.ptr(idx), n,
+                                         self.stream()), "mi_set_dof_state")
+
+    def set_world_poses(self, positions=None, orientations=None, indices=None) -> None:
+        p, r = self._f32(positions), self._f32(orientations)
+        idx, n = self._idx64(indices)
+        N.check(N.lib().mi_set_root_state(self.handle, N.ptr(p), N.ptr(r), None, N.ptr(idx), n,
+                                          self.stream()), "mi_set_root_state")
+
+    def set_velocities(self, velocities: torch.Tensor, indices=None) -> None:
+        v = self._f32(velocities)
+        idx, n = self._idx64(indices)
+        N.check(N.lib().mi_set_root_state(self.handle, None, None, v.data_ptr(), N.ptr(idx), n,
+                                          self.stream()), "mi_set_root_state")
+
+    # ---- physics ----
+    def sim_step(self, substeps: int = 1) -> None:
+        N.check(N.lib().mi_sim_step(self.handle, int(substeps), self.stream()), "mi_sim_step")
+
+    def nan_count(self) -> int:
+        c = C.c_int64()
+        N.check(N.lib().mi_sim_nan_count(self.handle, C.byref(c)), "mi_sim_nan_count")
+        return int(c.value)

@@ -1,0 +1,1197 @@
+/*
+ * oracle.c — TEST INFRASTRUCTURE ONLY (see oracle.h for the pinning status).
+ *
+ * A plain-C CPU restatement of the hot path that libmi_sim.so implements on gfx950:
+ *   - task layer: tasks/shared/locomotion.py:80-321, tasks/humanoid.py:116-127,
+ *     tasks/ant.py:88-95, tasks/cartpole.py:80-162, tasks/base/rl_task.py:231-251,
+ *     envs/vec_env_rlgames.py:41-89, with the closed omni.isaac.core.utils.torch helpers
+ *     restated from their public IsaacGym-lineage definitions (wxyz quaternions).
+ *   - physics: the build's articulated integrator (PhysX is closed): floating/fixed-base
+ *     tree of 1-DOF links, spatial algebra about the root origin with world axes,
+ *     mass matrix as sum over links of J^T I J (dense), bias by per-link Newton-Euler,
+ *     dense Cholesky, ground contacts + joint limits solved by projected Gauss-Seidel,
+ *     semi-implicit Euler. Independent of the device's tree CRBA / LTDL code.
+ * OpenMP parallelises over envs (the cpu_baseline leg of bench.py).
+ */
+#include "oracle.h"
+#include <math.h>
+#include <stdlib.h>
+#include <string.h>
+#ifdef _OPENMP
+#include <omp.h>
+#endif
+
+#define ORC_PI 3.14159265358979323846
+
+/* ------------------------------------------------------------------------------------ */
+/* Philox4x32-10 (Salmon et al., SC'11; Random123 reference constants)                   */
+/* ------------------------------------------------------------------------------------ */
+void orc_philox4x32_10(const uint32_t ctr[4], const uint32_t key[2], uint32_t out[4]) {
+    uint32_t c0 = ctr[0], c1 = ctr[1], c2 = ctr[2], c3 = ctr[3];
+    uint32_t k0 = key[0], k1 = key[1];
+    for (int r = 0; r < 10; ++r) {
+        if (r) { k0 += 0x9E3779B9u; k1 += 0xBB67AE85u; }
+        uint64_t p0 = (uint64_t)0xD2511F53u * c0;
+        uint64_t p1 = (uint64_t)0xCD9E8D57u * c2;
+        uint32_t n0 = (uint32_t)(p1 >> 32) ^ c1 ^ k0;
+        uint32_t n2 = (uint32_t)(p0 >> 32) ^ c3 ^ k1;
+        c1 = (uint32_t)p1; c3 = (uint32_t)p0; c0 = n0; c2 = n2;
+    }
+    out[0] = c0; out[1] = c1; out[2] = c2; out[3] = c3;
+}
+
+/* One U[0,1) float from the build's counter-based stream:
+ * key = seed, counter = {slot/4, counter_hi, env_lo, env_hi ^ (stream << 28)}. */
+float orc_uniform(uint64_t seed, uint64_t env_id, uint32_t counter_hi, uint32_t slot,
+                  uint32_t stream) {
+    uint32_t ctr[4] = {slot >> 2, counter_hi, (uint32_t)env_id,
+                       (uint32_t)(env_id >> 32) ^ (stream << 28)};
+    uint32_t key[2] = {(uint32_t)seed, (uint32_t)(seed >> 32)};
+    uint32_t o[4];
+    orc_philox4x32_10(ctr, key, o);
+    return (float)(o[slot & 3] >> 8) * (1.0f / 16777216.0f);
+}
+
+/* ------------------------------------------------------------------------------------ */
+/* omni.isaac.core.utils.torch helpers, restated (wxyz). Closed dependency: unverified.  */
+/* ------------------------------------------------------------------------------------ */
+/* quat_mul: the 8-multiply form of the IsaacGym-lineage torch_utils */
+static void ref_quat_mul(const float* a, const float* b, float* o) {
+    float w1 = a[0], x1 = a[1], y1 = a[2], z1 = a[3];
+    float w2 = b[0], x2 = b[1], y2 = b[2], z2 = b[3];
+    float ww = (z1 + x1) * (x2 + y2);
+    float yy = (w1 - y1) * (w2 + z2);
+    float zz = (w1 + y1) * (w2 - z2);
+    float xx = ww + yy + zz;
+    float qq = 0.5f * (xx + (z1 - x1) * (x2 - y2));
+    o[0] = qq - ww + (z1 - y1) * (y2 - z2);
+    o[1] = qq - xx + (x1 + w1) * (x2 + w2);
+    o[2] = qq - yy + (w1 - x1) * (y2 + z2);
+    o[3] = qq - zz + (z1 + y1) * (w2 - x2);
+}
+/* quat_rotate / quat_rotate_inverse: a = v(2w^2-1), b = (qv x v) w 2, c = qv (qv.v) 2 */
+static void ref_quat_rotate(const float* q, const float* v, float* o, int inverse) {
+    float w = q[0], x = q[1], y = q[2], z = q[3];
+    float s = 2.0f * (w * w) - 1.0f;
+    float cx = y * v[2] - z * v[1], cy = z * v[0] - x * v[2], cz = x * v[1] - y * v[0];
+    float d = x * v[0] + y * v[1] + z * v[2];
+    float bx = cx * w * 2.0f, by = cy * w * 2.0f, bz = cz * w * 2.0f;
+    float ccx = x * d * 2.0f, ccy = y * d * 2.0f, ccz = z * d * 2.0f;
+    if (inverse) {
+        o[0] = v[0] * s - bx + ccx; o[1] = v[1] * s - by + ccy; o[2] = v[2] * s - bz + ccz;
+    } else {
+        o[0] = v[0] * s + bx + ccx; o[1] = v[1] * s + by + ccy; o[2] = v[2] * s + bz + ccz;
+    }
+}
+/* torch float remainder (sign of divisor) */
+static float ref_fmod_pos(float a, float b) {
+    float r = fmodf(a, b);
+    if (r != 0.0f && ((r < 0.0f) != (b < 0.0f))) r += b;
+    return r;
+}
+/* get_euler_xyz: returns roll, pitch, yaw each % 2pi */
+static void ref_get_euler_xyz(const float* q, float* roll, float* pitch, float* yaw) {
+    const float two_pi = (float)(2.0 * ORC_PI);
+    float w = q[0], x = q[1], y = q[2], z = q[3];
+    float sinr = 2.0f * (w * x + y * z);
+    float cosr = w * w - x * x - y * y + z * z;
+    float r = atan2f(sinr, cosr);
+    float sinp = 2.0f * (w * y - z * x);
+    float p = fabsf(sinp) >= 1.0f ? copysignf((float)(ORC_PI / 2.0), sinp) : asinf(sinp);
+    float siny = 2.0f * (w * z + x * y);
+    float cosy = w * w + x * x - y * y - z * z;
+    float yw = atan2f(siny, cosy);
+    *roll = ref_fmod_pos(r, two_pi);
+    *pitch = ref_fmod_pos(p, two_pi);
+    *yaw = ref_fmod_pos(yw, two_pi);
+}
+/* locomotion.py:190-192 */
+static float ref_normalize_angle(float x) { return atan2f(sinf(x), cosf(x)); }
+/* unscale(x, lower, upper) = (2x - upper - lower) / (upper - lower) */
+static float ref_unscale(float x, float l, float u) { return (2.0f * x - u - l) / (u - l); }
+
+/* ------------------------------------------------------------------------------------ */
+/* small linear algebra                                                                  */
+/* ------------------------------------------------------------------------------------ */
+static void m3_from_quat(const float* q, float* R) {
+    float w = q[0], x = q[1], y = q[2], z = q[3];
+    R[0] = 1 - 2 * (y * y + z * z); R[1] = 2 * (x * y - w * z); R[2] = 2 * (x * z + w * y);
+    R[3] = 2 * (x * y + w * z); R[4] = 1 - 2 * (x * x + z * z); R[5] = 2 * (y * z - w * x);
+    R[6] = 2 * (x * z - w * y); R[7] = 2 * (y * z + w * x); R[8] = 1 - 2 * (x * x + y * y);
+}
+static void m3_mul(const float* A, const float* B, float* C) {
+    float T[9];
+    for (int i = 0; i < 3; ++i)
+        for (int j = 0; j < 3; ++j)
+            T[3 * i + j] = A[3 * i] * B[j] + A[3 * i + 1] * B[3 + j] + A[3 * i + 2] * B[6 + j];
+    memcpy(C, T, sizeof T);
+}
+static void m3_vec(const float* A, const float* v, float* o) {
+    float t0 = A[0] * v[0] + A[1] * v[1] + A[2] * v[2];
+    float t1 = A[3] * v[0] + A[4] * v[1] + A[5] * v[2];
+    float t2 = A[6] * v[0] + A[7] * v[1] + A[8] * v[2];
+    o[0] = t0; o[1] = t1; o[2] = t2;
+}
+static void m3_tvec(const float* A, const float* v, float* o) {
+    float t0 = A[0] * v[0] + A[3] * v[1] + A[6] * v[2];
+    float t1 = A[1] * v[0] + A[4] * v[1] + A[7] * v[2];
+    float t2 = A[2] * v[0] + A[5] * v[1] + A[8] * v[2];
+    o[0] = t0; o[1] = t1; o[2] = t2;
+}
+/* rotation by angle t about unit axis a (Rodrigues) */
+static void m3_axis_angle(const float* a, float t, float* R) {
+    float c = cosf(t), s = sinf(t), C = 1.0f - c;
+    float x = a[0], y = a[1], z = a[2];
+    R[0] = c + x * x * C;     R[1] = x * y * C - z * s; R[2] = x * z * C + y * s;
+    R[3] = y * x * C + z * s; R[4] = c + y * y * C;     R[5] = y * z * C - x * s;
+    R[6] = z * x * C - y * s; R[7] = z * y * C + x * s; R[8] = c + z * z * C;
+}
+static void cross3(const float* a, const float* b, float* o) {
+    float t0 = a[1] * b[2] - a[2] * b[1], t1 = a[2] * b[0] - a[0] * b[2],
+          t2 = a[0] * b[1] - a[1] * b[0];
+    o[0] = t0; o[1] = t1; o[2] = t2;
+}
+static float dot3(const float* a, const float* b) { return a[0] * b[0] + a[1] * b[1] + a[2] * b[2]; }
+static float dot6(const float* a, const float* b) {
+    return a[0] * b[0] + a[1] * b[1] + a[2] * b[2] + a[3] * b[3] + a[4] * b[4] + a[5] * b[5];
+}
+/* spatial motion cross: [w;v] x [a;b] = [w x a; w x b + v x a] */
+static void crm(const float* V, const float* s, float* o) {
+    float t[6], u[3];
+    cross3(V, s, t);
+    cross3(V, s + 3, t + 3);
+    cross3(V + 3, s, u);
+    t[3] += u[0]; t[4] += u[1]; t[5] += u[2];
+    memcpy(o, t, sizeof t);
+}
+/* spatial force cross: [w;v] x* [n;f] = [w x n + v x f; w x f] */
+static void crf(const float* V, const float* f, float* o) {
+    float t[6], u[3];
+    cross3(V, f, t);
+    cross3(V + 3, f + 3, u);
+    t[0] += u[0]; t[1] += u[1]; t[2] += u[2];
+    cross3(V, f + 3, t + 3);
+    memcpy(o, t, sizeof t);
+}
+static void m6_vec(const float* A, const float* v, float* o) {
+    float t[6];
+    for (int i = 0; i < 6; ++i) {
+        float acc = 0.0f;
+        for (int j = 0; j < 6; ++j) acc += A[6 * i + j] * v[j];
+        t[i] = acc;
+    }
+    memcpy(o, t, sizeof t);
+}
+
+/* ------------------------------------------------------------------------------------ */
+/* model + sim                                                                           */
+/* ------------------------------------------------------------------------------------ */
+typedef struct {
+    int dyn, root_free, L, G, S, P, D, nv, nr, npts, max_rows;
+    int *parent, *jtype, *geom_link, *geom_type, *sensor_link, *pairs;
+    float *axis, *pos, *quat, *mass, *com, *inertia, *lower, *upper, *damping, *armature;
+    float *geom_p0, *geom_p1, *geom_radius, *sensor_pos;
+    int *pt_geom, *pt_end; /* contact candidate points */
+    float cart_mass, pole_mass, pole_com, pole_inertia, cart_damping, pole_damping;
+} model_t;
+
+struct orc_sim {
+    model_t m;
+    mi_sim_params p;
+    mi_task_params tp;
+    int task_ok;
+    float gears[64], ratio[64], init_dof[64];
+    int N;
+    int64_t off;
+    uint64_t seed;
+    float *origins, *root_pos, *root_quat, *root_vel, *q, *qd, *eff, *sens;
+    uint32_t* reset_count;
+    int32_t* nan_flag;
+    int64_t nan_total;
+};
+
+static int g_threads = 1;
+void orc_set_threads(int n) { g_threads = n > 0 ? n : 1; }
+
+static void* dupmem(const void* src, size_t bytes) {
+    if (!bytes) return NULL;
+    void* d = malloc(bytes);
+    if (src) memcpy(d, src, bytes); else memset(d, 0, bytes);
+    return d;
+}
+
+orc_sim* orc_sim_create(const mi_model_desc* md, const mi_sim_params* params, int32_t N,
+                        int64_t off, const float* origins, uint64_t seed) {
+    orc_sim* s = (orc_sim*)calloc(1, sizeof(orc_sim));
+    model_t* m = &s->m;
+    m->dyn = md->dyn_kind;
+    m->root_free = md->root_free;
+    m->L = md->num_links; m->G = md->num_geoms; m->S = md->num_sensors; m->P = md->num_pairs;
+    m->D = m->L - 1;
+    m->nr = m->root_free ? 6 : 0;
+    m->nv = m->nr + m->D;
+    int L = m->L, G = m->G;
+    m->parent = (int*)dupmem(md->parent, L * 4);
+    m->jtype = (int*)dupmem(md->jtype, L * 4);
+    m->axis = (float*)dupmem(md->axis, L * 12);
+    m->pos = (float*)dupmem(md->pos, L * 12);
+    m->quat = (float*)dupmem(md->quat, L * 16);
+    m->mass = (float*)dupmem(md->mass, L * 4);
+    m->com = (float*)dupmem(md->com, L * 12);
+    m->inertia = (float*)dupmem(md->inertia, L * 24);
+    m->lower = (float*)dupmem(md->lower, L * 4);
+    m->upper = (float*)dupmem(md->upper, L * 4);
+    m->damping = (float*)dupmem(md->damping, L * 4);
+    m->armature = (float*)dupmem(md->armature, L * 4);
+    m->geom_link = (int*)dupmem(md->geom_link, G * 4);
+    m->geom_type = (int*)dupmem(md->geom_type, G * 4);
+    m->geom_p0 = (float*)dupmem(md->geom_p0, G * 12);
+    m->geom_p1 = (float*)dupmem(md->geom_p1, G * 12);
+    m->geom_radius = (float*)dupmem(md->geom_radius, G * 4);
+    m->sensor_link = (int*)dupmem(md->sensor_link, m->S * 4);
+    m->sensor_pos = (float*)dupmem(md->sensor_pos, m->S * 12);
+    m->pairs = (int*)dupmem(md->pairs, m->P * 8);
+    m->cart_mass = md->cart_mass; m->pole_mass = md->pole_mass; m->pole_com = md->pole_com;
+    m->pole_inertia = md->pole_inertia; m->cart_damping = md->cart_damping;
+    m->pole_damping = md->pole_damping;
+    m->npts = 0;
+    for (int g = 0; g < G; ++g) m->npts += m->geom_type[g] == MI_GEOM_CAPSULE ? 2 : 1;
+    m->pt_geom = (int*)malloc((m->npts + 1) * 4);
+    m->pt_end = (int*)malloc((m->npts + 1) * 4);
+    int k = 0;
+    for (int g = 0; g < G; ++g) {
+        m->pt_geom[k] = g; m->pt_end[k++] = 0;
+        if (m->geom_type[g] == MI_GEOM_CAPSULE) { m->pt_geom[k] = g; m->pt_end[k++] = 1; }
+    }
+    m->max_rows = 3 * m->npts + m->D;
+    s->p = *params;
+    s->N = N; s->off = off; s->seed = seed;
+    int D = m->D > 0 ? m->D : 1, S = m->S > 0 ? m->S : 1;
+    s->origins = (float*)dupmem(origins, (size_t)N * 12);
+    s->root_pos = (float*)dupmem(NULL, (size_t)N * 12);
+    s->root_quat = (float*)dupmem(NULL, (size_t)N * 16);
+    s->root_vel = (float*)dupmem(NULL, (size_t)N * 24);
+    s->q = (float*)dupmem(NULL, (size_t)N * D * 4);
+    s->qd = (float*)dupmem(NULL, (size_t)N * D * 4);
+    s->eff = (float*)dupmem(NULL, (size_t)N * D * 4);
+    s->sens = (float*)dupmem(NULL, (size_t)N * S * 24);
+    s->reset_count = (uint32_t*)dupmem(NULL, (size_t)N * 4);
+    s->nan_flag = (int32_t*)dupmem(NULL, (size_t)N * 4);
+    for (int i = 0; i < N; ++i) {
+        s->root_quat[4 * i] = 1.0f;
+        for (int c = 0; c < 3; ++c) s->root_pos[3 * i + c] = s->origins[3 * i + c];
+    }
+    return s;
+}
+
+void orc_sim_destroy(orc_sim* s) {
+    if (!s) return;
+    model_t* m = &s->m;
+    void* ptrs[] = {m->parent, m->jtype, m->axis, m->pos, m->quat, m->mass, m->com, m->inertia,
+                    m->lower, m->upper, m->damping, m->armature, m->geom_link, m->geom_type,
+                    m->geom_p0, m->geom_p1, m->geom_radius, m->sensor_link, m->sensor_pos,
+                    m->pairs, m->pt_geom, m->pt_end, s->origins, s->root_pos, s->root_quat,
+                    s->root_vel, s->q, s->qd, s->eff, s->sens, s->reset_count, s->nan_flag};
+    for (size_t i = 0; i < sizeof ptrs / sizeof ptrs[0]; ++i) free(ptrs[i]);
+    free(s);
+}
+int orc_sim_num_dof(const orc_sim* s) { return s->m.D; }
+
+void orc_get_root_state(const orc_sim* s, float* pos, float* quat, float* vel) {
+    if (pos) memcpy(pos, s->root_pos, (size_t)s->N * 12);
+    if (quat) memcpy(quat, s->root_quat, (size_t)s->N * 16);
+    if (vel) memcpy(vel, s->root_vel, (size_t)s->N * 24);
+}
+void orc_get_dof_state(const orc_sim* s, float* q, float* qd) {
+    if (q) memcpy(q, s->q, (size_t)s->N * s->m.D * 4);
+    if (qd) memcpy(qd, s->qd, (size_t)s->N * s->m.D * 4);
+}
+void orc_get_sensor_wrench(const orc_sim* s, float* out) {
+    memcpy(out, s->sens, (size_t)s->N * s->m.S * 24);
+}
+void orc_set_root_state(orc_sim* s, const float* pos, const float* quat, const float* vel) {
+    if (pos) memcpy(s->root_pos, pos, (size_t)s->N * 12);
+    if (quat) memcpy(s->root_quat, quat, (size_t)s->N * 16);
+    if (vel) memcpy(s->root_vel, vel, (size_t)s->N * 24);
+}
+void orc_set_dof_state(orc_sim* s, const float* q, const float* qd) {
+    if (q) memcpy(s->q, q, (size_t)s->N * s->m.D * 4);
+    if (qd) memcpy(s->qd, qd, (size_t)s->N * s->m.D * 4);
+}
+void orc_set_dof_efforts(orc_sim* s, const float* eff) {
+    memcpy(s->eff, eff, (size_t)s->N * s->m.D * 4);
+}
+void orc_get_reset_count(const orc_sim* s, uint32_t* out) {
+    memcpy(out, s->reset_count, (size_t)s->N * 4);
+}
+void orc_set_reset_count(orc_sim* s, const uint32_t* in) {
+    memcpy(s->reset_count, in, (size_t)s->N * 4);
+}
+int64_t orc_nan_count(const orc_sim* s) { return s->nan_total; }
+
+/* ------------------------------------------------------------------------------------ */
+/* analytic cart-pole (prismatic cart along x, hinge pole about y, theta=0 upright)      */
+/* ------------------------------------------------------------------------------------ */
+static void cartpole_substep(const model_t* m, const mi_sim_params* p, float* q, float* qd,
+                             const float* eff) {
+    const float mc = m->cart_mass, mp = m->pole_mass, l = m->pole_com, Ip = m->pole_inertia;
+    const float g = -p->gravity[2], dt = p->dt;
+    float x = q[0], th = q[1], xd = qd[0], thd = qd[1];
+    float s = sinf(th), c = cosf(th);
+    float m11 = mc + mp, m12 = mp * l * c, m22 = Ip + mp * l * l;
+    float r1 = eff[0] + mp * l * s * thd * thd - m->cart_damping * xd;
+    float r2 = eff[1] + mp * g * l * s - m->pole_damping * thd;
+    float det = m11 * m22 - m12 * m12;
+    float xdd = (m22 * r1 - m12 * r2) / det;
+    float thdd = (m11 * r2 - m12 * r1) / det;
+    xd = xd + dt * xdd;
+    thd = thd + dt * thdd;
+    q[0] = x + dt * xd;
+    q[1] = th + dt * thd;
+    qd[0] = xd;
+    qd[1] = thd;
+}
+
+/* ------------------------------------------------------------------------------------ */
+/* articulated physics — per-env workspace                                               */
+/* ------------------------------------------------------------------------------------ */
+typedef struct {
+    float *R, *o, *aw, *I6, *S, *V, *A, *J, *M, *Gc, *C, *u, *rhs, *ud;
+    float *Jr, *W, *b, *lam, *Ad, *cpt;
+    int *rkind, *rcon, *clink;
+    int nrows, ncon;
+} ws_t;
+
+static ws_t* ws_new(const model_t* m) {
+    ws_t* w = (ws_t*)calloc(1, sizeof(ws_t));
+    int L = m->L, nv = m->nv, R = m->max_rows > 0 ? m->max_rows : 1;
+    w->R = (float*)calloc(L * 9, 4); w->o = (float*)calloc(L * 3, 4);
+    w->aw = (float*)calloc(L * 3, 4); w->I6 = (float*)calloc(L * 36, 4);
+    w->S = (float*)calloc(nv * 6 + 6, 4); w->V = (float*)calloc(L * 6, 4);
+    w->A = (float*)calloc(L * 6, 4); w->J = (float*)calloc((size_t)L * 6 * nv + 1, 4);
+    w->M = (float*)calloc(nv * nv + 1, 4); w->Gc = (float*)calloc(nv * nv + 1, 4);
+    w->C = (float*)calloc(nv + 1, 4); w->u = (float*)calloc(nv + 1, 4);
+    w->rhs = (float*)calloc(nv + 1, 4); w->ud = (float*)calloc(nv + 1, 4);
+    w->Jr = (float*)calloc((size_t)R * nv + 1, 4); w->W = (float*)calloc((size_t)R * nv + 1, 4);
+    w->b = (float*)calloc(R, 4); w->lam = (float*)calloc(R, 4); w->Ad = (float*)calloc(R, 4);
+    w->rkind = (int*)calloc(R, 4); w->rcon = (int*)calloc(R, 4);
+    w->cpt = (float*)calloc(m->npts * 3 + 3, 4); w->clink = (int*)calloc(m->npts + 1, 4);
+    return w;
+}
+static void ws_free(ws_t* w) {
+    void* p[] = {w->R, w->o, w->aw, w->I6, w->S, w->V, w->A, w->J, w->M, w->Gc, w->C, w->u,
+                 w->rhs, w->ud, w->Jr, w->W, w->b, w->lam, w->Ad, w->rkind, w->rcon, w->cpt,
+                 w->clink};
+    for (size_t i = 0; i < sizeof p / sizeof p[0]; ++i) free(p[i]);
+    free(w);
+}
+
+/* dof index of link l (l>=1) */
+static int link_dof(const model_t* m, int l) { return m->nr + l - 1; }
+
+/* forward kinematics + spatial quantities about p0 = root origin (world axes) */
+static void kinematics(const model_t* m, ws_t* w, const float* rq, const float* q, const float* u) {
+    int L = m->L, nv = m->nv, nr = m->nr;
+    float* R = w->R; float* o = w->o;
+    m3_from_quat(rq, R);
+    o[0] = o[1] = o[2] = 0.0f;
+    for (int l = 1; l < L; ++l) {
+        int P = m->parent[l];
+        float Rq[9], Rj[9], a[3], op[3];
+        m3_from_quat(m->quat + 4 * l, Rq);
+        m3_mul(R + 9 * P, Rq, Rj);
+        m3_vec(Rj, m->axis + 3 * l, a);
+        m3_vec(R + 9 * P, m->pos + 3 * l, op);
+        float qj = q[l - 1];
+        if (m->jtype[l] == MI_JOINT_HINGE) {
+            float Ra[9];
+            m3_axis_angle(m->axis + 3 * l, qj, Ra);
+            m3_mul(Rj, Ra, R + 9 * l);
+            for (int c = 0; c < 3; ++c) o[3 * l + c] = o[3 * P + c] + op[c];
+        } else {
+            memcpy(R + 9 * l, Rj, 36);
+            for (int c = 0; c < 3; ++c) o[3 * l + c] = o[3 * P + c] + op[c] + a[c] * qj;
+        }
+        memcpy(w->aw + 3 * l, a, 12);
+    }
+    /* spatial inertia about p0, [ang; lin] ordering */
+    for (int l = 0; l < L; ++l) {
+        float* I = w->I6 + 36 * l;
+        memset(I, 0, 144);
+        float mass = m->mass[l];
+        if (mass <= 0.0f) continue;
+        float c[3], Ic[9], T[9], Rl[9];
+        memcpy(Rl, R + 9 * l, 36);
+        m3_vec(Rl, m->com + 3 * l, c);
+        for (int k = 0; k < 3; ++k) c[k] += o[3 * l + k];
+        const float* in = m->inertia + 6 * l;
+        float Ib[9] = {in[0], in[3], in[4], in[3], in[1], in[5], in[4], in[5], in[2]};
+        m3_mul(Rl, Ib, T);
+        float Rt[9] = {Rl[0], Rl[3], Rl[6], Rl[1], Rl[4], Rl[7], Rl[2], Rl[5], Rl[8]};
+        m3_mul(T, Rt, Ic);
+        /* Ibar = Ic + m (|c|^2 1 - c c^T) ; [c]x[c]x^T = |c|^2 1 - c c^T */
+        float cc = dot3(c, c);
+        for (int i = 0; i < 3; ++i)
+            for (int j = 0; j < 3; ++j)
+                I[6 * i + j] = Ic[3 * i + j] + mass * ((i == j ? cc : 0.0f) - c[i] * c[j]);
+        /* upper-right m[c]x ; lower-left m[c]x^T */
+        float h[3] = {mass * c[0], mass * c[1], mass * c[2]};
+        float hx[9] = {0, -h[2], h[1], h[2], 0, -h[0], -h[1], h[0], 0};
+        for (int i = 0; i < 3; ++i)
+            for (int j = 0; j < 3; ++j) {
+                I[6 * i + 3 + j] = hx[3 * i + j];
+                I[6 * (3 + i) + j] = hx[3 * j + i];
+            }
+        for (int i = 0; i < 3; ++i) I[6 * (3 + i) + 3 + i] = mass;
+    }
+    /* motion subspaces */
+    float* S = w->S;
+    memset(S, 0, nv * 24);
+    if (m->root_free) {
+        for (int k = 0; k < 3; ++k) S[6 * k + 3 + k] = 1.0f;       /* linear */
+        for (int k = 0; k < 3; ++k) S[6 * (3 + k) + k] = 1.0f;     /* angular */
+    }
+    for (int l = 1; l < L; ++l) {
+        float* s = S + 6 * link_dof(m, l);
+        const float* a = w->aw + 3 * l;
+        if (m->jtype[l] == MI_JOINT_HINGE) {
+            s[0] = a[0]; s[1] = a[1]; s[2] = a[2];
+            cross3(o + 3 * l, a, s + 3);
+        } else {
+            s[3] = a[0]; s[4] = a[1]; s[5] = a[2];
+        }
+    }
+    /* link Jacobians J_l (6 x nv, row-major [6][nv]) */
+    memset(w->J, 0, (size_t)L * 6 * nv * 4);
+    for (int l = 0; l < L; ++l) {
+        float* Jl = w->J + (size_t)6 * nv * l;
+        int x = l;
+        while (x > 0) {
+            int k = link_dof(m, x);
+            for (int r = 0; r < 6; ++r) Jl[r * nv + k] = S[6 * k + r];
+            x = m->parent[x];
+        }
+        for (int k = 0; k < nr; ++k)
+            for (int r = 0; r < 6; ++r) Jl[r * nv + k] = S[6 * k + r];
+    }
+    /* link velocities */
+    for (int l = 0; l < L; ++l) {
+        float* Jl = w->J + (size_t)6 * nv * l;
+        for (int r = 0; r < 6; ++r) {
+            float acc = 0.0f;
+            for (int k = 0; k < nv; ++k) acc += Jl[r * nv + k] * u[k];
+            w->V[6 * l + r] = acc;
+        }
+    }
+}
+
+/* dense M (J^T I J summed over links) and bias C (per-link Newton-Euler) */
+static void dynamics_terms(const model_t* m, const mi_sim_params* p, ws_t* w, const float* u) {
+    int L = m->L, nv = m->nv;
+    memset(w->M, 0, nv * nv * 4);
+    memset(w->C, 0, nv * 4);
+    for (int l = 0; l < L; ++l) {
+        if (m->mass[l] <= 0.0f) continue;
+        const float* Jl = w->J + (size_t)6 * nv * l;
+        const float* I = w->I6 + 36 * l;
+        /* velocity-product acceleration of link l incl. fictitious gravity */
+        float Al[6] = {0, 0, 0, -p->gravity[0], -p->gravity[1], -p->gravity[2]};
+        if (m->root_free) {
+            float wv[3];
+            cross3(u + 3, u, wv);
+            Al[3] -= wv[0]; Al[4] -= wv[1]; Al[5] -= wv[2];
+        }
+        int x = l;
+        while (x > 0) {
+            int k = link_dof(m, x), P = m->parent[x];
+            float sd[6];
+            crm(w->V + 6 * P, w->S + 6 * k, sd);
+            for (int r = 0; r < 6; ++r) Al[r] += sd[r] * u[k];
+            x = P;
+        }
+        float f[6], Iv[6], t[6];
+        m6_vec(I, Al, f);
+        m6_vec(I, w->V + 6 * l, Iv);
+        crf(w->V + 6 * l, Iv, t);
+        for (int r = 0; r < 6; ++r) f[r] += t[r];
+        for (int k = 0; k < nv; ++k) {
+            float acc = 0.0f;
+            for (int r = 0; r < 6; ++r) acc += Jl[r * nv + k] * f[r];
+            w->C[k] += acc;
+        }
+        /* M += J^T I J */
+        float IJ[6 * 64];
+        for (int r = 0; r < 6; ++r)
+            for (int k = 0; k < nv; ++k) {
+                float acc = 0.0f;
+                for (int c = 0; c < 6; ++c) acc += I[6 * r + c] * Jl[c * nv + k];
+                IJ[r * nv + k] = acc;
+            }
+        for (int i = 0; i < nv; ++i)
+            for (int j = 0; j < nv; ++j) {
+                float acc = 0.0f;
+                for (int r = 0; r < 6; ++r) acc += Jl[r * nv + i] * IJ[r * nv + j];
+                w->M[i * nv + j] += acc;
+            }
+    }
+    for (int l = 1; l < L; ++l) {
+        int k = link_dof(m, l);
+        w->M[k * nv + k] += m->armature[l] + p->dt * m->damping[l];
+    }
+}
+
+static void cholesky(int n, const float* A, float* G) {
+    memset(G, 0, n * n * 4);
+    for (int j = 0; j < n; ++j) {
+        float d = A[j * n + j];
+        for (int k = 0; k < j; ++k) d -= G[j * n + k] * G[j * n + k];
+        d = sqrtf(d > 1e-12f ? d : 1e-12f);
+        G[j * n + j] = d;
+        for (int i = j + 1; i < n; ++i) {
+            float v = A[i * n + j];
+            for (int k = 0; k < j; ++k) v -= G[i * n + k] * G[j * n + k];
+            G[i * n + j] = v / d;
+        }
+    }
+}
+static void chol_solve(int n, const float* G, const float* b, float* x) {
+    float y[64];
+    for (int i = 0; i < n; ++i) {
+        float v = b[i];
+        for (int k = 0; k < i; ++k) v -= G[i * n + k] * y[k];
+        y[i] = v / G[i * n + i];
+    }
+    for (int i = n - 1; i >= 0; --i) {
+        float v = y[i];
+        for (int k = i + 1; k < n; ++k) v -= G[k * n + i] * x[k];
+        x[i] = v / G[i * n + i];
+    }
+}
+
+static void spatial_to_dof_row(const model_t* m, const ws_t* w, int link, const float* f,
+                               float* row) {
+    int nv = m->nv;
+    const float* Jl = w->J + (size_t)6 * nv * link;
+    for (int k = 0; k < nv; ++k) {
+        float acc = 0.0f;
+        for (int r = 0; r < 6; ++r) acc += Jl[r * nv + k] * f[r];
+        row[k] = acc;
+    }
+}
+
+static int is_finite_state(int D, const float* rp, const float* rq, const float* rv,
+                           const float* q, const float* qd) {
+    float acc = 0.0f;
+    for (int i = 0; i < 3; ++i) acc += rp[i] * 0.0f;
+    for (int i = 0; i < 4; ++i) acc += rq[i] * 0.0f;
+    for (int i = 0; i < 6; ++i) acc += rv[i] * 0.0f;
+    for (int i = 0; i < D; ++i) acc += q[i] * 0.0f + qd[i] * 0.0f;
+    return acc == 0.0f;
+}
+
+/* one articulated substep for one env; state arrays are that env's rows */
+static void artic_substep(const model_t* m, const mi_sim_params* p, ws_t* w, float* rp, float* rq,
+                          float* rv, float* q, float* qd, const float* eff, float* sens) {
+    int nv = m->nv, nr = m->nr, D = m->D;
+    const float dt = p->dt;
+    float* u = w->u;
+    for (int k = 0; k < nr; ++k) u[k] = rv[k];
+    for (int j = 0; j < D; ++j) u[nr + j] = qd[j];
+    kinematics(m, w, rq, q, u);
+    dynamics_terms(m, p, w, u);
+    for (int k = 0; k < nr; ++k) w->rhs[k] = -w->C[k];
+    for (int j = 0; j < D; ++j)
+        w->rhs[nr + j] = eff[j] - w->C[nr + j] - m->damping[j + 1] * u[nr + j];
+    cholesky(nv, w->M, w->Gc);
+    chol_solve(nv, w->Gc, w->rhs, w->ud);
+    for (int k = 0; k < nv; ++k) u[k] = u[k] + dt * w->ud[k];
+
+    /* ---- constraint rows ---- */
+    int nrows = 0, ncon = 0;
+    for (int c = 0; c < m->npts; ++c) {
+        int g = m->pt_geom[c], l = m->geom_link[g];
+        const float* pl = m->pt_end[c] ? m->geom_p1 + 3 * g : m->geom_p0 + 3 * g;
+        float x[3];
+        m3_vec(w->R + 9 * l, pl, x);
+        for (int k = 0; k < 3; ++k) x[k] += w->o[3 * l + k];
+        float r = m->geom_radius[g];
+        float gap = rp[2] + x[2] - r;
+        if (!(gap < p->contact_offset)) continue;
+        float pc[3] = {x[0], x[1], x[2] - r};
+        float d = gap - p->rest_offset;
+        float bn = d >= 0.0f ? -d / dt : -p->erp * d / dt;
+        if (bn > p->max_depenetration_velocity) bn = p->max_depenetration_velocity;
+        memcpy(w->cpt + 3 * ncon, pc, 12);
+        w->clink[ncon] = l;
+        static const float dirs[3][3] = {{0, 0, 1}, {1, 0, 0}, {0, 1, 0}};
+        for (int t = 0; t < 3; ++t) {
+            float f[6];
+            cross3(pc, dirs[t], f);
+            f[3] = dirs[t][0]; f[4] = dirs[t][1]; f[5] = dirs[t][2];
+            spatial_to_dof_row(m, w, l, f, w->Jr + (size_t)nrows * nv);
+            w->rkind[nrows] = t;          /* 0 normal, 1/2 friction */
+            w->rcon[nrows] = nrows - t;   /* index of the contact's normal row */
+            w->b[nrows] = t == 0 ? bn : 0.0f;
+            ++nrows;
+        }
+        ++ncon;
+    }
+    for (int j = 0; j < D; ++j) {
+        int l = j + 1, k = nr + j;
+        float lo = m->lower[l], hi = m->upper[l];
+        if (!(lo < hi)) continue;
+        float qp = q[j] + dt * u[k];
+        float d, sg;
+        if (q[j] < lo || qp < lo) { d = q[j] - lo; sg = 1.0f; }
+        else if (q[j] > hi || qp > hi) { d = hi - q[j]; sg = -1.0f; }
+        else continue;
+        float* row = w->Jr + (size_t)nrows * nv;
+        memset(row, 0, nv * 4);
+        row[k] = sg;
+        float bl = d >= 0.0f ? -d / dt : -p->erp * d / dt;
+        if (bl > p->max_depenetration_velocity) bl = p->max_depenetration_velocity;
+        w->b[nrows] = bl;
+        w->rkind[nrows] = 3;
+        w->rcon[nrows] = nrows;
+        ++nrows;
+    }
+    w->nrows = nrows; w->ncon = ncon;
+    for (int r = 0; r < nrows; ++r) {
+        chol_solve(nv, w->Gc, w->Jr + (size_t)r * nv, w->W + (size_t)r * nv);
+        float a = 0.0f;
+        for (int k = 0; k < nv; ++k) a += w->Jr[(size_t)r * nv + k] * w->W[(size_t)r * nv + k];
+        w->Ad[r] = a > 1e-12f ? a : 1e-12f;
+        w->lam[r] = 0.0f;
+    }
+    /* ---- projected Gauss-Seidel ---- */
+    const float mu = p->friction;
+    for (int it = 0; it < p->solver_iterations; ++it) {
+        for (int r = 0; r < nrows; ++r) {
+            const float* Jr = w->Jr + (size_t)r * nv;
+            float jv = 0.0f;
+            for (int k = 0; k < nv; ++k) jv += Jr[k] * u[k];
+            float l0 = w->lam[r];
+            float ln = l0 + (w->b[r] - jv) / w->Ad[r];
+            if (w->rkind[r] == 1 || w->rkind[r] == 2) {
+                float lim = mu * w->lam[w->rcon[r]];
+                ln = ln > lim ? lim : (ln < -lim ? -lim : ln);
+            } else {
+                ln = ln > 0.0f ? ln : 0.0f;
+            }
+            float dl = ln - l0;
+            const float* Wr = w->W + (size_t)r * nv;
+            for (int k = 0; k < nv; ++k) u[k] += Wr[k] * dl;
+            w->lam[r] = ln;
+        }
+    }
+    /* ---- force sensors: contact wrench on the sensor link, link frame ---- */
+    for (int si = 0; si < m->S; ++si) {
+        int l = m->sensor_link[si];
+        float xs[3], F[3] = {0, 0, 0}, T[3] = {0, 0, 0};
+        m3_vec(w->R + 9 * l, m->sensor_pos + 3 * si, xs);
+        for (int k = 0; k < 3; ++k) xs[k] += w->o[3 * l + k];
+        for (int c = 0; c < ncon; ++c) {
+            if (w->clink[c] != l) continue;
+            float fn = w->lam[3 * c] / dt, f1 = w->lam[3 * c + 1] / dt, f2 = w->lam[3 * c + 2] / dt;
+            float fc[3] = {f1, f2, fn}, rr[3], tc[3];
+            for (int k = 0; k < 3; ++k) rr[k] = w->cpt[3 * c + k] - xs[k];
+            cross3(rr, fc, tc);
+            for (int k = 0; k < 3; ++k) { F[k] += fc[k]; T[k] += tc[k]; }
+        }
+        m3_tvec(w->R + 9 * l, F, sens + 6 * si);
+        m3_tvec(w->R + 9 * l, T, sens + 6 * si + 3);
+    }
+    /* ---- integrate (semi-implicit Euler) ---- */
+    if (m->root_free) {
+        float* om = u + 3;
+        float wn = sqrtf(dot3(om, om));
+        if (wn > p->max_angular_velocity) {
+            float sc = p->max_angular_velocity / wn;
+            om[0] *= sc; om[1] *= sc; om[2] *= sc;
+            wn = p->max_angular_velocity;
+        }
+        for (int k = 0; k < 3; ++k) rp[k] += dt * u[k];
+        float th = wn * dt;
+        if (th > 0.0f) {
+            float sh = sinf(0.5f * th) / wn, ch = cosf(0.5f * th);
+            float dq[4] = {ch, om[0] * sh, om[1] * sh, om[2] * sh};
+            float w0 = dq[0], x0 = dq[1], y0 = dq[2], z0 = dq[3];
+            float w1 = rq[0], x1 = rq[1], y1 = rq[2], z1 = rq[3];
+            float nq[4] = {w0 * w1 - x0 * x1 - y0 * y1 - z0 * z1,
+                           w0 * x1 + x0 * w1 + y0 * z1 - z0 * y1,
+                           w0 * y1 - x0 * z1 + y0 * w1 + z0 * x1,
+                           w0 * z1 + x0 * y1 - y0 * x1 + z0 * w1};
+            float nn = 1.0f / sqrtf(nq[0] * nq[0] + nq[1] * nq[1] + nq[2] * nq[2] + nq[3] * nq[3]);
+            for (int k = 0; k < 4; ++k) rq[k] = nq[k] * nn;
+        }
+        for (int k = 0; k < 6; ++k) rv[k] = u[k];
+    }
+    for (int j = 0; j < D; ++j) {
+        qd[j] = u[nr + j];
+        q[j] = q[j] + dt * qd[j];
+    }
+}
+
+/* reset the physics state of env i to the task's initial pose with Philox noise
+ * (locomotion.py:116-145 / cartpole.py:114-134) */
+static void task_reset_env(orc_sim* s, int i, int64_t* reset_buf, int64_t* progress_buf,
+                           float* potentials, float* prev_potentials) {
+    const model_t* m = &s->m;
+    const mi_task_params* tp = &s->tp;
+    int D = m->D;
+    uint64_t gid = (uint64_t)(s->off + i);
+    uint32_t cnt = s->reset_count[i];
+    float* q = s->q + (size_t)D * i;
+    float* qd = s->qd + (size_t)D * i;
+    if (tp->task_kind == MI_TASK_CARTPOLE) {
+        float u0 = orc_uniform(s->seed, gid, cnt, 0, 0), u1 = orc_uniform(s->seed, gid, cnt, 1, 0);
+        float u2 = orc_uniform(s->seed, gid, cnt, 2, 0), u3 = orc_uniform(s->seed, gid, cnt, 3, 0);
+        q[0] = 1.0f * (1.0f - 2.0f * u0);
+        q[1] = (float)(0.125 * ORC_PI) * (1.0f - 2.0f * u1);
+        qd[0] = 0.5f * (1.0f - 2.0f * u2);
+        qd[1] = (float)(0.25 * ORC_PI) * (1.0f - 2.0f * u3);
+    } else {
+        float pn = tp->dof_pos_noise, vn = tp->dof_vel_noise;
+        float pw = (float)((double)pn - (double)(-pn)), vw = (float)((double)vn - (double)(-vn));
+        for (int j = 0; j < D; ++j) {
+            float u = orc_uniform(s->seed, gid, cnt, (uint32_t)j, 0);
+            float v = s->init_dof[j] + (pw * u + (-pn));
+            float lo = m->lower[j + 1], hi = m->upper[j + 1];
+            if (lo < hi) { v = v < hi ? v : hi; v = v > lo ? v : lo; }
+            q[j] = v;
+        }
+        for (int j = 0; j < D; ++j) {
+            float u = orc_uniform(s->seed, gid, cnt, (uint32_t)(D + j), 0);
+            qd[j] = vw * u + (-vn);
+        }
+        float* rp = s->root_pos + 3 * i;
+        for (int k = 0; k < 3; ++k) rp[k] = s->origins[3 * i + k] + tp->init_root_pos[k];
+        memcpy(s->root_quat + 4 * i, tp->init_root_quat, 16);
+        memset(s->root_vel + 6 * i, 0, 24);
+        float tx = tp->target[0] - rp[0], ty = tp->target[1] - rp[1];
+        float pot = -sqrtf(tx * tx + ty * ty + 0.0f * 0.0f) / tp->task_dt;
+        if (prev_potentials) prev_potentials[i] = pot;
+        if (potentials) potentials[i] = pot;
+    }
+    s->reset_count[i] = cnt + 1;
+    if (reset_buf) reset_buf[i] = 0;
+    if (progress_buf) progress_buf[i] = 0;
+}
+
+static void env_physics(orc_sim* s, ws_t* w, int i, int substeps) {
+    const model_t* m = &s->m;
+    int D = m->D;
+    float* q = s->q + (size_t)D * i;
+    float* qd = s->qd + (size_t)D * i;
+    const float* eff = s->eff + (size_t)D * i;
+    for (int st = 0; st < substeps; ++st) {
+        if (m->dyn == MI_DYN_CARTPOLE)
+            cartpole_substep(m, &s->p, q, qd, eff);
+        else
+            artic_substep(m, &s->p, w, s->root_pos + 3 * i, s->root_quat + 4 * i,
+                          s->root_vel + 6 * i, q, qd, eff, s->sens + (size_t)6 * m->S * i);
+    }
+    if (!is_finite_state(D, s->root_pos + 3 * i, s->root_quat + 4 * i, s->root_vel + 6 * i, q, qd))
+        s->nan_flag[i] = 1;
+}
+
+void orc_sim_step(orc_sim* s, int substeps) {
+#pragma omp parallel num_threads(g_threads)
+    {
+        ws_t* w = ws_new(&s->m);
+#pragma omp for schedule(static)
+        for (int i = 0; i < s->N; ++i) env_physics(s, w, i, substeps);
+        ws_free(w);
+    }
+}
+
+/* ------------------------------------------------------------------------------------ */
+/* task layer                                                                            */
+/* ------------------------------------------------------------------------------------ */
+void orc_task_configure(orc_sim* s, const mi_task_params* tp) {
+    s->tp = *tp;
+    int A = tp->num_actions;
+    for (int j = 0; j < A && j < 64; ++j) {
+        s->gears[j] = tp->joint_gears ? tp->joint_gears[j] : 1.0f;
+        s->ratio[j] = tp->motor_effort_ratio ? tp->motor_effort_ratio[j] : 1.0f;
+    }
+    for (int j = 0; j < s->m.D && j < 64; ++j) s->init_dof[j] = tp->init_dof_pos ? tp->init_dof_pos[j] : 0.0f;
+    s->tp.joint_gears = NULL; s->tp.motor_effort_ratio = NULL; s->tp.init_dof_pos = NULL;
+    s->task_ok = 1;
+}
+
+static float clampf(float x, float lo, float hi) { return x < lo ? lo : (x > hi ? hi : x); }
+
+/* pre_physics_step for env i: reset if flagged, clamp actions, compute efforts */
+static void task_pre_env(orc_sim* s, int i, const float* actions, int64_t* reset_buf,
+                         int64_t* progress_buf, float* potentials, float* prev_potentials,
+                         float* actions_out, int clamp_actions) {
+    const mi_task_params* tp = &s->tp;
+    int A = tp->num_actions, D = s->m.D;
+    if (reset_buf[i] != 0) task_reset_env(s, i, reset_buf, progress_buf, potentials, prev_potentials);
+    float* eff = s->eff + (size_t)D * i;
+    if (tp->task_kind == MI_TASK_CARTPOLE) {
+        float a = actions[(size_t)A * i];
+        if (clamp_actions) a = clampf(a, -tp->clip_actions, tp->clip_actions);
+        if (actions_out) actions_out[(size_t)A * i] = a;
+        eff[0] = tp->max_push_effort * a;
+        eff[1] = 0.0f;
+    } else {
+        for (int j = 0; j < A; ++j) {
+            float a = actions[(size_t)A * i + j];
+            if (clamp_actions) a = clampf(a, -tp->clip_actions, tp->clip_actions);
+            if (actions_out) actions_out[(size_t)A * i + j] = a;
+            eff[j] = a * s->gears[j] * tp->power_scale;
+        }
+    }
+}
+
+void orc_task_pre_step(orc_sim* s, const float* actions, int64_t* reset_buf, int64_t* progress_buf,
+                       float* potentials, float* prev_potentials, float* actions_out) {
+    for (int i = 0; i < s->N; ++i)
+        task_pre_env(s, i, actions, reset_buf, progress_buf, potentials, prev_potentials,
+                     actions_out, 0);
+}
+
+void orc_task_reset_idx(orc_sim* s, const int64_t* env_ids, int n, int64_t* reset_buf,
+                        int64_t* progress_buf, float* potentials, float* prev_potentials) {
+    for (int k = 0; k < n; ++k)
+        task_reset_env(s, (int)env_ids[k], reset_buf, progress_buf, potentials, prev_potentials);
+}
+
+/* locomotion post-step for ONE env (get_observations + calculate_metrics + is_done) */
+static void loco_post_one(const mi_task_params* tp, int D, int S, const float* rp, const float* rq,
+                          const float* rv, const float* q, const float* qd, const float* sens,
+                          const float* act, const float* lower, const float* upper,
+                          const float* ratio, float* obs, float* rew, int64_t* reset,
+                          int64_t* progress, float* pot, float* prev) {
+    *progress += 1;                                   /* rl_task.py:242 */
+    /* ---- get_observations (locomotion.py:194-254) ---- */
+    float tt[3] = {tp->target[0] - rp[0], tp->target[1] - rp[1], tp->target[2] - rp[2]};
+    tt[2] = 0.0f;
+    float prev_p = *pot;
+    float nrm = sqrtf(tt[0] * tt[0] + tt[1] * tt[1] + tt[2] * tt[2]);
+    float new_p = -nrm / tp->task_dt;
+    /* compute_heading_and_up */
+    const float inv_start[4] = {1.0f, -0.0f, -0.0f, -0.0f};
+    float tq[4];
+    ref_quat_mul(rq, inv_start, tq);
+    const float b0[3] = {1.0f, 0.0f, 0.0f}, b1[3] = {0.0f, 0.0f, 1.0f};
+    float up[3], hd[3];
+    ref_quat_rotate(tq, b1, up, 0);
+    ref_quat_rotate(tq, b0, hd, 0);
+    float up_proj = up[2];
+    float tn = sqrtf(tt[0] * tt[0] + tt[1] * tt[1] + tt[2] * tt[2]);
+    tn = tn > 1e-9f ? tn : 1e-9f;
+    float td[3] = {tt[0] / tn, tt[1] / tn, tt[2] / tn};
+    float heading_proj = hd[0] * td[0] + hd[1] * td[1] + hd[2] * td[2];
+    /* compute_rot */
+    float vl[3], al[3];
+    ref_quat_rotate(tq, rv, vl, 1);
+    ref_quat_rotate(tq, rv + 3, al, 1);
+    float roll, pitch, yaw;
+    ref_get_euler_xyz(tq, &roll, &pitch, &yaw);
+    float walk = atan2f(tp->target[2] - rp[2], tp->target[0] - rp[0]);
+    float angle_to_target = walk - yaw;
+    int o = 0;
+    obs[o++] = rp[2];
+    obs[o++] = vl[0]; obs[o++] = vl[1]; obs[o++] = vl[2];
+    obs[o++] = al[0] * tp->angular_velocity_scale;
+    obs[o++] = al[1] * tp->angular_velocity_scale;
+    obs[o++] = al[2] * tp->angular_velocity_scale;
+    obs[o++] = ref_normalize_angle(yaw);
+    obs[o++] = ref_normalize_angle(roll);
+    obs[o++] = ref_normalize_angle(angle_to_target);
+    obs[o++] = up_proj;
+    obs[o++] = heading_proj;
+    for (int j = 0; j < D; ++j) obs[o++] = ref_unscale(q[j], lower[j], upper[j]);
+    for (int j = 0; j < D; ++j) obs[o++] = qd[j] * tp->dof_vel_scale;
+    for (int k = 0; k < 6 * S; ++k) obs[o++] = sens[k] * tp->contact_force_scale;
+    for (int j = 0; j < D; ++j) obs[o++] = act[j];
+    *prev = prev_p;
+    *pot = new_p;
+    /* ---- dof_at_limit_cost (humanoid.py:120-127 / ant.py:92-95) ---- */
+    float limit_cost = 0.0f;
+    if (tp->task_kind == MI_TASK_HUMANOID) {
+        for (int j = 0; j < D; ++j) {
+            float a = fabsf(obs[12 + j]);
+            float sc = tp->joints_at_limit_cost * (a - 0.98f) / 0.02f;
+            limit_cost += (a > 0.98f ? 1.0f : 0.0f) * sc * ratio[j];
+        }
+    } else {
+        int64_t cnt = 0;
+        for (int j = 0; j < D; ++j) cnt += obs[12 + j] > 0.99f;
+        limit_cost = (float)cnt;
+    }
+    /* ---- calculate_metrics (locomotion.py:271-321) ---- */
+    float o11 = obs[11], o10 = obs[10];
+    float heading = o11 > 0.8f ? tp->heading_weight : tp->heading_weight * o11 / 0.8f;
+    float upr = o10 > 0.93f ? 0.0f + tp->up_weight : 0.0f;
+    float act_cost = 0.0f, elec = 0.0f;
+    for (int j = 0; j < D; ++j) act_cost += act[j] * act[j];
+    for (int j = 0; j < D; ++j) elec += fabsf(act[j] * obs[12 + D + j]) * ratio[j];
+    float total = (*pot - *prev) + tp->alive_reward_scale + upr + heading -
+                  tp->actions_cost * act_cost - tp->energy_cost * elec - limit_cost;
+    if (obs[0] < tp->termination_height) total = tp->death_cost;
+    *rew = total;
+    /* ---- is_done (locomotion.py:257-268) ---- */
+    int64_t r = obs[0] < tp->termination_height ? 1 : *reset;
+    if ((float)*progress >= tp->max_episode_length - 1.0f) r = 1;
+    *reset = r;
+}
+
+static void cartpole_post_one(const mi_task_params* tp, const float* q, const float* qd,
+                              float* obs, float* rew, int64_t* reset, int64_t* progress) {
+    *progress += 1;
+    float x = q[0], xd = qd[0], th = q[1], thd = qd[1];
+    obs[0] = x; obs[1] = xd; obs[2] = th; obs[3] = thd;           /* cartpole.py:80-99 */
+    const float half_pi = (float)(ORC_PI / 2.0);
+    float r = 1.0f - th * th - 0.01f * fabsf(xd) - 0.005f * fabsf(thd);   /* :143-153 */
+    if (fabsf(x) > tp->reset_dist) r = -2.0f;
+    if (fabsf(th) > half_pi) r = -2.0f;
+    *rew = r;
+    int64_t d = fabsf(x) > tp->reset_dist ? 1 : 0;                        /* :155-162 */
+    if (fabsf(th) > half_pi) d = 1;
+    if ((float)*progress >= tp->max_episode_length) d = 1;
+    *reset = d;
+}
+
+void orc_loco_post_math(const mi_task_params* tp, int N, int D, int S, const float* root_pos,
+                        const float* root_quat, const float* root_vel, const float* q,
+                        const float* qd, const float* sensors, const float* actions,
+                        const float* lower, const float* upper, float* obs, float* rew,
+                        int64_t* reset_buf, int64_t* progress_buf, float* potentials,
+                        float* prev_potentials) {
+    int O = tp->num_obs;
+    for (int i = 0; i < N; ++i)
+        loco_post_one(tp, D, S, root_pos + 3 * i, root_quat + 4 * i, root_vel + 6 * i,
+                      q + (size_t)D * i, qd + (size_t)D * i, sensors + (size_t)6 * S * i,
+                      actions + (size_t)D * i, lower, upper, tp->motor_effort_ratio,
+                      obs + (size_t)O * i, rew + i, reset_buf + i, progress_buf + i,
+                      potentials + i, prev_potentials + i);
+}
+
+void orc_cartpole_post_math(const mi_task_params* tp, int N, const float* q, const float* qd,
+                            float* obs, float* rew, int64_t* reset_buf, int64_t* progress_buf) {
+    for (int i = 0; i < N; ++i)
+        cartpole_post_one(tp, q + 2 * i, qd + 2 * i, obs + 4 * i, rew + i, reset_buf + i,
+                          progress_buf + i);
+}
+
+static void task_post_env(orc_sim* s, int i, const float* actions, float* obs, float* rew,
+                          int64_t* reset_buf, int64_t* progress_buf, float* potentials,
+                          float* prev_potentials) {
+    const model_t* m = &s->m;
+    const mi_task_params* tp = &s->tp;
+    int D = m->D, O = tp->num_obs;
+    if (tp->task_kind == MI_TASK_CARTPOLE) {
+        cartpole_post_one(tp, s->q + 2 * i, s->qd + 2 * i, obs + (size_t)O * i, rew + i,
+                          reset_buf + i, progress_buf + i);
+    } else {
+        float lower[64], upper[64];
+        for (int j = 0; j < D; ++j) { lower[j] = m->lower[j + 1]; upper[j] = m->upper[j + 1]; }
+        loco_post_one(tp, D, m->S, s->root_pos + 3 * i, s->root_quat + 4 * i, s->root_vel + 6 * i,
+                      s->q + (size_t)D * i, s->qd + (size_t)D * i, s->sens + (size_t)6 * m->S * i,
+                      actions + (size_t)D * i, lower, upper, s->ratio, obs + (size_t)O * i,
+                      rew + i, reset_buf + i, progress_buf + i, potentials + i,
+                      prev_potentials + i);
+    }
+    if (s->nan_flag[i]) { reset_buf[i] = 1; s->nan_flag[i] = 0; }
+}
+
+void orc_task_post_step(orc_sim* s, const float* actions, float* obs, float* rew, int64_t* reset_buf,
+                        int64_t* progress_buf, float* potentials, float* prev_potentials) {
+    for (int i = 0; i < s->N; ++i)
+        task_post_env(s, i, actions, obs, rew, reset_buf, progress_buf, potentials, prev_potentials);
+}
+
+/* VecEnvRLGames.step fused: clamp -> pre -> substeps -> post -> clamp obs */
+void orc_env_step(orc_sim* s, const float* actions, int substeps, float* obs_out, float* obs_task,
+                  float* rew, int64_t* reset_buf, int64_t* progress_buf, float* potentials,
+                  float* prev_potentials, float* actions_out) {
+    const mi_task_params* tp = &s->tp;
+    int A = tp->num_actions, O = tp->num_obs;
+#pragma omp parallel num_threads(g_threads)
+    {
+        ws_t* w = ws_new(&s->m);
+        float act[64], ob[256];
+#pragma omp for schedule(static)
+        for (int i = 0; i < s->N; ++i) {
+            /* task.actions is per-env; use a private row so envs stay independent */
+            task_pre_env(s, i, actions, reset_buf, progress_buf, potentials, prev_potentials,
+                         NULL, 1);
+            for (int j = 0; j < A; ++j) act[j] = clampf(actions[(size_t)A * i + j], -tp->clip_actions, tp->clip_actions);
+            if (actions_out) memcpy(actions_out + (size_t)A * i, act, A * 4);
+            env_physics(s, w, i, substeps);
+            /* post on a one-env view */
+            const model_t* m = &s->m;
+            if (tp->task_kind == MI_TASK_CARTPOLE) {
+                cartpole_post_one(tp, s->q + 2 * i, s->qd + 2 * i, ob, rew + i, reset_buf + i,
+                                  progress_buf + i);
+            } else {
+                float lower[64], upper[64];
+                for (int j = 0; j < m->D; ++j) { lower[j] = m->lower[j + 1]; upper[j] = m->upper[j + 1]; }
+                loco_post_one(tp, m->D, m->S, s->root_pos + 3 * i, s->root_quat + 4 * i,
+                              s->root_vel + 6 * i, s->q + (size_t)m->D * i, s->qd + (size_t)m->D * i,
+                              s->sens + (size_t)6 * m->S * i, act, lower, upper, s->ratio, ob,
+                              rew + i, reset_buf + i, progress_buf + i, potentials + i,
+                              prev_potentials + i);
+            }
+            if (s->nan_flag[i]) { reset_buf[i] = 1; s->nan_flag[i] = 0; }
+            for (int k = 0; k < O; ++k) {
+                if (obs_task) obs_task[(size_t)O * i + k] = ob[k];
+                obs_out[(size_t)O * i + k] = clampf(ob[k], -tp->clip_obs, tp->clip_obs);
+            }
+        }
+        ws_free(w);
+    }
+}
+
+/* ------------------------------------------------------------------------------------ */
+/* cross-checks                                                                          */
+/* ------------------------------------------------------------------------------------ */
+static void load_env(orc_sim* s, ws_t* w, int i) {
+    const model_t* m = &s->m;
+    int nr = m->nr, D = m->D;
+    for (int k = 0; k < nr; ++k) w->u[k] = s->root_vel[6 * i + k];
+    for (int j = 0; j < D; ++j) w->u[nr + j] = s->qd[(size_t)D * i + j];
+    kinematics(m, w, s->root_quat + 4 * i, s->q + (size_t)D * i, w->u);
+}
+
+void orc_dynamics_terms(orc_sim* s, int env, float* M, float* C) {
+    ws_t* w = ws_new(&s->m);
+    load_env(s, w, env);
+    dynamics_terms(&s->m, &s->p, w, w->u);
+    int nv = s->m.nv;
+    memcpy(M, w->M, nv * nv * 4);
+    memcpy(C, w->C, nv * 4);
+    ws_free(w);
+}
+
+/* Featherstone articulated-body algorithm in the same single (p0, world-axes) frame;
+ * gravity as explicit link wrenches; armature + dt*damping on D_k to match M~. */
+void orc_aba(orc_sim* s, int env, const float* tau, float* udot) {
+    const model_t* m = &s->m;
+    const mi_sim_params* p = &s->p;
+    ws_t* w = ws_new(m);
+    load_env(s, w, env);
+    int L = m->L, nr = m->nr;
+    float* u = w->u;
+    float* IA = (float*)calloc(L * 36, 4);
+    float* pA = (float*)calloc(L * 6, 4);
+    float* cl = (float*)calloc(L * 6, 4);
+    float* U = (float*)calloc(L * 6, 4);
+    float* Dk = (float*)calloc(L, 4);
+    float* uk = (float*)calloc(L, 4);
+    float* Aa = (float*)calloc(L * 6, 4);
+    for (int l = 0; l < L; ++l) {
+        memcpy(IA + 36 * l, w->I6 + 36 * l, 144);
+        float Iv[6], t[6], fg[6], gv[6] = {0, 0, 0, p->gravity[0], p->gravity[1], p->gravity[2]};
+        m6_vec(w->I6 + 36 * l, w->V + 6 * l, Iv);
+        crf(w->V + 6 * l, Iv, t);
+        m6_vec(w->I6 + 36 * l, gv, fg);
+        for (int r = 0; r < 6; ++r) pA[6 * l + r] = t[r] - fg[r];
+        if (l == 0) {
+            if (m->root_free) {
+                float wv[3];
+                cross3(u + 3, u, wv);
+                cl[3] = -wv[0]; cl[4] = -wv[1]; cl[5] = -wv[2];
+            }
+        } else {
+            int k = link_dof(m, l);
+            float sd[6];
+            crm(w->V + 6 * m->parent[l], w->S + 6 * k, sd);
+            for (int r = 0; r < 6; ++r) cl[6 * l + r] = sd[r] * u[k];
+        }
+    }
+    for (int l = L - 1; l >= 1; --l) {
+        int k = link_dof(m, l), P = m->parent[l];
+        const float* sk = w->S + 6 * k;
+        m6_vec(IA + 36 * l, sk, U + 6 * l);
+        Dk[l] = dot6(sk, U + 6 * l) + m->armature[l] + p->dt * m->damping[l];
+        uk[l] = tau[k] - m->damping[l] * u[k] - dot6(sk, pA + 6 * l);
+        float Ia[36], pa[6], t[6];
+        for (int i = 0; i < 6; ++i)
+            for (int j = 0; j < 6; ++j)
+                Ia[6 * i + j] = IA[36 * l + 6 * i + j] - U[6 * l + i] * U[6 * l + j] / Dk[l];
+        m6_vec(Ia, cl + 6 * l, t);
+        for (int r = 0; r < 6; ++r) pa[r] = pA[6 * l + r] + t[r] + U[6 * l + r] * uk[l] / Dk[l];
+        for (int i = 0; i < 36; ++i) IA[36 * P + i] += Ia[i];
+        for (int r = 0; r < 6; ++r) pA[6 * P + r] += pa[r];
+    }
+    if (m->root_free) {
+        /* IA0 a0 = -pA0 (dense 6x6 solve via Cholesky) */
+        float G[36], rhs[6], a0[6];
+        for (int r = 0; r < 6; ++r) rhs[r] = -pA[r];
+        cholesky(6, IA, G);
+        chol_solve(6, G, rhs, a0);
+        memcpy(Aa, a0, 24);
+        /* udot root: [lin; ang] = [a0.lin - c0.lin ; a0.ang] */
+        for (int k = 0; k < 3; ++k) { udot[k] = a0[3 + k] - cl[3 + k]; udot[3 + k] = a0[k]; }
+    }
+    for (int l = 1; l < L; ++l) {
+        int k = link_dof(m, l), P = m->parent[l];
+        float Ap[6];
+        for (int r = 0; r < 6; ++r) Ap[r] = Aa[6 * P + r] + cl[6 * l + r];
+        float qdd = (uk[l] - dot6(U + 6 * l, Ap)) / Dk[l];
+        udot[k] = qdd;
+        for (int r = 0; r < 6; ++r) Aa[6 * l + r] = Ap[r] + w->S[6 * k + r] * qdd;
+    }
+    (void)nr;
+    free(IA); free(pA); free(cl); free(U); free(Dk); free(uk); free(Aa);
+    ws_free(w);
+}
+
+double orc_energy(orc_sim* s, int env) {
+    const model_t* m = &s->m;
+    ws_t* w = ws_new(m);
+    load_env(s, w, env);
+    double ke = 0.0, pe = 0.0;
+    for (int l = 0; l < m->L; ++l) {
+        float Iv[6];
+        m6_vec(w->I6 + 36 * l, w->V + 6 * l, Iv);
+        ke += 0.5 * (double)dot6(w->V + 6 * l, Iv);
+        if (m->mass[l] > 0.0f) {
+            float c[3];
+            m3_vec(w->R + 9 * l, m->com + 3 * l, c);
+            double cz[3];
+            for (int k = 0; k < 3; ++k) cz[k] = (double)c[k] + w->o[3 * l + k] + s->root_pos[3 * env + k];
+            pe -= m->mass[l] * (s->p.gravity[0] * cz[0] + s->p.gravity[1] * cz[1] + s->p.gravity[2] * cz[2]);
+        }
+    }
+    ws_free(w);
+    return ke + pe;
+}
+
+void orc_momentum(orc_sim* s, int env, double* out) {
+    const model_t* m = &s->m;
+    ws_t* w = ws_new(m);
+    load_env(s, w, env);
+    float h[6] = {0, 0, 0, 0, 0, 0};
+    for (int l = 0; l < m->L; ++l) {
+        float Iv[6];
+        m6_vec(w->I6 + 36 * l, w->V + 6 * l, Iv);
+        for (int r = 0; r < 6; ++r) h[r] += Iv[r];
+    }
+    /* shift angular momentum from p0 to the world origin: L_O = L_p0 + p0 x P */
+    float pxP[3];
+    cross3(s->root_pos + 3 * env, h + 3, pxP);
+    for (int k = 0; k < 3; ++k) { out[k] = (double)h[k] + pxP[k]; out[3 + k] = h[3 + k]; }
+    ws_free(w);
+}
+
+int orc_contact_count(orc_sim* s, int env) {
+    const model_t* m = &s->m;
+    ws_t* w = ws_new(m);
+    load_env(s, w, env);
+    int n = 0;
+    for (int c = 0; c < m->npts; ++c) {
+        int g = m->pt_geom[c], l = m->geom_link[g];
+        const float* pl = m->pt_end[c] ? m->geom_p1 + 3 * g : m->geom_p0 + 3 * g;
+        float x[3];
+        m3_vec(w->R + 9 * l, pl, x);
+        if (s->root_pos[3 * env + 2] + x[2] + w->o[3 * l + 2] - m->geom_radius[g] < s->p.contact_offset) ++n;
+    }
+    ws_free(w);
+    return n;
+}

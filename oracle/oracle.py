@@ -1,0 +1,226 @@
+"""TEST INFRASTRUCTURE ONLY — ctypes wrapper of oracle/liboracle.so (the CPU checker).
+
+Only tests/, __graft_entry__.smoke() and bench.py's cpu_baseline leg may import this module.
+The product package (omniisaacgymenvs_amd) never imports it.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+import subprocess
+
+import numpy as np
+
+from omniisaacgymenvs_amd import native as N
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "liboracle.so")
+_LIB = None
+
+_f = C.POINTER(C.c_float)
+_i64 = C.POINTER(C.c_int64)
+_u32 = C.POINTER(C.c_uint32)
+
+
+def build() -> str:
+    subprocess.run(["make", "-s", "-C", _HERE], check=True)
+    return LIB_PATH
+
+
+def lib() -> C.CDLL:
+    global _LIB
+    if _LIB is None:
+        if not os.path.exists(LIB_PATH):
+            build()
+        L = C.CDLL(LIB_PATH)
+        sig = {
+            "orc_philox4x32_10": (None, [_u32, _u32, _u32]),
+            "orc_uniform": (C.c_float, [C.c_uint64, C.c_uint64, C.c_uint32, C.c_uint32, C.c_uint32]),
+            "orc_sim_create": (C.c_void_p, [C.POINTER(N.MiModelDesc), C.POINTER(N.MiSimParams),
+                                            C.c_int32, C.c_int64, _f, C.c_uint64]),
+            "orc_sim_destroy": (None, [C.c_void_p]),
+            "orc_sim_num_dof": (C.c_int, [C.c_void_p]),
+            "orc_set_threads": (None, [C.c_int]),
+            "orc_get_root_state": (None, [C.c_void_p, _f, _f, _f]),
+            "orc_get_dof_state": (None, [C.c_void_p, _f, _f]),
+            "orc_get_sensor_wrench": (None, [C.c_void_p, _f]),
+            "orc_set_root_state": (None, [C.c_void_p, _f, _f, _f]),
+            "orc_set_dof_state": (None, [C.c_void_p, _f, _f]),
+            "orc_set_dof_efforts": (None, [C.c_void_p, _f]),
+            "orc_get_reset_count": (None, [C.c_void_p, _u32]),
+            "orc_set_reset_count": (None, [C.c_void_p, _u32]),
+            "orc_nan_count": (C.c_int64, [C.c_void_p]),
+            "orc_sim_step": (None, [C.c_void_p, C.c_int]),
+            "orc_task_configure": (None, [C.c_void_p, C.POINTER(N.MiTaskParams)]),
+            "orc_task_pre_step": (None, [C.c_void_p, _f, _i64, _i64, _f, _f, _f]),
+            "orc_task_post_step": (None, [C.c_void_p, _f, _f, _f, _i64, _i64, _f, _f]),
+            "orc_env_step": (None, [C.c_void_p, _f, C.c_int, _f, _f, _f, _i64, _i64, _f, _f, _f]),
+            "orc_task_reset_idx": (None, [C.c_void_p, _i64, C.c_int, _i64, _i64, _f, _f]),
+            "orc_loco_post_math": (None, [C.POINTER(N.MiTaskParams), C.c_int, C.c_int, C.c_int,
+                                          _f, _f, _f, _f, _f, _f, _f, _f, _f, _f, _f, _i64, _i64,
+                                          _f, _f]),
+            "orc_cartpole_post_math": (None, [C.POINTER(N.MiTaskParams), C.c_int, _f, _f, _f, _f,
+                                              _i64, _i64]),
+            "orc_dynamics_terms": (None, [C.c_void_p, C.c_int, _f, _f]),
+            "orc_aba": (None, [C.c_void_p, C.c_int, _f, _f]),
+            "orc_energy": (C.c_double, [C.c_void_p, C.c_int]),
+            "orc_momentum": (None, [C.c_void_p, C.c_int, C.POINTER(C.c_double)]),
+            "orc_contact_count": (C.c_int, [C.c_void_p, C.c_int]),
+        }
+        for name, (res, args) in sig.items():
+            fn = getattr(L, name)
+            fn.restype = res
+            fn.argtypes = args
+        _LIB = L
+    return _LIB
+
+
+def fp(a):
+    return None if a is None else a.ctypes.data_as(_f)
+
+
+def ip(a):
+    return None if a is None else a.ctypes.data_as(_i64)
+
+
+def philox(ctr, key):
+    c = np.ascontiguousarray(ctr, dtype=np.uint32)
+    k = np.ascontiguousarray(key, dtype=np.uint32)
+    out = np.zeros(4, dtype=np.uint32)
+    lib().orc_philox4x32_10(c.ctypes.data_as(_u32), k.ctypes.data_as(_u32), out.ctypes.data_as(_u32))
+    return out
+
+
+class OracleSim:
+    """Host-side twin of an mi_sim handle (same model, params, seed, env ids)."""
+
+    def __init__(self, model, sim_params: "N.MiSimParams", num_envs: int, env_origins: np.ndarray,
+                 seed: int = 42, env_id_offset: int = 0):
+        self.model = model
+        self._desc = model.to_desc()
+        self.params = sim_params
+        self.N = int(num_envs)
+        self.D = model.num_dof
+        self.S = model.num_sensors
+        self.origins = np.ascontiguousarray(env_origins, dtype=np.float32).reshape(self.N, 3)
+        self.h = lib().orc_sim_create(self._desc.ref(), C.byref(sim_params), self.N,
+                                      int(env_id_offset), fp(self.origins), int(seed))
+        self._tp_keep = None
+
+    def close(self):
+        if self.h:
+            lib().orc_sim_destroy(self.h)
+            self.h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    # state
+    def root_state(self):
+        p = np.zeros((self.N, 3), np.float32)
+        q = np.zeros((self.N, 4), np.float32)
+        v = np.zeros((self.N, 6), np.float32)
+        lib().orc_get_root_state(self.h, fp(p), fp(q), fp(v))
+        return p, q, v
+
+    def dof_state(self):
+        q = np.zeros((self.N, self.D), np.float32)
+        qd = np.zeros((self.N, self.D), np.float32)
+        lib().orc_get_dof_state(self.h, fp(q), fp(qd))
+        return q, qd
+
+    def sensors(self):
+        s = np.zeros((self.N, max(self.S, 1), 6), np.float32)
+        lib().orc_get_sensor_wrench(self.h, fp(s))
+        return s[:, : self.S]
+
+    def set_root_state(self, pos=None, quat=None, vel=None):
+        c = lambda a: None if a is None else np.ascontiguousarray(a, np.float32)
+        pos, quat, vel = c(pos), c(quat), c(vel)
+        lib().orc_set_root_state(self.h, fp(pos), fp(quat), fp(vel))
+
+    def set_dof_state(self, q=None, qd=None):
+        c = lambda a: None if a is None else np.ascontiguousarray(a, np.float32)
+        q, qd = c(q), c(qd)
+        lib().orc_set_dof_state(self.h, fp(q), fp(qd))
+
+    def set_efforts(self, eff):
+        e = np.ascontiguousarray(eff, np.float32)
+        lib().orc_set_dof_efforts(self.h, fp(e))
+
+    def reset_count(self):
+        out = np.zeros(self.N, np.uint32)
+        lib().orc_get_reset_count(self.h, out.ctypes.data_as(_u32))
+        return out
+
+    def set_reset_count(self, c):
+        c = np.ascontiguousarray(c, np.uint32)
+        lib().orc_set_reset_count(self.h, c.ctypes.data_as(_u32))
+
+    def step(self, substeps: int):
+        lib().orc_sim_step(self.h, int(substeps))
+
+    # task
+    def configure(self, tp, keep=None):
+        self._tp_keep = keep
+        lib().orc_task_configure(self.h, C.byref(tp))
+
+    def env_step(self, actions, substeps, bufs):
+        A = np.ascontiguousarray(actions, np.float32)
+        lib().orc_env_step(self.h, fp(A), int(substeps), fp(bufs["obs"]), fp(bufs.get("obs_task")),
+                           fp(bufs["rew"]), ip(bufs["reset"]), ip(bufs["progress"]),
+                           fp(bufs["pot"]), fp(bufs["prev"]), fp(bufs.get("actions")))
+
+    def pre_step(self, actions, bufs):
+        A = np.ascontiguousarray(actions, np.float32)
+        lib().orc_task_pre_step(self.h, fp(A), ip(bufs["reset"]), ip(bufs["progress"]),
+                                fp(bufs["pot"]), fp(bufs["prev"]), fp(bufs.get("actions")))
+
+    def post_step(self, actions, bufs):
+        A = np.ascontiguousarray(actions, np.float32)
+        lib().orc_task_post_step(self.h, fp(A), fp(bufs["obs"]), fp(bufs["rew"]), ip(bufs["reset"]),
+                                 ip(bufs["progress"]), fp(bufs["pot"]), fp(bufs["prev"]))
+
+    def reset_idx(self, env_ids, bufs):
+        ids = np.ascontiguousarray(env_ids, np.int64)
+        lib().orc_task_reset_idx(self.h, ip(ids), int(ids.size), ip(bufs["reset"]),
+                                 ip(bufs["progress"]), fp(bufs["pot"]), fp(bufs["prev"]))
+
+    # cross-checks
+    def dynamics_terms(self, env: int):
+        nv = self.D + 6 * self.model.root_free
+        M = np.zeros((nv, nv), np.float32)
+        Cv = np.zeros(nv, np.float32)
+        lib().orc_dynamics_terms(self.h, env, fp(M), fp(Cv))
+        return M, Cv
+
+    def aba(self, env: int, tau):
+        nv = self.D + 6 * self.model.root_free
+        t = np.ascontiguousarray(tau, np.float32)
+        out = np.zeros(nv, np.float32)
+        lib().orc_aba(self.h, env, fp(t), fp(out))
+        return out
+
+    def energy(self, env: int) -> float:
+        return float(lib().orc_energy(self.h, env))
+
+    def momentum(self, env: int):
+        out = (C.c_double * 6)()
+        lib().orc_momentum(self.h, env, out)
+        return np.array(out[:])
+
+    def contact_count(self, env: int) -> int:
+        return int(lib().orc_contact_count(self.h, env))
+
+    def nan_count(self) -> int:
+        return int(lib().orc_nan_count(self.h))
+
+
+def make_buffers(N_: int, O: int, A: int):
+    return dict(obs=np.zeros((N_, O), np.float32), obs_task=np.zeros((N_, O), np.float32),
+                rew=np.zeros(N_, np.float32), reset=np.ones(N_, np.int64),
+                progress=np.zeros(N_, np.int64), pot=np.zeros(N_, np.float32),
+                prev=np.zeros(N_, np.float32), actions=np.zeros((N_, A), np.float32))
