@@ -60,6 +60,9 @@ def cpu_baseline(task_name: str, env, seconds: float) -> dict:
         ncpu = len(os.sched_getaffinity(0))
     except AttributeError:
         pass
+    # the GPU box exposes the whole machine's CPUs but grants this job a share
+    # (OMP_NUM_THREADS=16 there); never oversubscribe that share
+    ncpu = min(ncpu, int(os.environ.get("OMP_NUM_THREADS", ncpu)))
     sweep = sorted({1, min(4, ncpu), ncpu})
     rng = np.random.default_rng(0)
     for threads in sweep:
@@ -129,21 +132,17 @@ def main():
         N.check(N.lib().mi_fill_uniform(view.handle, actions[k].data_ptr(), A, args.seed, k, -1.0, 1.0,
                                         view.stream()))
     env.reset()
-    rollout = None
-    if world > 1:
-        H = args.gather_every
-        rollout = torch.empty((H, n_local, O + 2), device=device)
-        gathered = torch.empty((world, H, n_local, O + 2), device=device) if True else None
+    from omniisaacgymenvs_amd.utils.distributed import RolloutGather
+
+    rollout = RolloutGather(args.gather_every, n_local, O, device, world) if world > 1 else None
 
     def one_step(k):
         obs, rew, done, _ = env.step(actions[k % pool])
         if rollout is not None:
             h = k % args.gather_every
-            rollout[h, :, :O].copy_(obs["obs"])
-            rollout[h, :, O].copy_(rew)
-            rollout[h, :, O + 1].copy_(done)
+            rollout.record(h, obs["obs"], rew, done)
             if h == args.gather_every - 1:
-                dist.all_gather_into_tensor(gathered.view(-1), rollout.view(-1))
+                rollout.gather()
         return obs
 
     for k in range(args.warmup):

@@ -191,8 +191,9 @@ class ModelDesc:
     """Keeps the numpy arrays alive while a ctypes MiModelDesc points into them."""
 
     def __init__(self, m: CompiledModel):
-        f = lambda a: np.ascontiguousarray(a, dtype=np.float32)
-        i = lambda a: np.ascontiguousarray(a, dtype=np.int32)
+        # private copies: the ctypes struct points into these for the handle's lifetime
+        f = lambda a: np.array(a, dtype=np.float32, order="C", copy=True)
+        i = lambda a: np.array(a, dtype=np.int32, order="C", copy=True)
         self._keep = dict(
             parent=i(m.parent), jtype=i(m.jtype), axis=f(m.axis), pos=f(m.pos), quat=f(m.quat),
             mass=f(m.mass), com=f(m.com), inertia=f(m.inertia), lower=f(m.lower),

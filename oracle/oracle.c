@@ -996,7 +996,7 @@ static void task_post_env(orc_sim* s, int i, const float* actions, float* obs, f
                       rew + i, reset_buf + i, progress_buf + i, potentials + i,
                       prev_potentials + i);
     }
-    if (s->nan_flag[i]) { reset_buf[i] = 1; s->nan_flag[i] = 0; }
+    if (s->nan_flag[i]) { reset_buf[i] = 1; s->nan_flag[i] = 0; s->nan_total++; }
 }
 
 void orc_task_post_step(orc_sim* s, const float* actions, float* obs, float* rew, int64_t* reset_buf,
@@ -1037,7 +1037,11 @@ void orc_env_step(orc_sim* s, const float* actions, int substeps, float* obs_out
                               rew + i, reset_buf + i, progress_buf + i, potentials + i,
                               prev_potentials + i);
             }
-            if (s->nan_flag[i]) { reset_buf[i] = 1; s->nan_flag[i] = 0; }
+            if (s->nan_flag[i]) {
+                reset_buf[i] = 1; s->nan_flag[i] = 0;
+#pragma omp atomic
+                s->nan_total++;
+            }
             for (int k = 0; k < O; ++k) {
                 if (obs_task) obs_task[(size_t)O * i + k] = ob[k];
                 obs_out[(size_t)O * i + k] = clampf(ob[k], -tp->clip_obs, tp->clip_obs);

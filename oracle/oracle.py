@@ -224,3 +224,36 @@ def make_buffers(N_: int, O: int, A: int):
                 rew=np.zeros(N_, np.float32), reset=np.ones(N_, np.int64),
                 progress=np.zeros(N_, np.int64), pot=np.zeros(N_, np.float32),
                 prev=np.zeros(N_, np.float32), actions=np.zeros((N_, A), np.float32))
+
+
+def _c64(a):
+    return np.ascontiguousarray(a, np.int64)
+
+
+def _c32(a):
+    return np.ascontiguousarray(a, np.float32)
+
+
+def loco_post_math(tp, root_pos, root_quat, root_vel, q, qd, sensors, actions, lower, upper,
+                   reset, progress, pot, prev):
+    """Stateless locomotion post_physics_step (obs, reward, done) on caller state."""
+    n, D = np.shape(q)
+    S = np.shape(sensors)[1]
+    arrs = [_c32(x) for x in (root_pos, root_quat, root_vel, q, qd, sensors, actions, lower, upper)]
+    out = dict(obs=np.zeros((n, tp.num_obs), np.float32), rew=np.zeros(n, np.float32),
+               reset=_c64(reset).copy(), progress=_c64(progress).copy(), pot=_c32(pot).copy(),
+               prev=_c32(prev).copy())
+    lib().orc_loco_post_math(C.byref(tp), n, D, S, *(fp(a) for a in arrs), fp(out["obs"]),
+                             fp(out["rew"]), ip(out["reset"]), ip(out["progress"]), fp(out["pot"]),
+                             fp(out["prev"]))
+    return out
+
+
+def cartpole_post_math(tp, q, qd, reset, progress):
+    n = np.shape(q)[0]
+    q, qd = _c32(q), _c32(qd)
+    out = dict(obs=np.zeros((n, 4), np.float32), rew=np.zeros(n, np.float32),
+               reset=_c64(reset).copy(), progress=_c64(progress).copy())
+    lib().orc_cartpole_post_math(C.byref(tp), n, fp(q), fp(qd), fp(out["obs"]), fp(out["rew"]),
+                                 ip(out["reset"]), ip(out["progress"]))
+    return out

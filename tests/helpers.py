@@ -68,3 +68,48 @@ def task_buffers(env):
 def rand_actions(n, a, seed):
     g = torch.Generator().manual_seed(seed)
     return (torch.rand((n, a), generator=g) * 2.4 - 1.2)  # exercises the ±1 clamp
+
+
+def task_params_from_cfg(task_name: str):
+    """MiTaskParams straight from the composed task config (no GPU / no task object)."""
+    from omniisaacgymenvs_amd.robots.model import load_robot
+    from omniisaacgymenvs_amd.utils.hydra_cfg.hydra_utils import compose
+
+    cfg = compose([f"task={task_name}"])["task"]["env"]
+    tp = N.MiTaskParams()
+    m = load_robot(task_name)
+    if task_name == "Cartpole":
+        tp.task_kind, tp.num_obs, tp.num_actions = N.MI_TASK_CARTPOLE, 4, 1
+        tp.clip_actions, tp.clip_obs = cfg["clipActions"], cfg["clipObservations"]
+        tp.max_episode_length = 500.0
+        tp.reset_dist, tp.max_push_effort = cfg["resetDist"], cfg["maxEffort"]
+        return tp, m, None
+    D, S = m.num_dof, m.num_sensors
+    tp.task_kind = N.MI_TASK_HUMANOID if task_name == "Humanoid" else N.MI_TASK_ANT
+    tp.num_obs, tp.num_actions = 12 + 3 * D + 6 * S, D
+    tp.clip_actions, tp.clip_obs = cfg["clipActions"], float("inf")
+    tp.max_episode_length = float(cfg["episodeLength"])
+    for k_c, k_t in [("powerScale", "power_scale"), ("headingWeight", "heading_weight"),
+                     ("upWeight", "up_weight"), ("actionsCost", "actions_cost"),
+                     ("energyCost", "energy_cost"), ("dofVelocityScale", "dof_vel_scale"),
+                     ("angularVelocityScale", "angular_velocity_scale"),
+                     ("contactForceScale", "contact_force_scale"),
+                     ("jointsAtLimitCost", "joints_at_limit_cost"), ("deathCost", "death_cost"),
+                     ("terminationHeight", "termination_height"),
+                     ("alive_reward_scale", "alive_reward_scale")]:
+        setattr(tp, k_t, float(cfg[k_c]))
+    tp.task_dt = 1.0 / 60.0
+    tp.target[:] = [1000.0, 0.0, 0.0]
+    tp.init_root_pos[:] = [0.0, 0.0, 1.34 if task_name == "Humanoid" else 0.5]
+    tp.init_root_quat[:] = [1.0, 0.0, 0.0, 0.0]
+    tp.dof_pos_noise, tp.dof_vel_noise = 0.2, 0.1
+    if task_name == "Humanoid":
+        gears = np.array([67.5] * 7 + [45.0, 45.0, 45.0, 135.0, 45.0, 45.0, 135.0, 45.0, 90.0, 90.0]
+                         + [22.5] * 4, np.float32)
+    else:
+        gears = np.full(D, 15.0, np.float32)
+    ratio = (gears / gears.max()).astype(np.float32) if task_name == "Humanoid" else np.ones(D, np.float32)
+    init = np.zeros(D, np.float32)
+    tp._keep = (gears, ratio, init)
+    tp.joint_gears, tp.motor_effort_ratio, tp.init_dof_pos = N.fptr(gears), N.fptr(ratio), N.fptr(init)
+    return tp, m, (gears, ratio, init)
