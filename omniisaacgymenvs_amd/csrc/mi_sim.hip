@@ -12,10 +12,12 @@
 #include <cstring>
 #include <string>
 #include <vector>
+#include <algorithm>
 
 #include "mi_artic.hpp"
 #include "mi_device.hpp"
 #include "mi_task.hpp"
+#include "mi_wave.hpp"
 
 using namespace mi;
 
@@ -60,6 +62,11 @@ struct mi_sim {
     SimP sp{};
     DevTask tp{};
     bool task_ok = false;
+    bool wave = false;      // wavefront-per-env articulation path (mi_wave.hpp)
+    WaveTabs wt{};
+    float* rows = nullptr;  // per-env global constraint-row slab of the wave path
+    size_t lds_bytes = 0;
+    void* kp_dev = nullptr;  // device copy of KParams (wave path)
     std::vector<float> lower, upper;  // host copy for mi_sim_info
     std::vector<void*> allocs;
 };
@@ -210,6 +217,83 @@ __global__ void k_env_step(DevModel m, DevState st, SimP p, DevTask tp, const fl
     }
 }
 
+// ---- wavefront-per-env articulation path (one 64-lane workgroup = one env) -------------
+// All model / table / state / task parameters sit in ONE device-resident block read through
+// a __restrict__ const pointer: fields are scalar-loaded on use instead of pinning ~1.2 KB
+// of by-value kernel arguments in SGPRs (which spilled).
+struct KParams {
+    DevModel m;
+    WaveTabs t;
+    DevState st;
+    SimP p;
+    DevTask tp;
+    float* rows;
+};
+
+static int sync_kparams(mi_sim* s) {
+    if (!s->wave) return MI_OK;
+    KParams h{};
+    h.m = s->dm; h.t = s->wt; h.st = s->ds; h.p = s->sp; h.tp = s->tp; h.rows = s->rows;
+    if (!s->kp_dev) {
+        void* p = nullptr;
+        int rc = dev_alloc(s, &p, sizeof(KParams));
+        if (rc) return rc;
+        s->kp_dev = p;
+    }
+    HIP_TRY(hipMemcpy(s->kp_dev, &h, sizeof(KParams), hipMemcpyHostToDevice));
+    return MI_OK;
+}
+
+__global__ __launch_bounds__(64) void k_sim_step_wave(const KParams* __restrict__ kp, int substeps) {
+    extern __shared__ __attribute__((aligned(16))) float smem[];
+    const DevModel& m = kp->m;
+    const WaveTabs& t = kp->t;
+    const DevState& st = kp->st;
+    const SimP& p = kp->p;
+    const int i = blockIdx.x;
+    float* gJ = kp->rows + (size_t)i * t.g_row_stride;
+    float* gW = gJ + (size_t)t.max_rows * WNV;
+    for (int s = 0; s < substeps; ++s) wave_artic_substep(m, t, st, p, i, smem, gJ, gW);
+}
+
+__global__ __launch_bounds__(64) void k_env_step_wave(const KParams* __restrict__ kp,
+                                                      const float* actions, int substeps,
+                                                      float* obs_out, float* obs_task, float* rew,
+                                                      int64_t* reset_buf, int64_t* progress_buf,
+                                                      float* pot, float* prev, float* actions_out) {
+    extern __shared__ __attribute__((aligned(16))) float smem[];
+    const DevModel& m = kp->m;
+    const WaveTabs& t = kp->t;
+    const DevState& st = kp->st;
+    const SimP& p = kp->p;
+    const DevTask& tp = kp->tp;
+    float* rows = kp->rows;
+    const int i = blockIdx.x;
+    const int lane = threadIdx.x;
+    // 1. clamp + pre_physics_step (scalar task math on lane 0)
+    if (lane == 0)
+        task_pre_env(m, st, tp, i, actions, reset_buf, progress_buf, pot, prev, actions_out, true);
+    __syncthreads();
+    // 2. controlFrequencyInv x World.step, wave-cooperative
+    float* gJ = rows + (size_t)i * t.g_row_stride;
+    float* gW = gJ + (size_t)t.max_rows * WNV;
+    for (int s = 0; s < substeps; ++s) wave_artic_substep(m, t, st, p, i, smem, gJ, gW);
+    // 3. post_physics_step + obs clamp (lane 0)
+    if (lane == 0) {
+        const int O = tp.O;
+        float* R = (obs_task ? obs_task : obs_out) + (size_t)O * i;
+        loco_post(m, st, tp, i, actions + (size_t)tp.A * i, tp.clip_actions, R, rew, reset_buf,
+                  progress_buf, pot, prev);
+        const float co = tp.clip_obs;
+        float* OUT = obs_out + (size_t)O * i;
+        if (obs_task) {
+            for (int k = 0; k < O; ++k) OUT[k] = clampf(R[k], -co, co);
+        } else if (co < INFINITY) {
+            for (int k = 0; k < O; ++k) OUT[k] = clampf(OUT[k], -co, co);
+        }
+    }
+}
+
 __global__ void k_reset_idx(DevModel m, DevState st, DevTask tp, const int64_t* ids, int n,
                             int64_t* reset_buf, int64_t* progress_buf, float* pot, float* prev) {
     const int t = blockIdx.x * blockDim.x + threadIdx.x;
@@ -263,6 +347,16 @@ __global__ void k_fill_uniform(int N, int64_t off, float* out, int cols, uint64_
 extern "C" {
 
 int mi_abi_version(void) { return MI_ABI_VERSION; }
+
+#ifdef MI_STAMPS
+// diagnostic build only: phase stamps of workgroup MI_STAMP_BLOCK's last substep
+int mi_debug_stamps(unsigned long long* out, int n) {
+    if (!out || n <= 0 || n > 32) return MI_E_ARG;
+    HIP_TRY(hipDeviceSynchronize());
+    HIP_TRY(hipMemcpyFromSymbol(out, HIP_SYMBOL(g_stamps), sizeof(unsigned long long) * n));
+    return MI_OK;
+}
+#endif
 const char* mi_last_error(void) { return g_err.c_str(); }
 
 int mi_sim_create(const mi_model_desc* md, const mi_sim_params* prm, int32_t N, int64_t off,
@@ -369,6 +463,92 @@ int mi_sim_create(const mi_model_desc* md, const mi_sim_params* prm, int32_t N, 
         m.o_cl = o; o += m.npts;
     }
     m.slots = o;
+    // wavefront-per-env path: eligibility + host-built tree tables + LDS layout
+    {
+        const char* path = getenv("MI_SIM_PATH");
+        const bool want_thread = path && std::string(path) == "thread";
+        s->wave = m.dyn == MI_DYN_ARTICULATION && !want_thread && m.nv <= WNV && m.npts <= 64 &&
+                  m.max_rows <= 128 && L <= 64;
+    }
+    if (s->wave) {
+        WaveTabs& t = s->wt;
+        std::vector<int> depth(L, 0);
+        int maxd = 0;
+        for (int l = 1; l < L; ++l) { depth[l] = depth[md->parent[l]] + 1; maxd = std::max(maxd, depth[l]); }
+        t.nlev = maxd + 1;
+        std::vector<int> lev_start(t.nlev + 1, 0), lev_links;
+        for (int d = 0; d < t.nlev; ++d) {
+            lev_start[d] = (int)lev_links.size();
+            for (int l = 0; l < L; ++l) if (depth[l] == d) lev_links.push_back(l);
+        }
+        lev_start[t.nlev] = (int)lev_links.size();
+        std::vector<int> child_start(L + 1, 0), child_list;
+        for (int l = 0; l < L; ++l) {
+            child_start[l] = (int)child_list.size();
+            for (int c = l + 1; c < L; ++c) if (md->parent[c] == l) child_list.push_back(c);
+        }
+        child_start[L] = (int)child_list.size();
+        std::vector<int> desc_start(L + 1, 0), desc_list;
+        for (int l = 0; l < L; ++l) {
+            desc_start[l] = (int)desc_list.size();
+            for (int c = l + 1; c < L; ++c) {
+                int x = md->parent[c];
+                while (x > l) x = md->parent[x];
+                if (x == l) desc_list.push_back(c);
+            }
+        }
+        desc_start[L] = (int)desc_list.size();
+        if (desc_list.empty()) desc_list.push_back(0);
+        std::vector<int> anc_start(m.nv + 1, 0), anc_list;
+        int na_max = 0;
+        for (int k = 0; k < m.nv; ++k) {
+            anc_start[k] = (int)anc_list.size();
+            for (int j = dof_parent[k]; j >= 0; j = dof_parent[j]) anc_list.push_back(j);
+            na_max = std::max(na_max, (int)anc_list.size() - anc_start[k]);
+        }
+        anc_start[m.nv] = (int)anc_list.size();
+        std::vector<unsigned long long> link_mask(L, 0ull);
+        for (int l = 0; l < L; ++l) {
+            unsigned long long msk = 0ull;
+            for (int k = 0; k < m.nr; ++k) msk |= 1ull << k;
+            for (int x = l; x > 0; x = md->parent[x]) msk |= 1ull << (m.nr + x - 1);
+            link_mask[l] = msk;
+        }
+        std::vector<unsigned char> tri_p, tri_q;
+        for (int q = 0; q < na_max; ++q)
+            for (int p2 = 0; p2 <= q; ++p2) { tri_p.push_back((unsigned char)p2); tri_q.push_back((unsigned char)q); }
+        if (tri_p.empty()) { tri_p.push_back(0); tri_q.push_back(0); }
+        if (child_list.empty()) child_list.push_back(0);
+        if (anc_list.empty()) anc_list.push_back(0);
+#define UPW(field, vec) if ((rc = upload(s, vec.data(), vec.size(), &t.field))) return cleanup(rc)
+        UPW(lev_start, lev_start); UPW(lev_links, lev_links); UPW(child_start, child_start);
+        UPW(child_list, child_list); UPW(anc_start, anc_start); UPW(anc_list, anc_list);
+        UPW(desc_start, desc_start); UPW(desc_list, desc_list);
+        UPW(link_mask, link_mask); UPW(tri_p, tri_p); UPW(tri_q, tri_q);
+#undef UPW
+        auto al4 = [](int x) { return (x + 3) & ~3; };
+        int so = 0;
+        auto take = [&](int n) { const int at = so; so += al4(n); return at; };
+        t.s_R = take(9 * L); t.s_o = take(3 * L); t.s_S = take(6 * m.nv); t.s_V = take(6 * L);
+        t.s_A = take(6 * L); t.s_F = take(6 * L); t.s_Ic = take(10 * L); t.s_M = take(WNV * WNV);
+        t.s_X = take(16 * L);  // aux: local transforms (P1), composite inertia / force (P2)
+        t.s_D = take(WNV); t.s_r = take(WNV); t.s_us = take(WNV);
+        t.s_q = take(WNV); t.s_rp = take(8); t.s_cp = take(3 * 64); t.s_cl = take(64);
+        t.s_rl = take(128); t.s_rf = take(6 * 128); t.s_rb = take(128); t.s_rk = take(128);
+        t.s_ad = take(128);
+        t.s_xs = take(WNV * 64);   // lane-private solve vectors
+        t.s_total = so;
+        {   // every region must be distinct: offsets strictly increase in declaration order
+            const int offs[] = {t.s_R, t.s_o, t.s_S, t.s_V, t.s_A, t.s_F, t.s_Ic, t.s_M, t.s_X,
+                                t.s_D, t.s_r, t.s_us, t.s_q, t.s_rp, t.s_cp, t.s_cl, t.s_rl,
+                                t.s_rf, t.s_rb, t.s_rk, t.s_ad, t.s_xs, t.s_total};
+            for (size_t c = 1; c < sizeof(offs) / sizeof(offs[0]); ++c)
+                if (offs[c] <= offs[c - 1]) return cleanup(fail(MI_E_STATE, "wave LDS layout: region %zu overlaps", c));
+        }
+        t.max_rows = m.max_rows;
+        t.g_row_stride = (size_t)2 * m.max_rows * WNV;
+        s->lds_bytes = (size_t)so * sizeof(float);
+    }
     s->lower.assign(md->lower, md->lower + L);
     s->upper.assign(md->upper, md->upper + L);
     // params
@@ -393,7 +573,13 @@ int mi_sim_create(const mi_model_desc* md, const mi_sim_params* prm, int32_t N, 
     AL(q, float, (size_t)D * N); AL(qd, float, (size_t)D * N); AL(eff, float, (size_t)D * N);
     AL(sens, float, (size_t)6 * S * N); AL(reset_count, uint32_t, N); AL(nan_flag, int32_t, N);
     AL(nan_total, unsigned long long, 1);
-    AL(ws, float, (size_t)((N + 63) / 64) * 64 * (m.slots > 0 ? m.slots : 1));
+    if (s->wave) {
+        if ((rc = dev_alloc(s, &p, sizeof(float) * (size_t)N * s->wt.g_row_stride))) return cleanup(rc);
+        s->rows = (float*)p;
+        AL(ws, float, 64);
+    } else {
+        AL(ws, float, (size_t)((N + 63) / 64) * 64 * (m.slots > 0 ? m.slots : 1));
+    }
 #undef AL
     std::vector<float> org((size_t)3 * N);
     for (int i = 0; i < N; ++i)
@@ -404,6 +590,7 @@ int mi_sim_create(const mi_model_desc* md, const mi_sim_params* prm, int32_t N, 
     hipLaunchKernelGGL(k_init_state, grid_for(s, N), dim3(s->block), 0, 0, st, m.D);
     hipError_t e = hipDeviceSynchronize();
     if (e != hipSuccess) return cleanup(fail(MI_E_HIP, "init: %s", hipGetErrorString(e)));
+    if ((rc = sync_kparams(s))) return cleanup(rc);
     *out = s;
     return MI_OK;
 }
@@ -507,8 +694,12 @@ int mi_sim_step(mi_sim* s, int32_t substeps, void* stream) {
     NEED(s);
     if (substeps < 0 || substeps > 64) return fail(MI_E_ARG, "substeps %d out of range", substeps);
     HIP_TRY(hipSetDevice(s->device));
-    hipLaunchKernelGGL(k_sim_step, grid_for(s, s->N), dim3(s->block), 0, STREAM(stream), s->dm,
-                       s->ds, s->sp, substeps);
+    if (s->wave)
+        hipLaunchKernelGGL(k_sim_step_wave, dim3(s->N), dim3(64), s->lds_bytes, STREAM(stream),
+                           (const KParams*)s->kp_dev, substeps);
+    else
+        hipLaunchKernelGGL(k_sim_step, grid_for(s, s->N), dim3(s->block), 0, STREAM(stream), s->dm,
+                           s->ds, s->sp, substeps);
     LAUNCH_CHECK();
     return MI_OK;
 }
@@ -550,6 +741,7 @@ int mi_task_configure(mi_sim* s, const mi_task_params* t) {
     }
     for (int j = 0; j < D && j < MI_MAXA; ++j) d.init_dof[j] = t->init_dof_pos ? t->init_dof_pos[j] : 0.0f;
     s->task_ok = true;
+    if (int rc = sync_kparams(s)) return rc;
     return MI_OK;
 }
 
@@ -630,9 +822,14 @@ int mi_env_step(mi_sim* s, const float* actions, int32_t substeps, float* obs_ou
     if (s->tp.kind != MI_TASK_CARTPOLE) { NEED(potentials); NEED(prev_potentials); }
     if (substeps < 0 || substeps > 64) return fail(MI_E_ARG, "substeps %d out of range", substeps);
     HIP_TRY(hipSetDevice(s->device));
-    hipLaunchKernelGGL(k_env_step, grid_for(s, s->N), dim3(s->block), 0, STREAM(stream), s->dm,
-                       s->ds, s->sp, s->tp, actions, substeps, obs_out, obs_task, rew, reset_buf,
-                       progress_buf, potentials, prev_potentials, actions_out);
+    if (s->wave && s->tp.kind != MI_TASK_CARTPOLE)
+        hipLaunchKernelGGL(k_env_step_wave, dim3(s->N), dim3(64), s->lds_bytes, STREAM(stream),
+                           (const KParams*)s->kp_dev, actions, substeps, obs_out, obs_task, rew,
+                           reset_buf, progress_buf, potentials, prev_potentials, actions_out);
+    else
+        hipLaunchKernelGGL(k_env_step, grid_for(s, s->N), dim3(s->block), 0, STREAM(stream), s->dm,
+                           s->ds, s->sp, s->tp, actions, substeps, obs_out, obs_task, rew, reset_buf,
+                           progress_buf, potentials, prev_potentials, actions_out);
     LAUNCH_CHECK();
     return MI_OK;
 }

@@ -1,0 +1,645 @@
+// mi_wave.hpp — wavefront-per-env articulated substep (gfx950).
+//
+// Same algorithm and constraint-row order as mi_artic.hpp (and the CPU oracle); the mapping
+// is what changes. One 64-lane wavefront owns one env and keeps that env's working set in
+// LDS; every phase is parallel over the tree's links, DOFs, candidate contact points or
+// constraint rows:
+//   P1  forward kinematics / velocities / Newton-Euler, level-synchronous over link depth
+//   P2  composite inertia + force sums, deepest level first (each parent sums its children
+//       in a fixed order: deterministic, no atomics)
+//   P3  bias C_k and CRBA row k (lane k walks its ancestor chain)
+//   P4  tree LTDL factorisation, k = nv-1..0, lanes over the (i,j) ancestor pairs of k
+//   P5  X = L^-1, lanes over columns (uniform row loop, lane-private column in LDS)
+//   P6  M~^-1 = X D^-1 X^T, lanes over entries, stored dense + zero-padded to 32x32
+//   P7  u* = u + dt M~^-1 rhs
+//   P8  contact / limit detection, lanes over candidates, ballot-prefix row compaction
+//       (rows in candidate order, as the oracle)
+//   P9  lanes over rows: J_r and W_r = M~^-1 J_r^T in registers (32x32 FMAs, Minv rows
+//       read as LDS broadcasts), A_rr = J_r . W_r; rows spilled to the env's global slab
+//   P10 projected Gauss-Seidel, lanes over DOFs (u_k in a register), one wave reduction
+//       per row update; lambda and row metadata live in lane registers (readlane)
+//   P11 force sensors, semi-implicit integration, write-back.
+// Requirements checked on the host: nv <= 32, npts <= 64, rows <= 128, L <= 64.
+#pragma once
+#include "mi_artic.hpp"
+#include "mi_device.hpp"
+
+namespace mi {
+
+constexpr int WNV = 32;  // padded DOF count of the wave path
+
+// Diagnostic phase stamps (built only with -DMI_STAMPS into a separate library; the product
+// build compiles them out). Workgroup MI_STAMP_BLOCK records s_memtime at every phase
+// boundary of its last substep.
+#ifdef MI_STAMPS
+#define MI_STAMP_BLOCK 7
+__device__ unsigned long long g_stamps[32];
+#define STAMP(k)                                                                          \
+    do {                                                                                  \
+        __builtin_amdgcn_sched_barrier(0);                                                \
+        unsigned long long t_;                                                            \
+        asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t_)::"memory");         \
+        if (blockIdx.x == MI_STAMP_BLOCK && threadIdx.x == 0) g_stamps[k] = t_;           \
+        __builtin_amdgcn_sched_barrier(0);                                                \
+    } while (0)
+#else
+#define STAMP(k) \
+    do {         \
+    } while (0)
+#endif
+
+struct WaveTabs {
+    int nlev;
+    const int* lev_start;     // [nlev+1]
+    const int* lev_links;     // [L]
+    const int* child_start;   // [L+1]
+    const int* child_list;    // [L]
+    const int* desc_start;    // [L+1] descendants of link l (excl. l), increasing index
+    const int* desc_list;
+    const int* anc_start;     // [nv+1] ancestors of dof k (excl. k), nearest first
+    const int* anc_list;
+    const unsigned long long* link_mask;  // [L] dofs on the root..l path
+    const unsigned char* tri_p;           // pair index -> (p, q), p <= q
+    const unsigned char* tri_q;
+    // LDS float offsets
+    int s_R, s_o, s_S, s_V, s_A, s_F, s_Ic, s_M, s_X, s_D, s_r, s_us, s_q, s_rp, s_cp, s_cl,
+        s_rl, s_rf, s_rb, s_rk, s_ad, s_xs, s_total;
+    int max_rows;
+    size_t g_row_stride;  // floats per env in the global row slab (2 * max_rows * WNV)
+};
+
+MI_D float wave_sum(float v) {
+#pragma unroll
+    for (int o = 32; o >= 1; o >>= 1) v += __shfl_xor(v, o, 64);
+    return v;
+}
+MI_D float readlane(float v, int l) {
+    return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), l));
+}
+template <int CTRL, int ROW_MASK = 0xF, bool BOUND_CTRL = true>
+MI_D float dpp(float v) {
+    return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), CTRL, ROW_MASK, 0xF, BOUND_CTRL));
+}
+// Sum over each 32-lane half of the wave with DPP only (no LDS crossbar): quad swaps,
+// half-row / row mirrors, then row_bcast:15 folds row 0 into row 1 (and 2 into 3).
+// Lane 31 holds sum(lanes 0..31), lane 63 holds sum(lanes 32..63).
+MI_D float half_sums(float v) {
+    v += dpp<0xB1>(v);          // quad_perm [1,0,3,2]
+    v += dpp<0x4E>(v);          // quad_perm [2,3,0,1]
+    v += dpp<0x141>(v);         // row_half_mirror
+    v += dpp<0x140>(v);         // row_mirror
+    v += dpp<0x142, 0xA, false>(v);  // row_bcast:15 into rows 1 and 3
+    return v;
+}
+
+// x <- M~^-1 x (tree LTDL factor of M~ in Mx, 1/D in Dinv) on a lane-private vector kept in LDS: element c of lane's vector at
+// xs[c * 64 + lane] (uniform offsets, consecutive banks: conflict-free). LDS operations of
+// one wave complete in order, so a read after a write to the same slot sees the write.
+MI_D void tree_solve_lds(const WaveTabs& t, const float* Mx, const float* Dinv, int nv,
+                         float* xs) {
+    for (int i = nv - 1; i >= 0; --i) {
+        const float xi = xs[i * 64];
+        for (int a = t.anc_start[i]; a < t.anc_start[i + 1]; ++a) {
+            const int j = t.anc_list[a];
+            xs[j * 64] -= Mx[i * nv + j] * xi;
+        }
+    }
+    for (int i = 0; i < nv; ++i) xs[i * 64] *= Dinv[i];
+    for (int i = 0; i < nv; ++i) {
+        float xi = xs[i * 64];
+        for (int a = t.anc_start[i]; a < t.anc_start[i + 1]; ++a) {
+            const int j = t.anc_list[a];
+            xi -= Mx[i * nv + j] * xs[j * 64];
+        }
+        xs[i * 64] = xi;
+    }
+}
+
+// P1a: local joint transform of link l >= 1 (independent of every other link):
+// aux[15 l ..] = {Rloc = Rq Rot(axis, q) (9), tloc (3), aloc = Rq axis (3)}
+MI_D void wave_link_local(const DevModel& m, const WaveTabs& t, float* sm, int l) {
+    float* aux = sm + t.s_X + 15 * l;
+    float Rq[9], a[3];
+    m3_from_quat(m.quat + 4 * l, Rq);
+    m3_vec(Rq, m.axis + 3 * l, a);
+    const float qj = sm[t.s_q + l - 1];
+    float R[9], tl[3] = {m.pos[3 * l], m.pos[3 * l + 1], m.pos[3 * l + 2]};
+    if (m.jtype[l] == MI_JOINT_HINGE) {
+        float Ra[9];
+        m3_axis_angle(m.axis + 3 * l, qj, Ra);
+        m3_mul(Rq, Ra, R);
+    } else {
+#pragma unroll
+        for (int c = 0; c < 9; ++c) R[c] = Rq[c];
+#pragma unroll
+        for (int c = 0; c < 3; ++c) tl[c] += a[c] * qj;
+    }
+#pragma unroll
+    for (int c = 0; c < 9; ++c) aux[c] = R[c];
+#pragma unroll
+    for (int c = 0; c < 3; ++c) { aux[9 + c] = tl[c]; aux[12 + c] = a[c]; }
+}
+
+// P1b: compose link l's world frame, subspace, velocity and velocity-product acceleration
+// from its parent (one tree level at a time)
+MI_D void wave_link_compose(const DevModel& m, const WaveTabs& t, float* sm, int l,
+                            const SimP& p) {
+    float* Rs = sm + t.s_R;
+    float* os = sm + t.s_o;
+    float* Vs = sm + t.s_V;
+    float* As = sm + t.s_A;
+    const int nr = m.nr;
+    float R[9], o[3], V[6], A[6];
+    if (l == 0) {
+        m3_from_quat(sm + t.s_rp + 4, R);
+        o[0] = o[1] = o[2] = 0.0f;
+        A[0] = A[1] = A[2] = 0.0f;
+        A[3] = -p.g[0]; A[4] = -p.g[1]; A[5] = -p.g[2];
+        if (nr) {
+            const float* u = sm + t.s_us;
+            const float v[3] = {u[0], u[1], u[2]};
+            const float om[3] = {u[3], u[4], u[5]};
+            float wv[3];
+            cross3(om, v, wv);
+            A[3] -= wv[0]; A[4] -= wv[1]; A[5] -= wv[2];
+            V[0] = om[0]; V[1] = om[1]; V[2] = om[2];
+            V[3] = v[0]; V[4] = v[1]; V[5] = v[2];
+        } else {
+#pragma unroll
+            for (int c = 0; c < 6; ++c) V[c] = 0.0f;
+        }
+    } else {
+        const int P = m.parent[l], k = nr + l - 1;
+        const float* aux = sm + t.s_X + 15 * l;
+        float RP[9], VP[6], AP[6], a[3], op[3], s[6];
+#pragma unroll
+        for (int c = 0; c < 9; ++c) RP[c] = Rs[9 * P + c];
+#pragma unroll
+        for (int c = 0; c < 6; ++c) { VP[c] = Vs[6 * P + c]; AP[c] = As[6 * P + c]; }
+        m3_mul(RP, aux, R);
+        m3_vec(RP, aux + 9, op);
+        m3_vec(RP, aux + 12, a);
+#pragma unroll
+        for (int c = 0; c < 3; ++c) o[c] = os[3 * P + c] + op[c];
+        if (m.jtype[l] == MI_JOINT_HINGE) {
+            s[0] = a[0]; s[1] = a[1]; s[2] = a[2];
+            cross3(o, a, s + 3);
+        } else {
+            s[0] = s[1] = s[2] = 0.0f;
+            s[3] = a[0]; s[4] = a[1]; s[5] = a[2];
+        }
+#pragma unroll
+        for (int c = 0; c < 6; ++c) sm[t.s_S + 6 * k + c] = s[c];
+        const float uk = sm[t.s_us + k];
+        float sd[6];
+        crm(VP, s, sd);
+#pragma unroll
+        for (int c = 0; c < 6; ++c) { V[c] = VP[c] + s[c] * uk; A[c] = AP[c] + sd[c] * uk; }
+    }
+#pragma unroll
+    for (int c = 0; c < 9; ++c) Rs[9 * l + c] = R[c];
+#pragma unroll
+    for (int c = 0; c < 3; ++c) os[3 * l + c] = o[c];
+#pragma unroll
+    for (int c = 0; c < 6; ++c) { Vs[6 * l + c] = V[c]; As[6 * l + c] = A[c]; }
+}
+
+// P1c: spatial inertia about p0 and Newton-Euler force of link l (independent per link)
+MI_D void wave_link_dynamics(const DevModel& m, const WaveTabs& t, float* sm, int l) {
+    float I[10] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
+    float F[6] = {0, 0, 0, 0, 0, 0};
+    const float mass = m.mass[l];
+    if (mass > 0.0f) {
+        float R[9], o[3], V[6], A[6];
+#pragma unroll
+        for (int c = 0; c < 9; ++c) R[c] = sm[t.s_R + 9 * l + c];
+#pragma unroll
+        for (int c = 0; c < 3; ++c) o[c] = sm[t.s_o + 3 * l + c];
+#pragma unroll
+        for (int c = 0; c < 6; ++c) { V[c] = sm[t.s_V + 6 * l + c]; A[c] = sm[t.s_A + 6 * l + c]; }
+        float c3[3], T[9], Iw[9];
+        m3_vec(R, m.com + 3 * l, c3);
+        c3[0] += o[0]; c3[1] += o[1]; c3[2] += o[2];
+        const float* in = m.inertia + 6 * l;
+        const float Ib[9] = {in[0], in[3], in[4], in[3], in[1], in[5], in[4], in[5], in[2]};
+        m3_mul(R, Ib, T);
+#pragma unroll
+        for (int a = 0; a < 3; ++a)
+#pragma unroll
+            for (int b = 0; b < 3; ++b)
+                Iw[3 * a + b] = T[3 * a] * R[3 * b] + T[3 * a + 1] * R[3 * b + 1] + T[3 * a + 2] * R[3 * b + 2];
+        const float cc = dot3(c3, c3);
+        I[0] = mass;
+        I[1] = mass * c3[0]; I[2] = mass * c3[1]; I[3] = mass * c3[2];
+        I[4] = Iw[0] + mass * (cc - c3[0] * c3[0]);
+        I[5] = Iw[4] + mass * (cc - c3[1] * c3[1]);
+        I[6] = Iw[8] + mass * (cc - c3[2] * c3[2]);
+        I[7] = Iw[1] - mass * c3[0] * c3[1];
+        I[8] = Iw[2] - mass * c3[0] * c3[2];
+        I[9] = Iw[5] - mass * c3[1] * c3[2];
+        float IA[6], IV[6], tt[6];
+        inertia_mul(I, A, IA);
+        inertia_mul(I, V, IV);
+        crf(V, IV, tt);
+#pragma unroll
+        for (int c = 0; c < 6; ++c) F[c] = IA[c] + tt[c];
+    }
+#pragma unroll
+    for (int c = 0; c < 10; ++c) sm[t.s_Ic + 10 * l + c] = I[c];
+#pragma unroll
+    for (int c = 0; c < 6; ++c) sm[t.s_F + 6 * l + c] = F[c];
+}
+
+// One articulated substep of env i, executed by the whole 64-lane workgroup.
+// sm: this env's LDS region; gJ / gW: this env's global row slab [max_rows][WNV] each.
+MI_D void wave_artic_substep(const DevModel& m, const WaveTabs& t, const DevState& st,
+                             const SimP& p, int i, float* sm, float* gJ, float* gW) {
+    const int lane = threadIdx.x;
+    const int N = st.N, L = m.L, D = m.D, nv = m.nv, nr = m.nr;
+    const float dt = p.dt;
+    float* us = sm + t.s_us;   // u, then u*
+    float* rhs = sm + t.s_r;
+    float* Mx = sm + t.s_M;    // M (lower), then dense padded M~^-1 [WNV][WNV]
+    float* Xc = sm + t.s_X;    // X = L^-1 by columns: Xc[j*nv + i] = X_ij
+    float* Dv = sm + t.s_D;
+    float* Ss = sm + t.s_S;
+
+    STAMP(0);
+    // ---- load state into LDS
+    if (lane < 3) sm[t.s_rp + lane] = st.root_pos[(size_t)lane * N + i];
+    if (lane < 4) sm[t.s_rp + 4 + lane] = st.root_quat[(size_t)lane * N + i];
+    if (lane < nr) us[lane] = st.root_vel[(size_t)lane * N + i];
+    else if (lane < nv) us[lane] = st.qd[(size_t)(lane - nr) * N + i];
+    if (lane < D) sm[t.s_q + lane] = st.q[(size_t)lane * N + i];
+    if (nr && lane < 6) {
+        float s[6] = {0, 0, 0, 0, 0, 0};
+        if (lane < 3) s[3 + lane] = 1.0f; else s[lane - 3] = 1.0f;
+#pragma unroll
+        for (int c = 0; c < 6; ++c) Ss[6 * lane + c] = s[c];
+    }
+    __syncthreads();
+
+    STAMP(1);
+    // ---- P1a: local joint transforms, every link at once
+    for (int l = 1 + lane; l < L; l += 64) wave_link_local(m, t, sm, l);
+    __syncthreads();
+    // ---- P1b: world frames / subspaces / velocities, one tree level at a time
+    for (int lev = 0; lev < t.nlev; ++lev) {
+        const int b = t.lev_start[lev], e = t.lev_start[lev + 1];
+        for (int c = b + lane; c < e; c += 64) wave_link_compose(m, t, sm, t.lev_links[c], p);
+        __syncthreads();
+    }
+    // ---- P1c: link inertias + Newton-Euler forces, every link at once
+    for (int l = lane; l < L; l += 64) wave_link_dynamics(m, t, sm, l);
+    __syncthreads();
+    STAMP(2);
+    // ---- P2: composite inertia / force = own + sum over the subtree (fixed descendant order,
+    // every link at once; results into the aux region: Ic at 16 l, F at 16 l + 10)
+    float* aux = sm + t.s_X;
+    for (int l = lane; l < L; l += 64) {
+        float I[10], F[6];
+#pragma unroll
+        for (int q = 0; q < 10; ++q) I[q] = sm[t.s_Ic + 10 * l + q];
+#pragma unroll
+        for (int q = 0; q < 6; ++q) F[q] = sm[t.s_F + 6 * l + q];
+        for (int di = t.desc_start[l]; di < t.desc_start[l + 1]; ++di) {
+            const int d = t.desc_list[di];
+#pragma unroll
+            for (int q = 0; q < 10; ++q) I[q] += sm[t.s_Ic + 10 * d + q];
+#pragma unroll
+            for (int q = 0; q < 6; ++q) F[q] += sm[t.s_F + 6 * d + q];
+        }
+#pragma unroll
+        for (int q = 0; q < 10; ++q) aux[16 * l + q] = I[q];
+#pragma unroll
+        for (int q = 0; q < 6; ++q) aux[16 * l + 10 + q] = F[q];
+    }
+    __syncthreads();
+    STAMP(3);
+    // ---- P3: bias + CRBA (lane k = dof k)
+    if (lane < nv) {
+        const int k = lane, l = m.dof_link[k];
+        float s[6], I[10], f[6], F[6];
+#pragma unroll
+        for (int c = 0; c < 6; ++c) { s[c] = Ss[6 * k + c]; F[c] = aux[16 * l + 10 + c]; }
+#pragma unroll
+        for (int c = 0; c < 10; ++c) I[c] = aux[16 * l + c];
+        inertia_mul(I, s, f);
+        float diag = dot6(s, f);
+        float r = -dot6(s, F);
+        if (k >= nr) {
+            diag += m.armature[l] + dt * m.damping[l];
+            r += st.eff[(size_t)(k - nr) * N + i] - m.damping[l] * us[k];
+        }
+        Mx[k * nv + k] = diag;
+        rhs[k] = r;
+        for (int a = t.anc_start[k]; a < t.anc_start[k + 1]; ++a) {
+            const int j = t.anc_list[a];
+            float sj[6];
+#pragma unroll
+            for (int c = 0; c < 6; ++c) sj[c] = Ss[6 * j + c];
+            Mx[k * nv + j] = dot6(sj, f);
+        }
+    }
+    __syncthreads();
+    STAMP(4);
+    // ---- P4: LTDL in place (M = L^T D L, L strictly below the diagonal)
+    for (int k = nv - 1; k >= 0; --k) {
+        const int a0 = t.anc_start[k], na = t.anc_start[k + 1] - a0;
+        const float inv = 1.0f / Mx[k * nv + k];
+        const int npair = na * (na + 1) / 2;
+        for (int pi = lane; pi < npair; pi += 64) {
+            const int ii = t.anc_list[a0 + t.tri_p[pi]], jj = t.anc_list[a0 + t.tri_q[pi]];
+            Mx[ii * nv + jj] -= (Mx[k * nv + ii] * inv) * Mx[k * nv + jj];
+        }
+        __syncthreads();
+        if (lane < na) {
+            const int ii = t.anc_list[a0 + lane];
+            Mx[k * nv + ii] = Mx[k * nv + ii] * inv;
+        }
+        __syncthreads();
+    }
+    STAMP(5);
+    // ---- P5: 1/D of the factor
+    if (lane < nv) Dv[lane] = 1.0f / Mx[lane * nv + lane];
+    __syncthreads();
+    STAMP(6);
+    STAMP(7);
+    // ---- P7: u* = u + dt M~^-1 rhs (one lane, register-resident tree solve)
+    float* xs = sm + t.s_xs + lane;   // this lane's private solve vector (stride 64)
+    if (lane == 0) {
+        for (int c = 0; c < nv; ++c) xs[c * 64] = rhs[c];
+        tree_solve_lds(t, Mx, Dv, nv, xs);
+        for (int c = 0; c < nv; ++c) us[c] = us[c] + dt * xs[c * 64];
+    }
+    __syncthreads();
+
+    STAMP(8);
+    // ---- P8: candidate contact points (lane c), ballot compaction in candidate order
+    int ncon = 0;
+    {
+        const float rpz = sm[t.s_rp + 2];
+        bool act = false;
+        float pc[3] = {0, 0, 0}, bn = 0.0f;
+        int l = 0;
+        if (lane < m.npts) {
+            const int g = m.pt_geom[lane];
+            l = m.geom_link[g];
+            const float* pl = m.pt_end[lane] ? m.geom_p1 + 3 * g : m.geom_p0 + 3 * g;
+            float R[9], x[3];
+#pragma unroll
+            for (int q = 0; q < 9; ++q) R[q] = sm[t.s_R + 9 * l + q];
+            m3_vec(R, pl, x);
+#pragma unroll
+            for (int q = 0; q < 3; ++q) x[q] += sm[t.s_o + 3 * l + q];
+            const float r = m.geom_radius[g];
+            const float gap = rpz + x[2] - r;
+            act = gap < p.contact_offset;
+            pc[0] = x[0]; pc[1] = x[1]; pc[2] = x[2] - r;
+            const float d = gap - p.rest_offset;
+            bn = d >= 0.0f ? -d / dt : -p.erp * d / dt;
+            if (bn > p.max_depen) bn = p.max_depen;
+        }
+        const unsigned long long mask = __ballot(act);
+        ncon = __popcll(mask);
+        if (act) {
+            const int ci = __popcll(mask & ((1ull << lane) - 1ull));
+#pragma unroll
+            for (int q = 0; q < 3; ++q) sm[t.s_cp + 3 * ci + q] = pc[q];
+            sm[t.s_cl + ci] = (float)l;
+#pragma unroll
+            for (int tt = 0; tt < 3; ++tt) {
+                const int r = 3 * ci + tt;
+                const float dir[3] = {tt == 1 ? 1.0f : 0.0f, tt == 2 ? 1.0f : 0.0f, tt == 0 ? 1.0f : 0.0f};
+                float f[6];
+                cross3(pc, dir, f);
+                f[3] = dir[0]; f[4] = dir[1]; f[5] = dir[2];
+#pragma unroll
+                for (int q = 0; q < 6; ++q) sm[t.s_rf + 6 * r + q] = f[q];
+                sm[t.s_rl + r] = (float)l;
+                sm[t.s_rb + r] = tt == 0 ? bn : 0.0f;
+                sm[t.s_rk + r] = (float)tt;
+            }
+        }
+    }
+    int nrows = 3 * ncon;
+    {
+        bool act = false;
+        float bl = 0.0f, sg = 0.0f;
+        if (lane < D) {
+            const int l = lane + 1, k = nr + lane;
+            const float lo = m.lower[l], hi = m.upper[l];
+            if (lo < hi) {
+                const float qj = sm[t.s_q + lane];
+                const float qp = qj + dt * us[k];
+                float d = 0.0f;
+                if (qj < lo || qp < lo) { d = qj - lo; sg = 1.0f; act = true; }
+                else if (qj > hi || qp > hi) { d = hi - qj; sg = -1.0f; act = true; }
+                bl = d >= 0.0f ? -d / dt : -p.erp * d / dt;
+                if (bl > p.max_depen) bl = p.max_depen;
+            }
+        }
+        const unsigned long long mask = __ballot(act);
+        if (act) {
+            const int r = nrows + __popcll(mask & ((1ull << lane) - 1ull));
+            sm[t.s_rl + r] = -(float)(nr + lane) - 1.0f;  // negative: limit row on dof
+            sm[t.s_rf + 6 * r] = sg;
+            sm[t.s_rb + r] = bl;
+            sm[t.s_rk + r] = 3.0f;
+        }
+        nrows += __popcll(mask);
+    }
+    __syncthreads();
+
+    STAMP(9);
+    // ---- P9: lanes over rows: J_r, W_r = M~^-1 J_r^T (tree solve in registers), A_rr
+    for (int r = lane; r < nrows; r += 64) {
+        float jr[WNV];
+        const float lk = sm[t.s_rl + r];
+        if (lk >= 0.0f) {
+            const int l = (int)lk;
+            const unsigned long long msk = t.link_mask[l];
+            float f[6];
+#pragma unroll
+            for (int q = 0; q < 6; ++q) f[q] = sm[t.s_rf + 6 * r + q];
+#pragma unroll
+            for (int c = 0; c < WNV; ++c) {
+                float v = 0.0f;
+                if ((msk >> c) & 1ull) {
+                    float s[6];
+#pragma unroll
+                    for (int q = 0; q < 6; ++q) s[q] = Ss[6 * c + q];
+                    v = dot6(s, f);
+                }
+                jr[c] = v;
+            }
+        } else {
+            const int kd = (int)(-lk - 1.0f);
+            const float sg = sm[t.s_rf + 6 * r];
+#pragma unroll
+            for (int c = 0; c < WNV; ++c) jr[c] = c == kd ? sg : 0.0f;
+        }
+        float wr[WNV];
+#pragma unroll
+        for (int c = 0; c < WNV; ++c)
+            if (c < nv) xs[c * 64] = jr[c];
+        tree_solve_lds(t, Mx, Dv, nv, xs);   // W_r = M~^-1 J_r^T
+#pragma unroll
+        for (int c = 0; c < WNV; ++c) wr[c] = c < nv ? xs[c * 64] : 0.0f;
+        float a = 0.0f;
+#pragma unroll
+        for (int c = 0; c < WNV; ++c) a += jr[c] * wr[c];
+        sm[t.s_ad + r] = a > 1e-12f ? a : 1e-12f;
+#pragma unroll
+        for (int c = 0; c < WNV; ++c) { gJ[(size_t)r * WNV + c] = jr[c]; gW[(size_t)r * WNV + c] = wr[c]; }
+    }
+    __syncthreads();
+
+    STAMP(10);
+    // ---- P10: projected Gauss-Seidel. Lane k (mod 32) owns dof k; the wave's lower half
+    // holds J / W of rows 0..63 in registers, the upper half rows 64..127. Rows are swept in
+    // order; only the half owning the current row is active and u is copied across halves
+    // between the two sub-sweeps. Row metadata and lambdas live in lane registers (row r in
+    // lane r % 64, bank r / 64) and are read with readlane.
+    {
+        const int half = lane >> 5, kl = lane & 31;
+        float Jr[64], Wr[64];
+#pragma unroll
+        for (int rr = 0; rr < 64; ++rr) {
+            const int r = rr + 64 * half;
+            const bool ok = r < nrows;
+            Jr[rr] = ok ? gJ[(size_t)r * WNV + kl] : 0.0f;
+            Wr[rr] = ok ? gW[(size_t)r * WNV + kl] : 0.0f;
+        }
+        float b0 = 0, b1 = 0, ia0 = 1, ia1 = 1, k0 = 0, k1 = 0, lam0 = 0.0f, lam1 = 0.0f;
+        if (lane < nrows) { b0 = sm[t.s_rb + lane]; ia0 = 1.0f / sm[t.s_ad + lane]; k0 = sm[t.s_rk + lane]; }
+        if (lane + 64 < nrows) { b1 = sm[t.s_rb + lane + 64]; ia1 = 1.0f / sm[t.s_ad + lane + 64]; k1 = sm[t.s_rk + lane + 64]; }
+        const float mu = p.friction;
+        float u = kl < nv ? us[kl] : 0.0f;
+        for (int it = 0; it < p.iters; ++it) {
+            // opaque per sweep: stops the compiler hoisting 3 x 128 loop-invariant readlanes
+            // out of the iteration loop (they would pin hundreds of SGPRs and spill)
+            asm volatile("" : "+v"(b0), "+v"(b1), "+v"(ia0), "+v"(ia1), "+v"(k0), "+v"(k1));
+#pragma unroll
+            for (int h = 0; h < 2; ++h) {
+                if (64 * h >= nrows) continue;
+                const float bb = h ? b1 : b0, ii = h ? ia1 : ia0, kk = h ? k1 : k0;
+                // fully unrolled (no early exit) so Jr / Wr stay register-indexed
+#pragma unroll
+                for (int rr = 0; rr < 64; ++rr) {
+                    const int r = rr + 64 * h;
+                    if (r >= nrows) continue;
+                    // keep each row's readlanes inside its own row (no SGPR hoisting)
+                    __builtin_amdgcn_sched_barrier(0);
+                    const float s = half_sums(Jr[rr] * u);
+                    const float jv = readlane(s, h ? 63 : 31);
+                    const float br = readlane(bb, rr), iar = readlane(ii, rr);
+                    const int kind = (int)readlane(kk, rr);
+                    const float l0 = readlane(h ? lam1 : lam0, rr);
+                    float ln = l0 + (br - jv) * iar;
+                    if (kind == 1 || kind == 2) {
+                        const int rn = r - kind;
+                        const float ln_n = rn >= 64 ? readlane(lam1, rn - 64) : readlane(lam0, rn);
+                        const float lim = mu * ln_n;
+                        ln = ln > lim ? lim : (ln < -lim ? -lim : ln);
+                    } else {
+                        ln = ln > 0.0f ? ln : 0.0f;
+                    }
+                    const float dl = ln - l0;
+                    if (half == h) u += Wr[rr] * dl;
+                    if (lane == rr) { if (h) lam1 = ln; else lam0 = ln; }
+                }
+                // hand u to the other half for its sub-sweep
+                u = __shfl(u, kl + 32 * h, 64);
+            }
+        }
+        if (lane < nv) us[lane] = u;
+        if (lane < nrows) sm[t.s_ad + lane] = lam0;          // reuse: lambda of row lane
+        if (lane + 64 < nrows) sm[t.s_ad + lane + 64] = lam1;
+    }
+    __syncthreads();
+
+    STAMP(11);
+    // ---- P11a: force sensors (lane s)
+    if (lane < m.S) {
+        const int si = lane, l = m.sensor_link[si];
+        float R[9], xs[3], F[3] = {0, 0, 0}, T[3] = {0, 0, 0};
+#pragma unroll
+        for (int q = 0; q < 9; ++q) R[q] = sm[t.s_R + 9 * l + q];
+        m3_vec(R, m.sensor_pos + 3 * si, xs);
+#pragma unroll
+        for (int q = 0; q < 3; ++q) xs[q] += sm[t.s_o + 3 * l + q];
+        for (int c = 0; c < ncon; ++c) {
+            if ((int)sm[t.s_cl + c] != l) continue;
+            const float* lam = sm + t.s_ad;
+            const float fc[3] = {lam[3 * c + 1] / dt, lam[3 * c + 2] / dt, lam[3 * c] / dt};
+            float rr[3], tc[3];
+#pragma unroll
+            for (int q = 0; q < 3; ++q) rr[q] = sm[t.s_cp + 3 * c + q] - xs[q];
+            cross3(rr, fc, tc);
+#pragma unroll
+            for (int q = 0; q < 3; ++q) { F[q] += fc[q]; T[q] += tc[q]; }
+        }
+        float Fl[3], Tl[3];
+        m3_tvec(R, F, Fl);
+        m3_tvec(R, T, Tl);
+#pragma unroll
+        for (int q = 0; q < 3; ++q) {
+            st.sens[(size_t)(6 * si + q) * N + i] = Fl[q];
+            st.sens[(size_t)(6 * si + 3 + q) * N + i] = Tl[q];
+        }
+    }
+    // ---- P11b: integrate; non-finite -> nan flag
+    bool finite = true;
+    if (lane < D) {
+        const float v = us[nr + lane];
+        const float qn = sm[t.s_q + lane] + dt * v;
+        st.qd[(size_t)lane * N + i] = v;
+        st.q[(size_t)lane * N + i] = qn;
+        finite = isfinite(v) && isfinite(qn);
+    }
+    if (nr && lane == 0) {
+        float u6[6], rp[3], rq[4];
+#pragma unroll
+        for (int k = 0; k < 6; ++k) u6[k] = us[k];
+#pragma unroll
+        for (int k = 0; k < 3; ++k) rp[k] = sm[t.s_rp + k];
+#pragma unroll
+        for (int k = 0; k < 4; ++k) rq[k] = sm[t.s_rp + 4 + k];
+        float* om = u6 + 3;
+        float wn = sqrtf(dot3(om, om));
+        if (wn > p.max_angvel) {
+            const float sc = p.max_angvel / wn;
+            om[0] *= sc; om[1] *= sc; om[2] *= sc;
+            wn = p.max_angvel;
+        }
+#pragma unroll
+        for (int k = 0; k < 3; ++k) rp[k] += dt * u6[k];
+        const float th = wn * dt;
+        if (th > 0.0f) {
+            float sh, ch;
+            sincosf(0.5f * th, &sh, &ch);
+            sh = sh / wn;
+            const float w0 = ch, x0 = om[0] * sh, y0 = om[1] * sh, z0 = om[2] * sh;
+            const float w1 = rq[0], x1 = rq[1], y1 = rq[2], z1 = rq[3];
+            float nq[4] = {w0 * w1 - x0 * x1 - y0 * y1 - z0 * z1,
+                           w0 * x1 + x0 * w1 + y0 * z1 - z0 * y1,
+                           w0 * y1 - x0 * z1 + y0 * w1 + z0 * x1,
+                           w0 * z1 + x0 * y1 - y0 * x1 + z0 * w1};
+            const float nn = 1.0f / sqrtf(nq[0] * nq[0] + nq[1] * nq[1] + nq[2] * nq[2] + nq[3] * nq[3]);
+#pragma unroll
+            for (int k = 0; k < 4; ++k) rq[k] = nq[k] * nn;
+        }
+#pragma unroll
+        for (int k = 0; k < 3; ++k) { st.root_pos[(size_t)k * N + i] = rp[k]; finite &= isfinite(rp[k]); }
+#pragma unroll
+        for (int k = 0; k < 4; ++k) { st.root_quat[(size_t)k * N + i] = rq[k]; finite &= isfinite(rq[k]); }
+#pragma unroll
+        for (int k = 0; k < 6; ++k) { st.root_vel[(size_t)k * N + i] = u6[k]; finite &= isfinite(u6[k]); }
+    }
+    if (__any(!finite) && lane == 0) st.nan_flag[i] = 1;
+    __syncthreads();
+    STAMP(12);
+}
+
+}  // namespace mi

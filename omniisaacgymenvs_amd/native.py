@@ -13,7 +13,7 @@ from typing import Optional
 import numpy as np
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "libmi_sim.so")
+LIB_PATH = os.environ.get("MI_SIM_LIB", os.path.join(_HERE, "libmi_sim.so"))
 
 MI_OK = 0
 MI_TASK_CARTPOLE, MI_TASK_ANT, MI_TASK_HUMANOID = 0, 1, 2

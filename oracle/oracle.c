@@ -208,6 +208,7 @@ struct orc_sim {
     uint32_t* reset_count;
     int32_t* nan_flag;
     int64_t nan_total;
+    float* margin; /* per env: ws_t.margin over the last physics call */
 };
 
 static int g_threads = 1;
@@ -277,6 +278,7 @@ orc_sim* orc_sim_create(const mi_model_desc* md, const mi_sim_params* params, in
     s->sens = (float*)dupmem(NULL, (size_t)N * S * 24);
     s->reset_count = (uint32_t*)dupmem(NULL, (size_t)N * 4);
     s->nan_flag = (int32_t*)dupmem(NULL, (size_t)N * 4);
+    s->margin = (float*)dupmem(NULL, (size_t)N * 4);
     for (int i = 0; i < N; ++i) {
         s->root_quat[4 * i] = 1.0f;
         for (int c = 0; c < 3; ++c) s->root_pos[3 * i + c] = s->origins[3 * i + c];
@@ -291,7 +293,7 @@ void orc_sim_destroy(orc_sim* s) {
                     m->lower, m->upper, m->damping, m->armature, m->geom_link, m->geom_type,
                     m->geom_p0, m->geom_p1, m->geom_radius, m->sensor_link, m->sensor_pos,
                     m->pairs, m->pt_geom, m->pt_end, s->origins, s->root_pos, s->root_quat,
-                    s->root_vel, s->q, s->qd, s->eff, s->sens, s->reset_count, s->nan_flag};
+                    s->root_vel, s->q, s->qd, s->eff, s->sens, s->reset_count, s->nan_flag, s->margin};
     for (size_t i = 0; i < sizeof ptrs / sizeof ptrs[0]; ++i) free(ptrs[i]);
     free(s);
 }
@@ -360,6 +362,7 @@ typedef struct {
     float *Jr, *W, *b, *lam, *Ad, *cpt;
     int *rkind, *rcon, *clink;
     int nrows, ncon;
+    float margin; /* min distance of any activation decision from its threshold (test aid) */
 } ws_t;
 
 static ws_t* ws_new(const model_t* m) {
@@ -616,6 +619,7 @@ static void artic_substep(const model_t* m, const mi_sim_params* p, ws_t* w, flo
         for (int k = 0; k < 3; ++k) x[k] += w->o[3 * l + k];
         float r = m->geom_radius[g];
         float gap = rp[2] + x[2] - r;
+        w->margin = fminf(w->margin, fabsf(gap - p->contact_offset));
         if (!(gap < p->contact_offset)) continue;
         float pc[3] = {x[0], x[1], x[2] - r};
         float d = gap - p->rest_offset;
@@ -641,6 +645,8 @@ static void artic_substep(const model_t* m, const mi_sim_params* p, ws_t* w, flo
         float lo = m->lower[l], hi = m->upper[l];
         if (!(lo < hi)) continue;
         float qp = q[j] + dt * u[k];
+        w->margin = fminf(w->margin, fminf(fminf(fabsf(q[j] - lo), fabsf(qp - lo)),
+                                           fminf(fabsf(q[j] - hi), fabsf(qp - hi))));
         float d, sg;
         if (q[j] < lo || qp < lo) { d = q[j] - lo; sg = 1.0f; }
         else if (q[j] > hi || qp > hi) { d = hi - q[j]; sg = -1.0f; }
@@ -784,6 +790,7 @@ static void env_physics(orc_sim* s, ws_t* w, int i, int substeps) {
     float* q = s->q + (size_t)D * i;
     float* qd = s->qd + (size_t)D * i;
     const float* eff = s->eff + (size_t)D * i;
+    w->margin = INFINITY;
     for (int st = 0; st < substeps; ++st) {
         if (m->dyn == MI_DYN_CARTPOLE)
             cartpole_substep(m, &s->p, q, qd, eff);
@@ -793,7 +800,13 @@ static void env_physics(orc_sim* s, ws_t* w, int i, int substeps) {
     }
     if (!is_finite_state(D, s->root_pos + 3 * i, s->root_quat + 4 * i, s->root_vel + 6 * i, q, qd))
         s->nan_flag[i] = 1;
+    s->margin[i] = w->margin;
 }
+
+/* Per env: how close (in metres / radians) any contact or joint-limit activation decision of
+ * the last physics call came to its threshold. Test aid: a device whose float summation
+ * order differs can take the other branch only where this is within rounding. */
+void orc_decision_margin(const orc_sim* s, float* out) { memcpy(out, s->margin, (size_t)s->N * 4); }
 
 void orc_sim_step(orc_sim* s, int substeps) {
 #pragma omp parallel num_threads(g_threads)

@@ -66,6 +66,7 @@ def lib() -> C.CDLL:
             "orc_energy": (C.c_double, [C.c_void_p, C.c_int]),
             "orc_momentum": (None, [C.c_void_p, C.c_int, C.POINTER(C.c_double)]),
             "orc_contact_count": (C.c_int, [C.c_void_p, C.c_int]),
+            "orc_decision_margin": (None, [C.c_void_p, C.c_void_p]),
         }
         for name, (res, args) in sig.items():
             fn = getattr(L, name)
@@ -214,6 +215,13 @@ class OracleSim:
 
     def contact_count(self, env: int) -> int:
         return int(lib().orc_contact_count(self.h, env))
+
+    def decision_margin(self) -> np.ndarray:
+        """[N] min |x - threshold| over every contact / limit activation test of the last
+        physics call (contact gap vs contact_offset, q and q + dt*qd vs limits)."""
+        out = np.empty(self.N, np.float32)
+        lib().orc_decision_margin(self.h, out.ctypes.data)
+        return out
 
     def nan_count(self) -> int:
         return int(lib().orc_nan_count(self.h))

@@ -11,6 +11,7 @@ import torch
 
 from omniisaacgymenvs_amd import native as N
 from omniisaacgymenvs_amd.utils.task_util import make_env
+from oracle import oracle as oracle_mod
 from oracle.oracle import lib as orc_lib
 from tests.helpers import oracle_twin, rand_actions, sync_oracle, task_buffers
 
@@ -93,28 +94,17 @@ def test_task_math_from_identical_state(env_pair):
     # device: the modular post_physics_step (progress += 1, obs, reward, done)
     task.post_physics_step()
     torch.cuda.synchronize()
-    rq_, rp_, rv_ = None, None, None
     p_orc, r_orc, v_orc = orc.root_state()
     q_orc, qd_orc = orc.dof_state()
     if name == "Cartpole":
-        orc_lib().orc_cartpole_post_math(__import__("ctypes").byref(task.task_params()), n,
-                                         *(x.ctypes.data_as(__import__("ctypes").POINTER(__import__("ctypes").c_float)) for x in (q_orc, qd_orc, b["obs"], b["rew"])),
-                                         b["reset"].ctypes.data_as(__import__("ctypes").POINTER(__import__("ctypes").c_int64)),
-                                         b["progress"].ctypes.data_as(__import__("ctypes").POINTER(__import__("ctypes").c_int64)))
+        ref = oracle_mod.cartpole_post_math(task.task_params(), q_orc, qd_orc, b["reset"], b["progress"])
     else:
-        import ctypes as C
-        fp = lambda a: np.ascontiguousarray(a, np.float32).ctypes.data_as(C.POINTER(C.c_float))
         lim = task.model.dof_limits()
-        lo, hi = np.ascontiguousarray(lim[:, 0]), np.ascontiguousarray(lim[:, 1])
         sens = np.zeros((n, task.model.num_sensors, 6), np.float32)
-        a_np = np.ascontiguousarray(acts.numpy(), np.float32)
-        tp = task.task_params()
-        keep = [p_orc, r_orc, v_orc, q_orc, qd_orc, sens, a_np, lo, hi]
-        orc_lib().orc_loco_post_math(C.byref(tp), n, task.model.num_dof, task.model.num_sensors,
-                                     *(fp(x) for x in keep), fp(b["obs"]), fp(b["rew"]),
-                                     b["reset"].ctypes.data_as(C.POINTER(C.c_int64)),
-                                     b["progress"].ctypes.data_as(C.POINTER(C.c_int64)),
-                                     fp(b["pot"]), fp(b["prev"]))
+        ref = oracle_mod.loco_post_math(task.task_params(), p_orc, r_orc, v_orc, q_orc, qd_orc, sens,
+                                        acts.numpy(), lim[:, 0], lim[:, 1], b["reset"], b["progress"],
+                                        b["pot"], b["prev"])
+    b.update(ref)
     obs = task.obs_buf.cpu().numpy()
     if name != "Cartpole":
         obs[:, 12 + 2 * task.model.num_dof: 12 + 2 * task.model.num_dof + 6 * task.model.num_sensors] = 0
@@ -124,6 +114,34 @@ def test_task_math_from_identical_state(env_pair):
     assert np.array_equal(task.progress_buf.cpu().numpy(), b["progress"])
     if name == "Cartpole":
         np.testing.assert_allclose(task.rew_buf.cpu().numpy(), b["rew"], rtol=1e-5, atol=1e-5)
+
+
+def _sensor_cols(task):
+    D, S = task.model.num_dof, task.model.num_sensors
+    return slice(12 + 2 * D, 12 + 2 * D + 6 * S)
+
+
+# A contact / limit activation decision taken within this distance (m or rad) of its threshold
+# may go either way under a different float summation order (contact model discontinuity).
+DECISION_EPS = 1e-4
+
+
+def check_pair(name, task, obs, rew, obs_ref, rew_ref, tol, margin):
+    """Per-env parity. Every env must agree to `tol` on all observations and the reward,
+    except envs whose oracle `margin` (closest activation decision to its threshold during
+    the step, OracleSim.decision_margin) is below DECISION_EPS: there the discrete branch may
+    legitimately differ. Such envs must stay rare (< 2 %)."""
+    bad = ~np.all(np.isclose(obs, obs_ref, rtol=tol, atol=tol), axis=1)
+    bad |= ~np.isclose(rew, rew_ref, rtol=tol, atol=tol)
+    if name == "Cartpole":
+        assert not bad.any(), f"{name}: envs {np.nonzero(bad)[0]}"
+        return
+    near = margin < DECISION_EPS
+    unexplained = bad & ~near
+    assert not unexplained.any(), (
+        f"{name}: envs {np.nonzero(unexplained)[0]} differ with decision margins "
+        f"{margin[unexplained]}")
+    assert bad.mean() < 0.02, f"{name}: {bad.sum()} envs at a threshold differ"
 
 
 def test_fused_env_step_matches_oracle(env_pair):
@@ -139,10 +157,9 @@ def test_fused_env_step_matches_oracle(env_pair):
         obs_dict, rew, resets, _ = env.step(acts.to("cuda:0"))
         torch.cuda.synchronize()
         orc.env_step(acts.numpy(), task.control_frequency_inv, b)
-        obs = obs_dict["obs"].cpu().numpy()
         tol = 1e-4 if name == "Cartpole" else 2e-3
-        np.testing.assert_allclose(obs, b["obs"], rtol=tol, atol=tol, err_msg=f"{name} step {step}")
-        np.testing.assert_allclose(rew.cpu().numpy(), b["rew"], rtol=tol, atol=tol)
+        check_pair(name, task, obs_dict["obs"].cpu().numpy(), rew.cpu().numpy(), b["obs"], b["rew"],
+                   tol, orc.decision_margin())
         assert np.array_equal(resets.cpu().numpy(), b["reset"])
         assert np.array_equal(task.progress_buf.cpu().numpy(), b["progress"])
         sync_oracle(env, orc)   # re-align (chaotic contact dynamics)
@@ -162,6 +179,28 @@ def test_fused_equals_modular(gpu):
             torch.cuda.synchronize()
             np.testing.assert_allclose(oa["obs"].cpu().numpy(), ob["obs"].cpu().numpy(), rtol=1e-5, atol=1e-5)
             np.testing.assert_allclose(ra.cpu().numpy(), rb.cpu().numpy(), rtol=1e-5, atol=1e-5)
+            assert torch.equal(da, db)
+        ea.close()
+        eb.close()
+
+
+def test_wave_path_matches_thread_path(gpu, monkeypatch):
+    """Wavefront-per-env kernel (default) vs the one-lane-per-env reference kernel."""
+    for name in ("Ant", "Humanoid"):
+        ea = make_env(name, num_envs=128, device="cuda:0", seed=31)
+        monkeypatch.setenv("MI_SIM_PATH", "thread")
+        eb = make_env(name, num_envs=128, device="cuda:0", seed=31)
+        monkeypatch.delenv("MI_SIM_PATH")
+        orc = oracle_twin(ea, 31)   # only to measure decision margins of the same state
+        for step in range(3):
+            acts = rand_actions(128, ea.num_actions, 50 + step)
+            sync_oracle(ea, orc)
+            orc.env_step(acts.numpy(), ea.task.control_frequency_inv, task_buffers(ea))
+            oa, ra, da, _ = ea.step(acts.to("cuda:0"))
+            ob, rb, db, _ = eb.step(acts.to("cuda:0"))
+            torch.cuda.synchronize()
+            check_pair(name, ea.task, oa["obs"].cpu().numpy(), ra.cpu().numpy(), ob["obs"].cpu().numpy(),
+                       rb.cpu().numpy(), 2e-3, orc.decision_margin())
             assert torch.equal(da, db)
         ea.close()
         eb.close()
