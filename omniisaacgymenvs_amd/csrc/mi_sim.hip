@@ -63,6 +63,7 @@ struct mi_sim {
     DevTask tp{};
     bool task_ok = false;
     bool wave = false;      // wavefront-per-env articulation path (mi_wave.hpp)
+    int topo = 0;           // generated compile-time topology id (0: runtime tables)
     WaveTabs wt{};
     float* rows = nullptr;  // per-env global constraint-row slab of the wave path
     size_t lds_bytes = 0;
@@ -230,6 +231,28 @@ struct KParams {
     float* rows;
 };
 
+// launch with the model's compile-time topology (mi_topo_gen.hpp) or the runtime tables
+template <class F>
+static void with_topo(int id, F&& f) {
+    switch (id) {
+        case RobotHumanoid::id: f(TopoCT<RobotHumanoid>{}); break;
+        case RobotAnt::id: f(TopoCT<RobotAnt>{}); break;
+        default: f(TopoRuntime{}); break;
+    }
+}
+
+// id of the generated topology whose link tree equals the model's (0: none)
+static int match_topology(const mi_model_desc* md) {
+    const int nr = md->root_free ? 6 : 0;
+    for (const GenTopo& g : kGenTopos) {
+        if (g.L != md->num_links || g.nr != nr) continue;
+        bool same = true;
+        for (int l = 1; l < g.L && same; ++l) same = g.link_parent[l] == md->parent[l];
+        if (same) return g.id;
+    }
+    return 0;
+}
+
 static int sync_kparams(mi_sim* s) {
     if (!s->wave) return MI_OK;
     KParams h{};
@@ -244,6 +267,15 @@ static int sync_kparams(mi_sim* s) {
     return MI_OK;
 }
 
+// The parameter block is loop-invariant across substeps; laundering its pointer per substep
+// keeps the compiler from hoisting every field it reads into SGPRs for the whole loop
+// (hundreds of values, spilled to VGPR lanes). Fields are re-read (scalar cache hits).
+__device__ __forceinline__ const KParams* opaque_kp(const KParams* kp) {
+    asm volatile("" : "+s"(kp));
+    return kp;
+}
+
+template <class T>
 __global__ __launch_bounds__(64) void k_sim_step_wave(const KParams* __restrict__ kp, int substeps) {
     extern __shared__ __attribute__((aligned(16))) float smem[];
     const DevModel& m = kp->m;
@@ -251,11 +283,14 @@ __global__ __launch_bounds__(64) void k_sim_step_wave(const KParams* __restrict_
     const DevState& st = kp->st;
     const SimP& p = kp->p;
     const int i = blockIdx.x;
-    float* gJ = kp->rows + (size_t)i * t.g_row_stride;
-    float* gW = gJ + (size_t)t.max_rows * WNV;
-    for (int s = 0; s < substeps; ++s) wave_artic_substep(m, t, st, p, i, smem, gJ, gW);
+    float* gW = kp->rows + (size_t)i * t.g_row_stride;
+    for (int s = 0; s < substeps; ++s) {
+        const KParams* k = opaque_kp(kp);
+        wave_artic_substep<T>(k->m, k->t, k->st, k->p, i, smem, gW);
+    }
 }
 
+template <class T>
 __global__ __launch_bounds__(64) void k_env_step_wave(const KParams* __restrict__ kp,
                                                       const float* actions, int substeps,
                                                       float* obs_out, float* obs_task, float* rew,
@@ -275,9 +310,11 @@ __global__ __launch_bounds__(64) void k_env_step_wave(const KParams* __restrict_
         task_pre_env(m, st, tp, i, actions, reset_buf, progress_buf, pot, prev, actions_out, true);
     __syncthreads();
     // 2. controlFrequencyInv x World.step, wave-cooperative
-    float* gJ = rows + (size_t)i * t.g_row_stride;
-    float* gW = gJ + (size_t)t.max_rows * WNV;
-    for (int s = 0; s < substeps; ++s) wave_artic_substep(m, t, st, p, i, smem, gJ, gW);
+    float* gW = rows + (size_t)i * t.g_row_stride;
+    for (int s = 0; s < substeps; ++s) {
+        const KParams* k = opaque_kp(kp);
+        wave_artic_substep<T>(k->m, k->t, k->st, k->p, i, smem, gW);
+    }
     // 3. post_physics_step + obs clamp (lane 0)
     if (lane == 0) {
         const int O = tp.O;
@@ -471,6 +508,8 @@ int mi_sim_create(const mi_model_desc* md, const mi_sim_params* prm, int32_t N, 
                   m.max_rows <= 128 && L <= 64;
     }
     if (s->wave) {
+        const char* tsel = getenv("MI_SIM_TOPO");
+        s->topo = (tsel && std::string(tsel) == "runtime") ? 0 : match_topology(md);
         WaveTabs& t = s->wt;
         std::vector<int> depth(L, 0);
         int maxd = 0;
@@ -546,7 +585,7 @@ int mi_sim_create(const mi_model_desc* md, const mi_sim_params* prm, int32_t N, 
                 if (offs[c] <= offs[c - 1]) return cleanup(fail(MI_E_STATE, "wave LDS layout: region %zu overlaps", c));
         }
         t.max_rows = m.max_rows;
-        t.g_row_stride = (size_t)2 * m.max_rows * WNV;
+        t.g_row_stride = (size_t)128 * WNV;   // padded: PGS loads all 128 row slots
         s->lds_bytes = (size_t)so * sizeof(float);
     }
     s->lower.assign(md->lower, md->lower + L);
@@ -695,8 +734,10 @@ int mi_sim_step(mi_sim* s, int32_t substeps, void* stream) {
     if (substeps < 0 || substeps > 64) return fail(MI_E_ARG, "substeps %d out of range", substeps);
     HIP_TRY(hipSetDevice(s->device));
     if (s->wave)
-        hipLaunchKernelGGL(k_sim_step_wave, dim3(s->N), dim3(64), s->lds_bytes, STREAM(stream),
-                           (const KParams*)s->kp_dev, substeps);
+        with_topo(s->topo, [&](auto T) {
+            hipLaunchKernelGGL(k_sim_step_wave<decltype(T)>, dim3(s->N), dim3(64), s->lds_bytes,
+                               STREAM(stream), (const KParams*)s->kp_dev, substeps);
+        });
     else
         hipLaunchKernelGGL(k_sim_step, grid_for(s, s->N), dim3(s->block), 0, STREAM(stream), s->dm,
                            s->ds, s->sp, substeps);
@@ -823,9 +864,12 @@ int mi_env_step(mi_sim* s, const float* actions, int32_t substeps, float* obs_ou
     if (substeps < 0 || substeps > 64) return fail(MI_E_ARG, "substeps %d out of range", substeps);
     HIP_TRY(hipSetDevice(s->device));
     if (s->wave && s->tp.kind != MI_TASK_CARTPOLE)
-        hipLaunchKernelGGL(k_env_step_wave, dim3(s->N), dim3(64), s->lds_bytes, STREAM(stream),
-                           (const KParams*)s->kp_dev, actions, substeps, obs_out, obs_task, rew,
-                           reset_buf, progress_buf, potentials, prev_potentials, actions_out);
+        with_topo(s->topo, [&](auto T) {
+            hipLaunchKernelGGL(k_env_step_wave<decltype(T)>, dim3(s->N), dim3(64), s->lds_bytes,
+                               STREAM(stream), (const KParams*)s->kp_dev, actions, substeps,
+                               obs_out, obs_task, rew, reset_buf, progress_buf, potentials,
+                               prev_potentials, actions_out);
+        });
     else
         hipLaunchKernelGGL(k_env_step, grid_for(s, s->N), dim3(s->block), 0, STREAM(stream), s->dm,
                            s->ds, s->sp, s->tp, actions, substeps, obs_out, obs_task, rew, reset_buf,
@@ -859,6 +903,13 @@ int mi_sim_nan_count(mi_sim* s, int64_t* count) {
     unsigned long long v = 0;
     HIP_TRY(hipMemcpy(&v, s->ds.nan_total, sizeof v, hipMemcpyDeviceToHost));
     *count = (int64_t)v;
+    return MI_OK;
+}
+
+int mi_sim_kernel_path(const mi_sim* s, int32_t* path, int32_t* topology) {
+    NEED(s); NEED(path); NEED(topology);
+    *path = s->wave ? 1 : 0;
+    *topology = s->wave ? s->topo : 0;
     return MI_OK;
 }
 

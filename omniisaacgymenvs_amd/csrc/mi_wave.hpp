@@ -23,6 +23,7 @@
 #pragma once
 #include "mi_artic.hpp"
 #include "mi_device.hpp"
+#include "mi_topo_gen.hpp"
 
 namespace mi {
 
@@ -113,6 +114,100 @@ MI_D void tree_solve_lds(const WaveTabs& t, const float* Mx, const float* Dinv, 
         }
         xs[i * 64] = xi;
     }
+}
+
+// ---- compile-time-topology (CT) tree kernels --------------------------------------------
+// Layout: lane c holds column c of M~ in Mc[0..nv-1] (Mc[r] = M~[r][c], lower triangle and
+// tree pattern only; every other entry exactly 0). Factor entries are broadcast with
+// v_readlane at compile-time (register, lane) pairs, so no LDS or barrier is involved.
+// Arithmetic is operation-for-operation that of the runtime-table path above.
+
+// Mc[r] <- Mx[r][lane] for lane == r or lane an ancestor of r, else 0
+// An opaque copy of the lane id: lane-compare masks built from it cannot be hoisted out of
+// the unrolled step that uses them (dozens of hoisted 64-bit masks would spill SGPRs).
+MI_D int lane_here(int lane) {
+    asm volatile("" : "+v"(lane));
+    return lane;
+}
+
+template <class T>
+MI_D void ct_load_columns(const float* Mx, int lane, float (&Mc)[T::nvc]) {
+    const int c = lane < T::nv ? lane : 0;
+    sfor<0, T::nv>([&](auto R) {
+        constexpr int r = R;
+        constexpr unsigned long long keep = (unsigned long long)T::dof.anc_mask[r] | (1ull << r);
+        Mc[r] = ((keep >> lane_here(lane)) & 1ull) ? Mx[r * T::nv + c] : 0.0f;
+    });
+}
+
+// in-register tree LTDL: M~ = L^T D L, L strictly below the diagonal, D on it
+template <class T>
+MI_D void ct_ltdl(int lane, float (&Mc)[T::nvc]) {
+    sfor_down<0, T::nv>([&](auto K) {
+        constexpr int k = K;
+        __builtin_amdgcn_sched_barrier(0);
+        const int ln = lane_here(lane);
+        const float inv = 1.0f / readlane(Mc[k], k);
+        sfor<T::dof.anc_start[k], T::dof.anc_start[k + 1]>([&](auto A) {
+            constexpr int ii = T::dof.anc[A];
+            const float s = readlane(Mc[k], ii) * inv;
+            if (ln <= ii) Mc[ii] -= s * Mc[k];
+        });
+        if (ln < k) Mc[k] = Mc[k] * inv;
+    });
+}
+
+// lane c: 1 / D_c (lanes >= nv: unused)
+template <class T>
+MI_D float ct_dinv(int lane, const float (&Mc)[T::nvc]) {
+    float dg = 1.0f;
+    sfor<0, T::nv>([&](auto I) { dg = lane_here(lane) == I ? Mc[I] : dg; });
+    return 1.0f / dg;
+}
+
+template <class T>
+MI_D void ct_opaque(float (&Mc)[T::nvc]) {
+#pragma unroll
+    for (int i = 0; i < T::nv; ++i) asm volatile("" : "+v"(Mc[i]));
+}
+
+// x <- M~^-1 x on a lane-private register vector. Mc is made opaque before each pass so the
+// compiler re-issues the factor readlanes where they are used instead of keeping hundreds
+// of them live in SGPRs (which spill).
+// Step fence for the unrolled solves: every element of x and the factor column used next
+// pass through empty volatile asm (ordered among themselves), so the next step's readlanes
+// cannot be issued before this step's FMAs have consumed theirs. Without it the scheduler
+// front-loads ~200 readlanes into SGPRs and spills them. No instructions are emitted.
+template <class T>
+MI_D void ct_step_fence(float (&x)[T::nvc], float& mcol) {
+#pragma unroll
+    for (int c = 0; c < T::nv; ++c) asm volatile("" : "+v"(x[c]));
+    asm volatile("" : "+v"(mcol));
+}
+
+// x <- M~^-1 x on a lane-private register vector (same operation order as tree_solve_lds)
+template <class T>
+MI_D void ct_solve(float (&Mc)[T::nvc], float dvec, float (&x)[T::nvc]) {
+    sfor_down<0, T::nv>([&](auto I) {                 // x <- L^-T x (leaves -> root)
+        constexpr int i = I;
+        ct_step_fence<T>(x, Mc[i]);
+        const float xi = x[i];
+        sfor<T::dof.anc_start[i], T::dof.anc_start[i + 1]>([&](auto A) {
+            constexpr int j = T::dof.anc[A];
+            x[j] -= readlane(Mc[i], j) * xi;
+        });
+    });
+    sfor<0, T::nv>([&](auto I) { x[I] *= readlane(dvec, I); });   // x <- D^-1 x
+    sfor<0, T::nv>([&](auto I) {                      // x <- L^-1 x (root -> leaves)
+        constexpr int i = I;
+        ct_step_fence<T>(x, Mc[i]);
+        float xi = x[i];
+        sfor<T::dof.anc_start[i], T::dof.anc_start[i + 1]>([&](auto A) {
+            constexpr int j = T::dof.anc[A];
+            xi -= readlane(Mc[i], j) * x[j];
+        });
+        x[i] = xi;
+    });
 }
 
 // P1a: local joint transform of link l >= 1 (independent of every other link):
@@ -251,9 +346,10 @@ MI_D void wave_link_dynamics(const DevModel& m, const WaveTabs& t, float* sm, in
 }
 
 // One articulated substep of env i, executed by the whole 64-lane workgroup.
-// sm: this env's LDS region; gJ / gW: this env's global row slab [max_rows][WNV] each.
+// sm: this env's LDS region; gW: this env's global slab of W rows [max_rows][WNV].
+template <class TP>
 MI_D void wave_artic_substep(const DevModel& m, const WaveTabs& t, const DevState& st,
-                             const SimP& p, int i, float* sm, float* gJ, float* gW) {
+                             const SimP& p, int i, float* sm, float* gW) {
     const int lane = threadIdx.x;
     const int N = st.N, L = m.L, D = m.D, nv = m.nv, nr = m.nr;
     const float dt = p.dt;
@@ -344,33 +440,53 @@ MI_D void wave_artic_substep(const DevModel& m, const WaveTabs& t, const DevStat
     __syncthreads();
     STAMP(4);
     // ---- P4: LTDL in place (M = L^T D L, L strictly below the diagonal)
-    for (int k = nv - 1; k >= 0; --k) {
-        const int a0 = t.anc_start[k], na = t.anc_start[k + 1] - a0;
-        const float inv = 1.0f / Mx[k * nv + k];
-        const int npair = na * (na + 1) / 2;
-        for (int pi = lane; pi < npair; pi += 64) {
-            const int ii = t.anc_list[a0 + t.tri_p[pi]], jj = t.anc_list[a0 + t.tri_q[pi]];
-            Mx[ii * nv + jj] -= (Mx[k * nv + ii] * inv) * Mx[k * nv + jj];
+    float Mc[TP::nvc];     // CT path: column `lane` of M~, then of its factor (rows 0..nv-1)
+    float dvec = 1.0f;    // CT path: lane c holds 1 / D_c
+    if constexpr (TP::kCT) {
+        ct_load_columns<TP>(Mx, lane, Mc);
+        ct_ltdl<TP>(lane, Mc);
+        dvec = ct_dinv<TP>(lane, Mc);
+    } else {
+        for (int k = nv - 1; k >= 0; --k) {
+            const int a0 = t.anc_start[k], na = t.anc_start[k + 1] - a0;
+            const float inv = 1.0f / Mx[k * nv + k];
+            const int npair = na * (na + 1) / 2;
+            for (int pi = lane; pi < npair; pi += 64) {
+                const int ii = t.anc_list[a0 + t.tri_p[pi]], jj = t.anc_list[a0 + t.tri_q[pi]];
+                Mx[ii * nv + jj] -= (Mx[k * nv + ii] * inv) * Mx[k * nv + jj];
+            }
+            __syncthreads();
+            if (lane < na) {
+                const int ii = t.anc_list[a0 + lane];
+                Mx[k * nv + ii] = Mx[k * nv + ii] * inv;
+            }
+            __syncthreads();
         }
-        __syncthreads();
-        if (lane < na) {
-            const int ii = t.anc_list[a0 + lane];
-            Mx[k * nv + ii] = Mx[k * nv + ii] * inv;
-        }
-        __syncthreads();
     }
     STAMP(5);
     // ---- P5: 1/D of the factor
-    if (lane < nv) Dv[lane] = 1.0f / Mx[lane * nv + lane];
-    __syncthreads();
+    if constexpr (!TP::kCT) {
+        if (lane < nv) Dv[lane] = 1.0f / Mx[lane * nv + lane];
+        __syncthreads();
+    }
     STAMP(6);
     STAMP(7);
-    // ---- P7: u* = u + dt M~^-1 rhs (one lane, register-resident tree solve)
-    float* xs = sm + t.s_xs + lane;   // this lane's private solve vector (stride 64)
-    if (lane == 0) {
-        for (int c = 0; c < nv; ++c) xs[c * 64] = rhs[c];
-        tree_solve_lds(t, Mx, Dv, nv, xs);
-        for (int c = 0; c < nv; ++c) us[c] = us[c] + dt * xs[c * 64];
+    // ---- P7: u* = u + dt M~^-1 rhs
+    float* xs = sm + t.s_xs + lane;   // generic path: this lane's private solve vector (stride 64)
+    if constexpr (TP::kCT) {
+        float x[TP::nvc];              // every lane solves the same vector (LDS broadcasts)
+        sfor<0, TP::nv>([&](auto I) { x[I] = rhs[I]; });
+        // opaque: a provably uniform vector would be solved in SGPRs (and spill)
+#pragma unroll
+        for (int c = 0; c < TP::nv; ++c) asm volatile("" : "+v"(x[c]));
+        ct_solve<TP>(Mc, dvec, x);
+        if (lane == 0) sfor<0, TP::nv>([&](auto I) { us[I] = us[I] + dt * x[I]; });
+    } else {
+        if (lane == 0) {
+            for (int c = 0; c < nv; ++c) xs[c * 64] = rhs[c];
+            tree_solve_lds(t, Mx, Dv, nv, xs);
+            for (int c = 0; c < nv; ++c) us[c] = us[c] + dt * xs[c * 64];
+        }
     }
     __syncthreads();
 
@@ -480,18 +596,27 @@ MI_D void wave_artic_substep(const DevModel& m, const WaveTabs& t, const DevStat
             for (int c = 0; c < WNV; ++c) jr[c] = c == kd ? sg : 0.0f;
         }
         float wr[WNV];
+        if constexpr (TP::kCT) {
+            float x[TP::nvc];
+            sfor<0, TP::nv>([&](auto I) { x[I] = jr[I]; });
+            ct_solve<TP>(Mc, dvec, x);          // W_r = M~^-1 J_r^T, registers only
 #pragma unroll
-        for (int c = 0; c < WNV; ++c)
-            if (c < nv) xs[c * 64] = jr[c];
-        tree_solve_lds(t, Mx, Dv, nv, xs);   // W_r = M~^-1 J_r^T
+            for (int c = 0; c < WNV; ++c) wr[c] = 0.0f;
+            sfor<0, TP::nv>([&](auto I) { wr[I] = x[I]; });
+        } else {
 #pragma unroll
-        for (int c = 0; c < WNV; ++c) wr[c] = c < nv ? xs[c * 64] : 0.0f;
+            for (int c = 0; c < WNV; ++c)
+                if (c < nv) xs[c * 64] = jr[c];
+            tree_solve_lds(t, Mx, Dv, nv, xs);   // W_r = M~^-1 J_r^T
+#pragma unroll
+            for (int c = 0; c < WNV; ++c) wr[c] = c < nv ? xs[c * 64] : 0.0f;
+        }
         float a = 0.0f;
 #pragma unroll
         for (int c = 0; c < WNV; ++c) a += jr[c] * wr[c];
         sm[t.s_ad + r] = a > 1e-12f ? a : 1e-12f;
 #pragma unroll
-        for (int c = 0; c < WNV; ++c) { gJ[(size_t)r * WNV + c] = jr[c]; gW[(size_t)r * WNV + c] = wr[c]; }
+        for (int c = 0; c < WNV; ++c) gW[(size_t)r * WNV + c] = wr[c];
     }
     __syncthreads();
 
@@ -501,40 +626,72 @@ MI_D void wave_artic_substep(const DevModel& m, const WaveTabs& t, const DevStat
     // order; only the half owning the current row is active and u is copied across halves
     // between the two sub-sweeps. Row metadata and lambdas live in lane registers (row r in
     // lane r % 64, bank r / 64) and are read with readlane.
+#ifndef MI_DIAG_NO_PGS
     {
         const int half = lane >> 5, kl = lane & 31;
-        float Jr[64], Wr[64];
+        // J_r[kl] is rebuilt per row from this lane's DOF subspace and the row's force
+        // direction (the same dot6 as P9), so only W_r occupies registers
+        float S6[6];
 #pragma unroll
-        for (int rr = 0; rr < 64; ++rr) {
-            const int r = rr + 64 * half;
-            const bool ok = r < nrows;
-            Jr[rr] = ok ? gJ[(size_t)r * WNV + kl] : 0.0f;
-            Wr[rr] = ok ? gW[(size_t)r * WNV + kl] : 0.0f;
-        }
+        for (int q = 0; q < 6; ++q) S6[q] = kl < nv ? Ss[6 * kl + q] : 0.0f;
+        // the slab holds 128 rows: load unconditionally (rows >= nrows are never swept).
+        // Opaque base: otherwise 64 row addresses are hoisted out of the substep loop.
+        const float* gWl = gW + (size_t)(64 * half) * WNV + kl;
+        asm volatile("" : "+v"(gWl));
+        float Wr[64];
+#pragma unroll
+        for (int rr = 0; rr < 64; ++rr) Wr[rr] = gWl[(size_t)rr * WNV];
+        // row r's data in lane r % 64, bank r / 64: b, 1/A_rr, kind, DOF mask, f (6)
         float b0 = 0, b1 = 0, ia0 = 1, ia1 = 1, k0 = 0, k1 = 0, lam0 = 0.0f, lam1 = 0.0f;
-        if (lane < nrows) { b0 = sm[t.s_rb + lane]; ia0 = 1.0f / sm[t.s_ad + lane]; k0 = sm[t.s_rk + lane]; }
-        if (lane + 64 < nrows) { b1 = sm[t.s_rb + lane + 64]; ia1 = 1.0f / sm[t.s_ad + lane + 64]; k1 = sm[t.s_rk + lane + 64]; }
+        float fa[6] = {0, 0, 0, 0, 0, 0}, fb[6] = {0, 0, 0, 0, 0, 0};
+        unsigned ma = 0u, mb = 0u;
+        {
+            auto load_row = [&](int r, float& b, float& ia, float& k, float (&f)[6], unsigned& msk) {
+                b = sm[t.s_rb + r];
+                ia = 1.0f / sm[t.s_ad + r];
+                k = sm[t.s_rk + r];
+#pragma unroll
+                for (int q = 0; q < 6; ++q) f[q] = sm[t.s_rf + 6 * r + q];
+                const float lk = sm[t.s_rl + r];
+                msk = lk >= 0.0f ? (unsigned)t.link_mask[(int)lk] : 1u << (int)(-lk - 1.0f);
+            };
+            if (lane < nrows) load_row(lane, b0, ia0, k0, fa, ma);
+            if (lane + 64 < nrows) load_row(lane + 64, b1, ia1, k1, fb, mb);
+        }
         const float mu = p.friction;
         float u = kl < nv ? us[kl] : 0.0f;
         for (int it = 0; it < p.iters; ++it) {
-            // opaque per sweep: stops the compiler hoisting 3 x 128 loop-invariant readlanes
-            // out of the iteration loop (they would pin hundreds of SGPRs and spill)
-            asm volatile("" : "+v"(b0), "+v"(b1), "+v"(ia0), "+v"(ia1), "+v"(k0), "+v"(k1));
+            // opaque per sweep: stops the compiler hoisting the loop-invariant readlanes of
+            // every row out of the iteration loop (they would pin hundreds of SGPRs and spill)
+            asm volatile("" : "+v"(b0), "+v"(b1), "+v"(ia0), "+v"(ia1), "+v"(k0), "+v"(k1),
+                         "+v"(ma), "+v"(mb));
+            asm volatile("" : "+v"(fa[0]), "+v"(fa[1]), "+v"(fa[2]), "+v"(fa[3]), "+v"(fa[4]),
+                         "+v"(fa[5]), "+v"(fb[0]), "+v"(fb[1]), "+v"(fb[2]), "+v"(fb[3]),
+                         "+v"(fb[4]), "+v"(fb[5]));
+            int nrow_it = nrows;   // opaque: 128 hoisted "r < nrows" masks would spill
+            asm volatile("" : "+s"(nrow_it));
 #pragma unroll
             for (int h = 0; h < 2; ++h) {
-                if (64 * h >= nrows) continue;
+                if (64 * h >= nrow_it) continue;
                 const float bb = h ? b1 : b0, ii = h ? ia1 : ia0, kk = h ? k1 : k0;
-                // fully unrolled (no early exit) so Jr / Wr stay register-indexed
+                const unsigned mm = h ? mb : ma;
+                // fully unrolled (no early exit) so Wr stays register-indexed
 #pragma unroll
                 for (int rr = 0; rr < 64; ++rr) {
                     const int r = rr + 64 * h;
-                    if (r >= nrows) continue;
+                    if (r >= nrow_it) continue;
                     // keep each row's readlanes inside its own row (no SGPR hoisting)
                     __builtin_amdgcn_sched_barrier(0);
-                    const float s = half_sums(Jr[rr] * u);
+                    float fr[6];
+#pragma unroll
+                    for (int q = 0; q < 6; ++q) fr[q] = readlane(h ? fb[q] : fa[q], rr);
+                    const unsigned msk = (unsigned)__builtin_amdgcn_readlane((int)mm, rr);
+                    const int kind = (int)readlane(kk, rr);
+                    float jc = kind == 3 ? fr[0] : dot6(S6, fr);
+                    jc = ((msk >> kl) & 1u) ? jc : 0.0f;
+                    const float s = half_sums(jc * u);
                     const float jv = readlane(s, h ? 63 : 31);
                     const float br = readlane(bb, rr), iar = readlane(ii, rr);
-                    const int kind = (int)readlane(kk, rr);
                     const float l0 = readlane(h ? lam1 : lam0, rr);
                     float ln = l0 + (br - jv) * iar;
                     if (kind == 1 || kind == 2) {
@@ -546,8 +703,9 @@ MI_D void wave_artic_substep(const DevModel& m, const WaveTabs& t, const DevStat
                         ln = ln > 0.0f ? ln : 0.0f;
                     }
                     const float dl = ln - l0;
-                    if (half == h) u += Wr[rr] * dl;
-                    if (lane == rr) { if (h) lam1 = ln; else lam0 = ln; }
+                    const int ln_id = lane_here(lane);
+                    if ((ln_id >> 5) == h) u += Wr[rr] * dl;
+                    if (ln_id == rr) { if (h) lam1 = ln; else lam0 = ln; }
                 }
                 // hand u to the other half for its sub-sweep
                 u = __shfl(u, kl + 32 * h, 64);
@@ -557,6 +715,7 @@ MI_D void wave_artic_substep(const DevModel& m, const WaveTabs& t, const DevStat
         if (lane < nrows) sm[t.s_ad + lane] = lam0;          // reuse: lambda of row lane
         if (lane + 64 < nrows) sm[t.s_ad + lane + 64] = lam1;
     }
+#endif
     __syncthreads();
 
     STAMP(11);

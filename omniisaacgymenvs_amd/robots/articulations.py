@@ -221,6 +221,16 @@ class ArticulationView:
     def sim_step(self, substeps: int = 1) -> None:
         N.check(N.lib().mi_sim_step(self.handle, int(substeps), self.stream()), "mi_sim_step")
 
+    def sim_kernel_path(self) -> tuple:
+        """(path, topology): path 1 = wavefront-per-env kernel, 0 = one lane per env;
+        topology = compile-time topology id (0: runtime tables)."""
+        p, t = C.c_int32(), C.c_int32()
+        N.check(N.lib().mi_sim_kernel_path(self.handle, C.byref(p), C.byref(t)), "mi_sim_kernel_path")
+        return int(p.value), int(t.value)
+
+    def sim_topology(self) -> int:
+        return self.sim_kernel_path()[1]
+
     def nan_count(self) -> int:
         c = C.c_int64()
         N.check(N.lib().mi_sim_nan_count(self.handle, C.byref(c)), "mi_sim_nan_count")

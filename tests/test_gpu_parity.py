@@ -204,3 +204,27 @@ def test_wave_path_matches_thread_path(gpu, monkeypatch):
             assert torch.equal(da, db)
         ea.close()
         eb.close()
+
+
+def test_compiled_topology_matches_runtime_tables(gpu, monkeypatch):
+    """Model-specialised (compile-time topology) wave kernel vs the runtime-table wave kernel:
+    same algorithm and operation order, so they agree to float rounding."""
+    for name in ("Ant", "Humanoid"):
+        ea = make_env(name, num_envs=128, device="cuda:0", seed=41)
+        monkeypatch.setenv("MI_SIM_TOPO", "runtime")
+        eb = make_env(name, num_envs=128, device="cuda:0", seed=41)
+        monkeypatch.delenv("MI_SIM_TOPO")
+        assert ea.task.get_robot().sim_topology() != 0 and eb.task.get_robot().sim_topology() == 0
+        orc = oracle_twin(ea, 41)
+        for step in range(3):
+            acts = rand_actions(128, ea.num_actions, 70 + step)
+            sync_oracle(ea, orc)
+            orc.env_step(acts.numpy(), ea.task.control_frequency_inv, task_buffers(ea))
+            oa, ra, da, _ = ea.step(acts.to("cuda:0"))
+            ob, rb, db, _ = eb.step(acts.to("cuda:0"))
+            torch.cuda.synchronize()
+            check_pair(name, ea.task, oa["obs"].cpu().numpy(), ra.cpu().numpy(), ob["obs"].cpu().numpy(),
+                       rb.cpu().numpy(), 2e-4, orc.decision_margin())
+            assert torch.equal(da, db)
+        ea.close()
+        eb.close()

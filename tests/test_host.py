@@ -143,3 +143,13 @@ def test_product_fails_loudly_without_gpu():
         make_env("Cartpole", num_envs=8, device="cpu")
     with pytest.raises(RuntimeError):
         make_env("Humanoid", num_envs=8, device="cuda:0")
+
+
+def test_generated_topologies_up_to_date():
+    """csrc/mi_topo_gen.hpp (compile-time topologies of the shipped robots) matches the assets."""
+    import subprocess
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    r = subprocess.run([sys.executable, os.path.join(root, "tools", "gen_topologies.py"), "--check"],
+                       capture_output=True, text=True)
+    assert r.returncode == 0, r.stdout + r.stderr
