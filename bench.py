@@ -92,6 +92,16 @@ def cpu_baseline(task_name: str, env, seconds: float) -> dict:
     }
 
 
+def kernel_name(view, task) -> str:
+    from omniisaacgymenvs_amd import native as N
+    """Name of the fused env-step kernel this configuration launches."""
+    path, topo = view.sim_kernel_path()
+    if path == 1 and task.task_params().task_kind != N.MI_TASK_CARTPOLE:   # wave path
+        return "k_env_step_wave<" + {0: "TopoRuntime", 1: "TopoCT<RobotHumanoid>",
+                                     2: "TopoCT<RobotAnt>"}.get(topo, str(topo)) + ">"
+    return "k_env_step"
+
+
 def read_traffic(task_name: str):
     """HBM bytes per launch from the committed PMC pass (profiles/traffic_<task>.json), if any."""
     p = os.path.join(ROOT, "profiles", f"traffic_{task_name}.json")
@@ -180,7 +190,7 @@ def main():
             achieved = ALGO_BYTES[args.task] * n_local / (kernel_ms * 1e-3) / 1e9
             roof = {"bound": "hbm", "achieved": round(achieved, 3), "peak": HBM_PEAK_GBS,
                     "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 6),
-                    "traffic": read_traffic(args.task), "kernel": "k_env_step",
+                    "traffic": read_traffic(args.task), "kernel": kernel_name(view, task),
                     "kernel_ms": round(kernel_ms, 4),
                     "algo_bytes_per_launch": ALGO_BYTES[args.task] * n_local}
         out = {

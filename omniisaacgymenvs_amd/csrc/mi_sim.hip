@@ -563,6 +563,16 @@ int mi_sim_create(const mi_model_desc* md, const mi_sim_params* prm, int32_t N, 
         UPW(lev_start, lev_start); UPW(lev_links, lev_links); UPW(child_start, child_start);
         UPW(child_list, child_list); UPW(anc_start, anc_start); UPW(anc_list, anc_list);
         UPW(desc_start, desc_start); UPW(desc_list, desc_list);
+        std::vector<int> chain_start(L + 1, 0), chain_list;
+        for (int l = 0; l < L; ++l) {
+            chain_start[l] = (int)chain_list.size();
+            std::vector<int> up;
+            for (int x = l; x > 0; x = md->parent[x]) up.push_back(x);
+            chain_list.insert(chain_list.end(), up.rbegin(), up.rend());
+        }
+        chain_start[L] = (int)chain_list.size();
+        if (chain_list.empty()) chain_list.push_back(0);
+        UPW(chain_start, chain_start); UPW(chain_list, chain_list);
         UPW(link_mask, link_mask); UPW(tri_p, tri_p); UPW(tri_q, tri_q);
 #undef UPW
         auto al4 = [](int x) { return (x + 3) & ~3; };
@@ -575,7 +585,8 @@ int mi_sim_create(const mi_model_desc* md, const mi_sim_params* prm, int32_t N, 
         t.s_q = take(WNV); t.s_rp = take(8); t.s_cp = take(3 * 64); t.s_cl = take(64);
         t.s_rl = take(128); t.s_rf = take(6 * 128); t.s_rb = take(128); t.s_rk = take(128);
         t.s_ad = take(128);
-        t.s_xs = take(WNV * 64);   // lane-private solve vectors
+        // lane-private solve vectors of the runtime-table solves (CT solves run in registers)
+        t.s_xs = take(s->topo ? 4 : WNV * 64);
         t.s_total = so;
         {   // every region must be distinct: offsets strictly increase in declaration order
             const int offs[] = {t.s_R, t.s_o, t.s_S, t.s_V, t.s_A, t.s_F, t.s_Ic, t.s_M, t.s_X,
@@ -585,7 +596,7 @@ int mi_sim_create(const mi_model_desc* md, const mi_sim_params* prm, int32_t N, 
                 if (offs[c] <= offs[c - 1]) return cleanup(fail(MI_E_STATE, "wave LDS layout: region %zu overlaps", c));
         }
         t.max_rows = m.max_rows;
-        t.g_row_stride = (size_t)128 * WNV;   // padded: PGS loads all 128 row slots
+        t.g_row_stride = (size_t)m.max_rows * WNV;
         s->lds_bytes = (size_t)so * sizeof(float);
     }
     s->lower.assign(md->lower, md->lower + L);

@@ -55,6 +55,8 @@ struct WaveTabs {
     const int* lev_links;     // [L]
     const int* child_start;   // [L+1]
     const int* child_list;    // [L]
+    const int* chain_start;   // [L+1] links on the path root -> l, excl. the root, root first
+    const int* chain_list;
     const int* desc_start;    // [L+1] descendants of link l (excl. l), increasing index
     const int* desc_list;
     const int* anc_start;     // [nv+1] ancestors of dof k (excl. k), nearest first
@@ -235,68 +237,75 @@ MI_D void wave_link_local(const DevModel& m, const WaveTabs& t, float* sm, int l
     for (int c = 0; c < 3; ++c) { aux[9 + c] = tl[c]; aux[12 + c] = a[c]; }
 }
 
-// P1b: compose link l's world frame, subspace, velocity and velocity-product acceleration
-// from its parent (one tree level at a time)
-MI_D void wave_link_compose(const DevModel& m, const WaveTabs& t, float* sm, int l,
-                            const SimP& p) {
-    float* Rs = sm + t.s_R;
-    float* os = sm + t.s_o;
-    float* Vs = sm + t.s_V;
-    float* As = sm + t.s_A;
-    const int nr = m.nr;
-    float R[9], o[3], V[6], A[6];
-    if (l == 0) {
-        m3_from_quat(sm + t.s_rp + 4, R);
-        o[0] = o[1] = o[2] = 0.0f;
-        A[0] = A[1] = A[2] = 0.0f;
-        A[3] = -p.g[0]; A[4] = -p.g[1]; A[5] = -p.g[2];
-        if (nr) {
-            const float* u = sm + t.s_us;
-            const float v[3] = {u[0], u[1], u[2]};
-            const float om[3] = {u[3], u[4], u[5]};
-            float wv[3];
-            cross3(om, v, wv);
-            A[3] -= wv[0]; A[4] -= wv[1]; A[5] -= wv[2];
-            V[0] = om[0]; V[1] = om[1]; V[2] = om[2];
-            V[3] = v[0]; V[4] = v[1]; V[5] = v[2];
-        } else {
-#pragma unroll
-            for (int c = 0; c < 6; ++c) V[c] = 0.0f;
-        }
+// P1b helpers. Root frame: orientation from the root quaternion, origin p0 (the spatial
+// origin), fictitious base acceleration -g (- w x v for a free root).
+MI_D void link_root(const WaveTabs& t, const float* sm, const SimP& p, int nr, float (&R)[9],
+                    float (&o)[3], float (&V)[6], float (&A)[6]) {
+    m3_from_quat(sm + t.s_rp + 4, R);
+    o[0] = o[1] = o[2] = 0.0f;
+    A[0] = A[1] = A[2] = 0.0f;
+    A[3] = -p.g[0]; A[4] = -p.g[1]; A[5] = -p.g[2];
+    if (nr) {
+        const float* u = sm + t.s_us;
+        const float v[3] = {u[0], u[1], u[2]};
+        const float om[3] = {u[3], u[4], u[5]};
+        float wv[3];
+        cross3(om, v, wv);
+        A[3] -= wv[0]; A[4] -= wv[1]; A[5] -= wv[2];
+        V[0] = om[0]; V[1] = om[1]; V[2] = om[2];
+        V[3] = v[0]; V[4] = v[1]; V[5] = v[2];
     } else {
-        const int P = m.parent[l], k = nr + l - 1;
-        const float* aux = sm + t.s_X + 15 * l;
-        float RP[9], VP[6], AP[6], a[3], op[3], s[6];
 #pragma unroll
-        for (int c = 0; c < 9; ++c) RP[c] = Rs[9 * P + c];
+        for (int c = 0; c < 6; ++c) V[c] = 0.0f;
+    }
+}
+
+// One tree step: link c's frame, DOF subspace s, velocity and velocity-product acceleration
+// from its parent's (R, o, V, A), updated in place.
+MI_D void link_step(const DevModel& m, const WaveTabs& t, const float* sm, int c, float (&R)[9],
+                    float (&o)[3], float (&V)[6], float (&A)[6], float (&s)[6]) {
+    const int k = m.nr + c - 1;
+    const float* aux = sm + t.s_X + 15 * c;
+    float RP[9], a[3], op[3];
 #pragma unroll
-        for (int c = 0; c < 6; ++c) { VP[c] = Vs[6 * P + c]; AP[c] = As[6 * P + c]; }
-        m3_mul(RP, aux, R);
-        m3_vec(RP, aux + 9, op);
-        m3_vec(RP, aux + 12, a);
+    for (int q = 0; q < 9; ++q) RP[q] = R[q];
+    m3_mul(RP, aux, R);
+    m3_vec(RP, aux + 9, op);
+    m3_vec(RP, aux + 12, a);
 #pragma unroll
-        for (int c = 0; c < 3; ++c) o[c] = os[3 * P + c] + op[c];
-        if (m.jtype[l] == MI_JOINT_HINGE) {
-            s[0] = a[0]; s[1] = a[1]; s[2] = a[2];
-            cross3(o, a, s + 3);
-        } else {
-            s[0] = s[1] = s[2] = 0.0f;
-            s[3] = a[0]; s[4] = a[1]; s[5] = a[2];
-        }
+    for (int q = 0; q < 3; ++q) o[q] = o[q] + op[q];
+    if (m.jtype[c] == MI_JOINT_HINGE) {
+        s[0] = a[0]; s[1] = a[1]; s[2] = a[2];
+        cross3(o, a, s + 3);
+    } else {
+        s[0] = s[1] = s[2] = 0.0f;
+        s[3] = a[0]; s[4] = a[1]; s[5] = a[2];
+    }
+    const float uk = sm[t.s_us + k];
+    float sd[6];
+    crm(V, s, sd);
 #pragma unroll
-        for (int c = 0; c < 6; ++c) sm[t.s_S + 6 * k + c] = s[c];
-        const float uk = sm[t.s_us + k];
-        float sd[6];
-        crm(VP, s, sd);
+    for (int q = 0; q < 6; ++q) { V[q] = V[q] + s[q] * uk; A[q] = A[q] + sd[q] * uk; }
+}
+
+// P1b: link l's world frame, subspace, velocity and velocity-product acceleration, composed
+// along its own root-to-l chain (no barriers between tree levels: every lane walks its chain;
+// each step is the same arithmetic a level-by-level sweep would do, so results are identical).
+MI_D void wave_link_chain(const DevModel& m, const WaveTabs& t, float* sm, int l, const SimP& p) {
+    float R[9], o[3], V[6], A[6], s[6];
+    link_root(t, sm, p, m.nr, R, o, V, A);
+    for (int j = t.chain_start[l]; j < t.chain_start[l + 1]; ++j)
+        link_step(m, t, sm, t.chain_list[j], R, o, V, A, s);
+    if (l > 0) {
 #pragma unroll
-        for (int c = 0; c < 6; ++c) { V[c] = VP[c] + s[c] * uk; A[c] = AP[c] + sd[c] * uk; }
+        for (int c = 0; c < 6; ++c) sm[t.s_S + 6 * (m.nr + l - 1) + c] = s[c];
     }
 #pragma unroll
-    for (int c = 0; c < 9; ++c) Rs[9 * l + c] = R[c];
+    for (int c = 0; c < 9; ++c) sm[t.s_R + 9 * l + c] = R[c];
 #pragma unroll
-    for (int c = 0; c < 3; ++c) os[3 * l + c] = o[c];
+    for (int c = 0; c < 3; ++c) sm[t.s_o + 3 * l + c] = o[c];
 #pragma unroll
-    for (int c = 0; c < 6; ++c) { Vs[6 * l + c] = V[c]; As[6 * l + c] = A[c]; }
+    for (int c = 0; c < 6; ++c) { sm[t.s_V + 6 * l + c] = V[c]; sm[t.s_A + 6 * l + c] = A[c]; }
 }
 
 // P1c: spatial inertia about p0 and Newton-Euler force of link l (independent per link)
@@ -379,14 +388,12 @@ MI_D void wave_artic_substep(const DevModel& m, const WaveTabs& t, const DevStat
     // ---- P1a: local joint transforms, every link at once
     for (int l = 1 + lane; l < L; l += 64) wave_link_local(m, t, sm, l);
     __syncthreads();
-    // ---- P1b: world frames / subspaces / velocities, one tree level at a time
-    for (int lev = 0; lev < t.nlev; ++lev) {
-        const int b = t.lev_start[lev], e = t.lev_start[lev + 1];
-        for (int c = b + lane; c < e; c += 64) wave_link_compose(m, t, sm, t.lev_links[c], p);
-        __syncthreads();
+    // ---- P1b+c: world frames / subspaces / velocities along each link's chain, then the
+    // link's inertia and Newton-Euler force (same lane: no barrier in between)
+    for (int l = lane; l < L; l += 64) {
+        wave_link_chain(m, t, sm, l, p);
+        wave_link_dynamics(m, t, sm, l);
     }
-    // ---- P1c: link inertias + Newton-Euler forces, every link at once
-    for (int l = lane; l < L; l += 64) wave_link_dynamics(m, t, sm, l);
     __syncthreads();
     STAMP(2);
     // ---- P2: composite inertia / force = own + sum over the subtree (fixed descendant order,
@@ -634,13 +641,18 @@ MI_D void wave_artic_substep(const DevModel& m, const WaveTabs& t, const DevStat
         float S6[6];
 #pragma unroll
         for (int q = 0; q < 6; ++q) S6[q] = kl < nv ? Ss[6 * kl + q] : 0.0f;
-        // the slab holds 128 rows: load unconditionally (rows >= nrows are never swept).
-        // Opaque base: otherwise 64 row addresses are hoisted out of the substep loop.
-        const float* gWl = gW + (size_t)(64 * half) * WNV + kl;
-        asm volatile("" : "+v"(gWl));
+        // Bounded buffer loads: the descriptor covers rows [0, nrows), so slots past the last
+        // row read as 0 without touching memory (no per-row branch, no wasted traffic).
         float Wr[64];
+        {
+            const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
+                (void*)gW, (short)0, nrows * WNV * (int)sizeof(float), 0x00020000);
+            const int vo = (64 * half * WNV + kl) * (int)sizeof(float);
 #pragma unroll
-        for (int rr = 0; rr < 64; ++rr) Wr[rr] = gWl[(size_t)rr * WNV];
+            for (int rr = 0; rr < 64; ++rr)
+                Wr[rr] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(
+                                                       rs, vo + rr * WNV * (int)sizeof(float), 0, 0));
+        }
         // row r's data in lane r % 64, bank r / 64: b, 1/A_rr, kind, DOF mask, f (6)
         float b0 = 0, b1 = 0, ia0 = 1, ia1 = 1, k0 = 0, k1 = 0, lam0 = 0.0f, lam1 = 0.0f;
         float fa[6] = {0, 0, 0, 0, 0, 0}, fb[6] = {0, 0, 0, 0, 0, 0};
