@@ -95,7 +95,7 @@ def cpu_baseline(task_name: str, env, seconds: float) -> dict:
 def kernel_name(view, task) -> str:
     from omniisaacgymenvs_amd import native as N
     """Name of the fused env-step kernel this configuration launches."""
-    path, topo = view.sim_kernel_path()
+    path, topo, _ = view.sim_kernel_path()
     if path == 1 and task.task_params().task_kind != N.MI_TASK_CARTPOLE:   # wave path
         return "k_env_step_wave<" + {0: "TopoRuntime", 1: "TopoCT<RobotHumanoid>",
                                      2: "TopoCT<RobotAnt>"}.get(topo, str(topo)) + ">"
@@ -203,6 +203,7 @@ def main():
                                    f"(controlFrequencyInv=2 substeps @ dt=0.0083)",
                        "task": args.task, "num_envs_per_gpu": n_local, "global_envs": world * n_local,
                        "substeps": task.control_frequency_inv, "path": "fused" if env.fused else "modular",
+                       "lds_bytes_per_env": view.sim_kernel_path()[2],
                        "parallelism": f"env-shard x{world}" + (f" + RCCL all_gather every {args.gather_every}" if world > 1 else "")},
             "roofline": roof,
             "nan_resets": nan,

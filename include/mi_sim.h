@@ -215,8 +215,9 @@ int mi_get_reset_count(mi_sim* sim, uint32_t* out /*[N] host*/);
 /* Number of env-steps whose physics produced a non-finite state and were forced to reset. */
 int mi_sim_nan_count(mi_sim* sim, int64_t* count);
 /* Diagnostics: which physics kernel runs. path: 0 one-lane-per-env, 1 wavefront-per-env;
- * topology: id of the compile-time (model-specialised) topology, 0 = runtime tables. */
-int mi_sim_kernel_path(const mi_sim* sim, int32_t* path, int32_t* topology);
+ * topology: id of the compile-time (model-specialised) topology, 0 = runtime tables;
+ * lds_bytes: LDS per env (= per workgroup) of the wave path. Any output may be NULL. */
+int mi_sim_kernel_path(const mi_sim* sim, int32_t* path, int32_t* topology, int32_t* lds_bytes);
 int mi_abi_version(void);
 const char* mi_last_error(void);
 

@@ -275,6 +275,12 @@ __device__ __forceinline__ const KParams* opaque_kp(const KParams* kp) {
     return kp;
 }
 
+// copy the per-model constant block into this workgroup's LDS (once per launch)
+__device__ __forceinline__ void stage_model_constants(const WaveTabs& t, float* smem) {
+    for (int q = threadIdx.x; q < t.mc_len; q += 64) smem[t.s_mc + q] = t.g_mc[q];
+    __syncthreads();
+}
+
 template <class T>
 __global__ __launch_bounds__(64) void k_sim_step_wave(const KParams* __restrict__ kp, int substeps) {
     extern __shared__ __attribute__((aligned(16))) float smem[];
@@ -284,6 +290,7 @@ __global__ __launch_bounds__(64) void k_sim_step_wave(const KParams* __restrict_
     const SimP& p = kp->p;
     const int i = blockIdx.x;
     float* gW = kp->rows + (size_t)i * t.g_row_stride;
+    stage_model_constants(t, smem);
     for (int s = 0; s < substeps; ++s) {
         const KParams* k = opaque_kp(kp);
         wave_artic_substep<T>(k->m, k->t, k->st, k->p, i, smem, gW);
@@ -305,10 +312,10 @@ __global__ __launch_bounds__(64) void k_env_step_wave(const KParams* __restrict_
     float* rows = kp->rows;
     const int i = blockIdx.x;
     const int lane = threadIdx.x;
-    // 1. clamp + pre_physics_step (scalar task math on lane 0)
+    // 1. clamp + pre_physics_step (scalar task math on lane 0); model constants into LDS
     if (lane == 0)
         task_pre_env(m, st, tp, i, actions, reset_buf, progress_buf, pot, prev, actions_out, true);
-    __syncthreads();
+    stage_model_constants(t, smem);
     // 2. controlFrequencyInv x World.step, wave-cooperative
     float* gW = rows + (size_t)i * t.g_row_stride;
     for (int s = 0; s < substeps; ++s) {
@@ -574,22 +581,73 @@ int mi_sim_create(const mi_model_desc* md, const mi_sim_params* prm, int32_t N, 
         if (chain_list.empty()) chain_list.push_back(0);
         UPW(chain_start, chain_start); UPW(chain_list, chain_list);
         UPW(link_mask, link_mask); UPW(tri_p, tri_p); UPW(tri_q, tri_q);
+        // per-model constant block (SoA), staged into LDS by every workgroup (McField & co.)
+        {
+            const int np = (int)pt_geom.size(), ns = md->num_sensors;
+            std::vector<float> mcb((size_t)MC_NLINKF * L, 0.0f);
+            for (int l = 0; l < L; ++l) {
+                auto put = [&](int f, float v) { mcb[(size_t)f * L + l] = v; };
+                for (int c = 0; c < 3; ++c) {
+                    put(MC_POS + c, md->pos[3 * l + c]); put(MC_AXIS + c, md->axis[3 * l + c]);
+                    put(MC_COM + c, md->com[3 * l + c]);
+                }
+                for (int c = 0; c < 4; ++c) put(MC_QUAT + c, md->quat[4 * l + c]);
+                for (int c = 0; c < 6; ++c) put(MC_INER + c, md->inertia[6 * l + c]);
+                put(MC_JTYPE, (float)md->jtype[l]); put(MC_MASS, md->mass[l]);
+                put(MC_ARM, md->armature[l]); put(MC_DAMP, md->damping[l]);
+                put(MC_LO, md->lower[l]); put(MC_HI, md->upper[l]);
+                const unsigned lo32 = (unsigned)(link_mask[l] & 0xffffffffull);
+                float mf; std::memcpy(&mf, &lo32, 4); put(MC_MASK, mf);
+            }
+            auto pad4 = [&]() { while (mcb.size() % 4) mcb.push_back(0.0f); };
+            pad4();
+            t.mc_pts = (int)mcb.size();
+            mcb.resize(mcb.size() + (size_t)MP_NF * np, 0.0f);
+            for (int c = 0; c < np; ++c) {
+                const int g = pt_geom[c];
+                const float* pg = pt_end[c] ? md->geom_p1 + 3 * g : md->geom_p0 + 3 * g;
+                mcb[t.mc_pts + (size_t)MP_LINK * np + c] = (float)md->geom_link[g];
+                for (int q = 0; q < 3; ++q) mcb[t.mc_pts + (size_t)(MP_X + q) * np + c] = pg[q];
+                mcb[t.mc_pts + (size_t)MP_RAD * np + c] = md->geom_radius[g];
+            }
+            pad4();
+            t.mc_sens = (int)mcb.size();
+            mcb.resize(mcb.size() + (size_t)MS_NF * ns, 0.0f);
+            for (int c = 0; c < ns; ++c) {
+                mcb[t.mc_sens + (size_t)MS_LINK * ns + c] = (float)md->sensor_link[c];
+                for (int q = 0; q < 3; ++q)
+                    mcb[t.mc_sens + (size_t)(MS_X + q) * ns + c] = md->sensor_pos[3 * c + q];
+            }
+            auto put_ints = [&](const std::vector<int>& v) {
+                pad4();
+                const int at = (int)mcb.size();
+                for (int x : v) { float f; std::memcpy(&f, &x, 4); mcb.push_back(f); }
+                return at;
+            };
+            t.mc_chs = put_ints(chain_start); t.mc_chl = put_ints(chain_list);
+            t.mc_dss = put_ints(desc_start); t.mc_dsl = put_ints(desc_list);
+            pad4();
+            t.mc_len = (int)mcb.size();
+            t.npts = np; t.nsens = ns;
+            UPW(g_mc, mcb);
+        }
 #undef UPW
         auto al4 = [](int x) { return (x + 3) & ~3; };
         int so = 0;
         auto take = [&](int n) { const int at = so; so += al4(n); return at; };
-        t.s_R = take(9 * L); t.s_o = take(3 * L); t.s_S = take(6 * m.nv); t.s_V = take(6 * L);
-        t.s_A = take(6 * L); t.s_F = take(6 * L); t.s_Ic = take(10 * L); t.s_M = take(WNV * WNV);
+        t.s_mc = take(t.mc_len);
+        t.s_R = take(9 * L); t.s_o = take(3 * L); t.s_S = take(6 * m.nv);
+        t.s_F = take(6 * L); t.s_Ic = take(10 * L); t.s_M = take(m.nv * m.nv);
         t.s_X = take(16 * L);  // aux: local transforms (P1), composite inertia / force (P2)
         t.s_D = take(WNV); t.s_r = take(WNV); t.s_us = take(WNV);
-        t.s_q = take(WNV); t.s_rp = take(8); t.s_cp = take(3 * 64); t.s_cl = take(64);
-        t.s_rl = take(128); t.s_rf = take(6 * 128); t.s_rb = take(128); t.s_rk = take(128);
-        t.s_ad = take(128);
+        t.s_q = take(WNV); t.s_rp = take(8); t.s_cp = take(3 * m.npts); t.s_cl = take(m.npts);
+        t.s_rl = take(m.max_rows); t.s_rf = take(6 * m.max_rows); t.s_rb = take(m.max_rows);
+        t.s_rk = take(m.max_rows); t.s_ad = take(m.max_rows);
         // lane-private solve vectors of the runtime-table solves (CT solves run in registers)
         t.s_xs = take(s->topo ? 4 : WNV * 64);
         t.s_total = so;
         {   // every region must be distinct: offsets strictly increase in declaration order
-            const int offs[] = {t.s_R, t.s_o, t.s_S, t.s_V, t.s_A, t.s_F, t.s_Ic, t.s_M, t.s_X,
+            const int offs[] = {t.s_mc, t.s_R, t.s_o, t.s_S, t.s_F, t.s_Ic, t.s_M, t.s_X,
                                 t.s_D, t.s_r, t.s_us, t.s_q, t.s_rp, t.s_cp, t.s_cl, t.s_rl,
                                 t.s_rf, t.s_rb, t.s_rk, t.s_ad, t.s_xs, t.s_total};
             for (size_t c = 1; c < sizeof(offs) / sizeof(offs[0]); ++c)
@@ -917,10 +975,11 @@ int mi_sim_nan_count(mi_sim* s, int64_t* count) {
     return MI_OK;
 }
 
-int mi_sim_kernel_path(const mi_sim* s, int32_t* path, int32_t* topology) {
-    NEED(s); NEED(path); NEED(topology);
-    *path = s->wave ? 1 : 0;
-    *topology = s->wave ? s->topo : 0;
+int mi_sim_kernel_path(const mi_sim* s, int32_t* path, int32_t* topology, int32_t* lds_bytes) {
+    NEED(s);
+    if (path) *path = s->wave ? 1 : 0;
+    if (topology) *topology = s->wave ? s->topo : 0;
+    if (lds_bytes) *lds_bytes = s->wave ? (int32_t)s->lds_bytes : 0;
     return MI_OK;
 }
 

@@ -65,11 +65,54 @@ struct WaveTabs {
     const unsigned char* tri_p;           // pair index -> (p, q), p <= q
     const unsigned char* tri_q;
     // LDS float offsets
-    int s_R, s_o, s_S, s_V, s_A, s_F, s_Ic, s_M, s_X, s_D, s_r, s_us, s_q, s_rp, s_cp, s_cl,
+    int s_mc, s_R, s_o, s_S, s_F, s_Ic, s_M, s_X, s_D, s_r, s_us, s_q, s_rp, s_cp, s_cl,
         s_rl, s_rf, s_rb, s_rk, s_ad, s_xs, s_total;
     int max_rows;
-    size_t g_row_stride;  // floats per env in the global row slab (2 * max_rows * WNV)
+    size_t g_row_stride;  // floats per env in the global W-row slab (max_rows * WNV)
+    // per-model constant block (see McLayout): global copy, staged into LDS at s_mc once per
+    // launch by every workgroup
+    const float* g_mc;
+    int mc_len, mc_pts, mc_sens, mc_chs, mc_chl, mc_dss, mc_dsl;   // offsets inside the block
+    int npts, nsens;
 };
+
+// Per-model constants in the LDS block, structure-of-arrays so lane-indexed reads (lane = link,
+// point or sensor) hit consecutive banks. Link field f of link l at [f * L + l].
+enum McField {
+    MC_POS = 0, MC_QUAT = 3, MC_AXIS = 7, MC_JTYPE = 10, MC_MASS = 11, MC_COM = 12,
+    MC_INER = 15, MC_ARM = 21, MC_DAMP = 22, MC_LO = 23, MC_HI = 24, MC_MASK = 25,
+    MC_NLINKF = 26
+};
+// point fields (at mc_pts + f * npts + c): link, x, y, z (link frame), radius
+enum McPoint { MP_LINK = 0, MP_X = 1, MP_RAD = 4, MP_NF = 5 };
+// sensor fields (at mc_sens + f * nsens + s): link, x, y, z
+enum McSensor { MS_LINK = 0, MS_X = 1, MS_NF = 4 };
+
+struct MC {
+    const float* b;
+    const int* bi;
+    int L, np, ns;
+    const WaveTabs* t;
+    MI_D float lf(int f, int l) const { return b[f * L + l]; }
+    MI_D void lf3(int f, int l, float* o) const { o[0] = lf(f, l); o[1] = lf(f + 1, l); o[2] = lf(f + 2, l); }
+    MI_D int jtype(int l) const { return (int)lf(MC_JTYPE, l); }
+    MI_D unsigned mask(int l) const { return (unsigned)bi[MC_MASK * L + l]; }
+    MI_D float pf(int f, int c) const { return b[t->mc_pts + f * np + c]; }
+    MI_D float sf(int f, int s) const { return b[t->mc_sens + f * ns + s]; }
+    MI_D int chain_start(int l) const { return bi[t->mc_chs + l]; }
+    MI_D int chain(int j) const { return bi[t->mc_chl + j]; }
+    MI_D int desc_start(int l) const { return bi[t->mc_dss + l]; }
+    MI_D int desc(int j) const { return bi[t->mc_dsl + j]; }
+};
+
+MI_D MC make_mc(const WaveTabs& t, float* sm, int L) {
+    MC c;
+    c.b = sm + t.s_mc;
+    c.bi = (const int*)(sm + t.s_mc);
+    c.L = L; c.np = t.npts; c.ns = t.nsens;
+    c.t = &t;
+    return c;
+}
 
 MI_D float wave_sum(float v) {
 #pragma unroll
@@ -214,16 +257,20 @@ MI_D void ct_solve(float (&Mc)[T::nvc], float dvec, float (&x)[T::nvc]) {
 
 // P1a: local joint transform of link l >= 1 (independent of every other link):
 // aux[15 l ..] = {Rloc = Rq Rot(axis, q) (9), tloc (3), aloc = Rq axis (3)}
-MI_D void wave_link_local(const DevModel& m, const WaveTabs& t, float* sm, int l) {
+MI_D void wave_link_local(const MC& mc, const WaveTabs& t, float* sm, int l) {
     float* aux = sm + t.s_X + 15 * l;
-    float Rq[9], a[3];
-    m3_from_quat(m.quat + 4 * l, Rq);
-    m3_vec(Rq, m.axis + 3 * l, a);
+    float Rq[9], a[3], qt[4], ax[3], tl[3];
+    qt[0] = mc.lf(MC_QUAT, l); qt[1] = mc.lf(MC_QUAT + 1, l);
+    qt[2] = mc.lf(MC_QUAT + 2, l); qt[3] = mc.lf(MC_QUAT + 3, l);
+    mc.lf3(MC_AXIS, l, ax);
+    mc.lf3(MC_POS, l, tl);
+    m3_from_quat(qt, Rq);
+    m3_vec(Rq, ax, a);
     const float qj = sm[t.s_q + l - 1];
-    float R[9], tl[3] = {m.pos[3 * l], m.pos[3 * l + 1], m.pos[3 * l + 2]};
-    if (m.jtype[l] == MI_JOINT_HINGE) {
+    float R[9];
+    if (mc.jtype(l) == MI_JOINT_HINGE) {
         float Ra[9];
-        m3_axis_angle(m.axis + 3 * l, qj, Ra);
+        m3_axis_angle(ax, qj, Ra);
         m3_mul(Rq, Ra, R);
     } else {
 #pragma unroll
@@ -262,9 +309,9 @@ MI_D void link_root(const WaveTabs& t, const float* sm, const SimP& p, int nr, f
 
 // One tree step: link c's frame, DOF subspace s, velocity and velocity-product acceleration
 // from its parent's (R, o, V, A), updated in place.
-MI_D void link_step(const DevModel& m, const WaveTabs& t, const float* sm, int c, float (&R)[9],
+MI_D void link_step(const MC& mc, int nr, const WaveTabs& t, const float* sm, int c, float (&R)[9],
                     float (&o)[3], float (&V)[6], float (&A)[6], float (&s)[6]) {
-    const int k = m.nr + c - 1;
+    const int k = nr + c - 1;
     const float* aux = sm + t.s_X + 15 * c;
     float RP[9], a[3], op[3];
 #pragma unroll
@@ -274,7 +321,7 @@ MI_D void link_step(const DevModel& m, const WaveTabs& t, const float* sm, int c
     m3_vec(RP, aux + 12, a);
 #pragma unroll
     for (int q = 0; q < 3; ++q) o[q] = o[q] + op[q];
-    if (m.jtype[c] == MI_JOINT_HINGE) {
+    if (mc.jtype(c) == MI_JOINT_HINGE) {
         s[0] = a[0]; s[1] = a[1]; s[2] = a[2];
         cross3(o, a, s + 3);
     } else {
@@ -288,43 +335,36 @@ MI_D void link_step(const DevModel& m, const WaveTabs& t, const float* sm, int c
     for (int q = 0; q < 6; ++q) { V[q] = V[q] + s[q] * uk; A[q] = A[q] + sd[q] * uk; }
 }
 
-// P1b: link l's world frame, subspace, velocity and velocity-product acceleration, composed
+// P1b+c: link l's world frame, subspace, velocity and velocity-product acceleration, composed
 // along its own root-to-l chain (no barriers between tree levels: every lane walks its chain;
-// each step is the same arithmetic a level-by-level sweep would do, so results are identical).
-MI_D void wave_link_chain(const DevModel& m, const WaveTabs& t, float* sm, int l, const SimP& p) {
+// each step is the same arithmetic a level-by-level sweep would do, so results are identical),
+// then the link's spatial inertia about p0 and Newton-Euler force from the register values.
+MI_D void wave_link_forward(const MC& mc, int nr, const WaveTabs& t, float* sm, int l,
+                            const SimP& p) {
     float R[9], o[3], V[6], A[6], s[6];
-    link_root(t, sm, p, m.nr, R, o, V, A);
-    for (int j = t.chain_start[l]; j < t.chain_start[l + 1]; ++j)
-        link_step(m, t, sm, t.chain_list[j], R, o, V, A, s);
+    link_root(t, sm, p, nr, R, o, V, A);
+    for (int j = mc.chain_start(l); j < mc.chain_start(l + 1); ++j)
+        link_step(mc, nr, t, sm, mc.chain(j), R, o, V, A, s);
     if (l > 0) {
 #pragma unroll
-        for (int c = 0; c < 6; ++c) sm[t.s_S + 6 * (m.nr + l - 1) + c] = s[c];
+        for (int c = 0; c < 6; ++c) sm[t.s_S + 6 * (nr + l - 1) + c] = s[c];
     }
 #pragma unroll
     for (int c = 0; c < 9; ++c) sm[t.s_R + 9 * l + c] = R[c];
 #pragma unroll
     for (int c = 0; c < 3; ++c) sm[t.s_o + 3 * l + c] = o[c];
-#pragma unroll
-    for (int c = 0; c < 6; ++c) { sm[t.s_V + 6 * l + c] = V[c]; sm[t.s_A + 6 * l + c] = A[c]; }
-}
 
-// P1c: spatial inertia about p0 and Newton-Euler force of link l (independent per link)
-MI_D void wave_link_dynamics(const DevModel& m, const WaveTabs& t, float* sm, int l) {
     float I[10] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
     float F[6] = {0, 0, 0, 0, 0, 0};
-    const float mass = m.mass[l];
+    const float mass = mc.lf(MC_MASS, l);
     if (mass > 0.0f) {
-        float R[9], o[3], V[6], A[6];
-#pragma unroll
-        for (int c = 0; c < 9; ++c) R[c] = sm[t.s_R + 9 * l + c];
-#pragma unroll
-        for (int c = 0; c < 3; ++c) o[c] = sm[t.s_o + 3 * l + c];
-#pragma unroll
-        for (int c = 0; c < 6; ++c) { V[c] = sm[t.s_V + 6 * l + c]; A[c] = sm[t.s_A + 6 * l + c]; }
-        float c3[3], T[9], Iw[9];
-        m3_vec(R, m.com + 3 * l, c3);
+        float c3[3], T[9], Iw[9], com[3];
+        mc.lf3(MC_COM, l, com);
+        m3_vec(R, com, c3);
         c3[0] += o[0]; c3[1] += o[1]; c3[2] += o[2];
-        const float* in = m.inertia + 6 * l;
+        float in[6];
+#pragma unroll
+        for (int c = 0; c < 6; ++c) in[c] = mc.lf(MC_INER + c, l);
         const float Ib[9] = {in[0], in[3], in[4], in[3], in[1], in[5], in[4], in[5], in[2]};
         m3_mul(R, Ib, T);
 #pragma unroll
@@ -365,9 +405,9 @@ MI_D void wave_artic_substep(const DevModel& m, const WaveTabs& t, const DevStat
     float* us = sm + t.s_us;   // u, then u*
     float* rhs = sm + t.s_r;
     float* Mx = sm + t.s_M;    // M (lower), then dense padded M~^-1 [WNV][WNV]
-    float* Xc = sm + t.s_X;    // X = L^-1 by columns: Xc[j*nv + i] = X_ij
     float* Dv = sm + t.s_D;
     float* Ss = sm + t.s_S;
+    const MC mc = make_mc(t, sm, L);
 
     STAMP(0);
     // ---- load state into LDS
@@ -386,14 +426,11 @@ MI_D void wave_artic_substep(const DevModel& m, const WaveTabs& t, const DevStat
 
     STAMP(1);
     // ---- P1a: local joint transforms, every link at once
-    for (int l = 1 + lane; l < L; l += 64) wave_link_local(m, t, sm, l);
+    for (int l = 1 + lane; l < L; l += 64) wave_link_local(mc, t, sm, l);
     __syncthreads();
     // ---- P1b+c: world frames / subspaces / velocities along each link's chain, then the
     // link's inertia and Newton-Euler force (same lane: no barrier in between)
-    for (int l = lane; l < L; l += 64) {
-        wave_link_chain(m, t, sm, l, p);
-        wave_link_dynamics(m, t, sm, l);
-    }
+    for (int l = lane; l < L; l += 64) wave_link_forward(mc, nr, t, sm, l, p);
     __syncthreads();
     STAMP(2);
     // ---- P2: composite inertia / force = own + sum over the subtree (fixed descendant order,
@@ -405,8 +442,8 @@ MI_D void wave_artic_substep(const DevModel& m, const WaveTabs& t, const DevStat
         for (int q = 0; q < 10; ++q) I[q] = sm[t.s_Ic + 10 * l + q];
 #pragma unroll
         for (int q = 0; q < 6; ++q) F[q] = sm[t.s_F + 6 * l + q];
-        for (int di = t.desc_start[l]; di < t.desc_start[l + 1]; ++di) {
-            const int d = t.desc_list[di];
+        for (int di = mc.desc_start(l); di < mc.desc_start(l + 1); ++di) {
+            const int d = mc.desc(di);
 #pragma unroll
             for (int q = 0; q < 10; ++q) I[q] += sm[t.s_Ic + 10 * d + q];
 #pragma unroll
@@ -421,7 +458,7 @@ MI_D void wave_artic_substep(const DevModel& m, const WaveTabs& t, const DevStat
     STAMP(3);
     // ---- P3: bias + CRBA (lane k = dof k)
     if (lane < nv) {
-        const int k = lane, l = m.dof_link[k];
+        const int k = lane, l = k < nr ? 0 : k - nr + 1;
         float s[6], I[10], f[6], F[6];
 #pragma unroll
         for (int c = 0; c < 6; ++c) { s[c] = Ss[6 * k + c]; F[c] = aux[16 * l + 10 + c]; }
@@ -431,17 +468,33 @@ MI_D void wave_artic_substep(const DevModel& m, const WaveTabs& t, const DevStat
         float diag = dot6(s, f);
         float r = -dot6(s, F);
         if (k >= nr) {
-            diag += m.armature[l] + dt * m.damping[l];
-            r += st.eff[(size_t)(k - nr) * N + i] - m.damping[l] * us[k];
+            const float damp = mc.lf(MC_DAMP, l);
+            diag += mc.lf(MC_ARM, l) + dt * damp;
+            r += st.eff[(size_t)(k - nr) * N + i] - damp * us[k];
         }
         Mx[k * nv + k] = diag;
         rhs[k] = r;
-        for (int a = t.anc_start[k]; a < t.anc_start[k + 1]; ++a) {
-            const int j = t.anc_list[a];
-            float sj[6];
+        if constexpr (TP::kCT) {
+            // ancestors of k from the link's DOF mask (root DOFs: the root chain below k);
+            // uniform j: the S_j reads are LDS broadcasts
+            const unsigned am = k < nr ? (1u << k) - 1u : mc.mask(l) & ~(1u << k);
+            sfor<0, TP::nv>([&](auto J) {
+                constexpr int j = J;
+                if ((am >> j) & 1u) {
+                    float sj[6];
 #pragma unroll
-            for (int c = 0; c < 6; ++c) sj[c] = Ss[6 * j + c];
-            Mx[k * nv + j] = dot6(sj, f);
+                    for (int c = 0; c < 6; ++c) sj[c] = Ss[6 * j + c];
+                    Mx[k * nv + j] = dot6(sj, f);
+                }
+            });
+        } else {
+            for (int a = t.anc_start[k]; a < t.anc_start[k + 1]; ++a) {
+                const int j = t.anc_list[a];
+                float sj[6];
+#pragma unroll
+                for (int c = 0; c < 6; ++c) sj[c] = Ss[6 * j + c];
+                Mx[k * nv + j] = dot6(sj, f);
+            }
         }
     }
     __syncthreads();
@@ -505,17 +558,16 @@ MI_D void wave_artic_substep(const DevModel& m, const WaveTabs& t, const DevStat
         bool act = false;
         float pc[3] = {0, 0, 0}, bn = 0.0f;
         int l = 0;
-        if (lane < m.npts) {
-            const int g = m.pt_geom[lane];
-            l = m.geom_link[g];
-            const float* pl = m.pt_end[lane] ? m.geom_p1 + 3 * g : m.geom_p0 + 3 * g;
+        if (lane < t.npts) {
+            l = (int)mc.pf(MP_LINK, lane);
+            const float pl[3] = {mc.pf(MP_X, lane), mc.pf(MP_X + 1, lane), mc.pf(MP_X + 2, lane)};
             float R[9], x[3];
 #pragma unroll
             for (int q = 0; q < 9; ++q) R[q] = sm[t.s_R + 9 * l + q];
             m3_vec(R, pl, x);
 #pragma unroll
             for (int q = 0; q < 3; ++q) x[q] += sm[t.s_o + 3 * l + q];
-            const float r = m.geom_radius[g];
+            const float r = mc.pf(MP_RAD, lane);
             const float gap = rpz + x[2] - r;
             act = gap < p.contact_offset;
             pc[0] = x[0]; pc[1] = x[1]; pc[2] = x[2] - r;
@@ -551,7 +603,7 @@ MI_D void wave_artic_substep(const DevModel& m, const WaveTabs& t, const DevStat
         float bl = 0.0f, sg = 0.0f;
         if (lane < D) {
             const int l = lane + 1, k = nr + lane;
-            const float lo = m.lower[l], hi = m.upper[l];
+            const float lo = mc.lf(MC_LO, l), hi = mc.lf(MC_HI, l);
             if (lo < hi) {
                 const float qj = sm[t.s_q + lane];
                 const float qp = qj + dt * us[k];
@@ -581,7 +633,7 @@ MI_D void wave_artic_substep(const DevModel& m, const WaveTabs& t, const DevStat
         const float lk = sm[t.s_rl + r];
         if (lk >= 0.0f) {
             const int l = (int)lk;
-            const unsigned long long msk = t.link_mask[l];
+            const unsigned long long msk = mc.mask(l);
             float f[6];
 #pragma unroll
             for (int q = 0; q < 6; ++q) f[q] = sm[t.s_rf + 6 * r + q];
@@ -665,7 +717,7 @@ MI_D void wave_artic_substep(const DevModel& m, const WaveTabs& t, const DevStat
 #pragma unroll
                 for (int q = 0; q < 6; ++q) f[q] = sm[t.s_rf + 6 * r + q];
                 const float lk = sm[t.s_rl + r];
-                msk = lk >= 0.0f ? (unsigned)t.link_mask[(int)lk] : 1u << (int)(-lk - 1.0f);
+                msk = lk >= 0.0f ? mc.mask((int)lk) : 1u << (int)(-lk - 1.0f);
             };
             if (lane < nrows) load_row(lane, b0, ia0, k0, fa, ma);
             if (lane + 64 < nrows) load_row(lane + 64, b1, ia1, k1, fb, mb);
@@ -733,11 +785,12 @@ MI_D void wave_artic_substep(const DevModel& m, const WaveTabs& t, const DevStat
     STAMP(11);
     // ---- P11a: force sensors (lane s)
     if (lane < m.S) {
-        const int si = lane, l = m.sensor_link[si];
+        const int si = lane, l = (int)mc.sf(MS_LINK, si);
         float R[9], xs[3], F[3] = {0, 0, 0}, T[3] = {0, 0, 0};
 #pragma unroll
         for (int q = 0; q < 9; ++q) R[q] = sm[t.s_R + 9 * l + q];
-        m3_vec(R, m.sensor_pos + 3 * si, xs);
+        const float sp[3] = {mc.sf(MS_X, si), mc.sf(MS_X + 1, si), mc.sf(MS_X + 2, si)};
+        m3_vec(R, sp, xs);
 #pragma unroll
         for (int q = 0; q < 3; ++q) xs[q] += sm[t.s_o + 3 * l + q];
         for (int c = 0; c < ncon; ++c) {

