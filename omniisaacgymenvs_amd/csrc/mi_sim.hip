@@ -655,6 +655,9 @@ int mi_sim_create(const mi_model_desc* md, const mi_sim_params* prm, int32_t N, 
         }
         t.max_rows = m.max_rows;
         t.g_row_stride = (size_t)m.max_rows * WNV;
+        // CT path: F, Ic, M, aux, D, rhs (contiguous, dead after P7) hold the first W rows
+        t.s_W = t.s_F;
+        t.w_rows_lds = s->topo ? std::min(64, (t.s_us - t.s_F) / m.nv) : 0;
         s->lds_bytes = (size_t)so * sizeof(float);
     }
     s->lower.assign(md->lower, md->lower + L);

@@ -69,6 +69,9 @@ struct WaveTabs {
         s_rl, s_rf, s_rb, s_rk, s_ad, s_xs, s_total;
     int max_rows;
     size_t g_row_stride;  // floats per env in the global W-row slab (max_rows * WNV)
+    // W rows [0, w_rows_lds) are handed from P9 to P10 through LDS at s_W (stride nv, in the
+    // span that is dead by then); rows beyond go through the global slab
+    int s_W, w_rows_lds;
     // per-model constant block (see McLayout): global copy, staged into LDS at s_mc once per
     // launch by every workgroup
     const float* g_mc;
@@ -674,8 +677,15 @@ MI_D void wave_artic_substep(const DevModel& m, const WaveTabs& t, const DevStat
 #pragma unroll
         for (int c = 0; c < WNV; ++c) a += jr[c] * wr[c];
         sm[t.s_ad + r] = a > 1e-12f ? a : 1e-12f;
+        if (nrows <= t.w_rows_lds) {   // uniform: every row of this substep fits in LDS
+            float* wl = sm + t.s_W + r * nv;
 #pragma unroll
-        for (int c = 0; c < WNV; ++c) gW[(size_t)r * WNV + c] = wr[c];
+            for (int c = 0; c < WNV; ++c)
+                if (c < nv) wl[c] = wr[c];
+        } else {
+#pragma unroll
+            for (int c = 0; c < WNV; ++c) gW[(size_t)r * WNV + c] = wr[c];
+        }
     }
     __syncthreads();
 
@@ -693,13 +703,28 @@ MI_D void wave_artic_substep(const DevModel& m, const WaveTabs& t, const DevStat
         float S6[6];
 #pragma unroll
         for (int q = 0; q < 6; ++q) S6[q] = kl < nv ? Ss[6 * kl + q] : 0.0f;
-        // Bounded buffer loads: the descriptor covers rows [0, nrows), so slots past the last
-        // row read as 0 without touching memory (no per-row branch, no wasted traffic).
+        // W rows: from LDS when this substep's rows all fit there (uniform branch), else by
+        // bounded buffer loads from the slab (the descriptor covers rows [0, nrows), so slots
+        // past the last row read as 0 without touching memory).
+        // one bank (nrows <= 64): both half-waves hold rows 0..63, so every lane applies every
+        // row's update and no half-to-half hand-over is needed; two banks: half h holds rows
+        // 64h .. 64h+63.
+        const bool one_bank = nrows <= 64;
         float Wr[64];
-        {
+        if (nrows <= t.w_rows_lds) {                  // implies one_bank (w_rows_lds <= 64)
+            const float km = kl < nv ? 1.0f : 0.0f;
+            const float* wl = sm + t.s_W + (kl < nv ? kl : 0);
+            if constexpr (TP::kCT) {
+#pragma unroll
+                for (int rr = 0; rr < 64; ++rr) Wr[rr] = wl[rr * TP::nv] * km;
+            } else {
+#pragma unroll
+                for (int rr = 0; rr < 64; ++rr) Wr[rr] = wl[rr * nv] * km;
+            }
+        } else {
             const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
                 (void*)gW, (short)0, nrows * WNV * (int)sizeof(float), 0x00020000);
-            const int vo = (64 * half * WNV + kl) * (int)sizeof(float);
+            const int vo = ((one_bank ? 0 : 64 * half) * WNV + kl) * (int)sizeof(float);
 #pragma unroll
             for (int rr = 0; rr < 64; ++rr)
                 Wr[rr] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(
@@ -724,57 +749,77 @@ MI_D void wave_artic_substep(const DevModel& m, const WaveTabs& t, const DevStat
         }
         const float mu = p.friction;
         float u = kl < nv ? us[kl] : 0.0f;
-        for (int it = 0; it < p.iters; ++it) {
-            // opaque per sweep: stops the compiler hoisting the loop-invariant readlanes of
-            // every row out of the iteration loop (they would pin hundreds of SGPRs and spill)
-            asm volatile("" : "+v"(b0), "+v"(b1), "+v"(ia0), "+v"(ia1), "+v"(k0), "+v"(k1),
-                         "+v"(ma), "+v"(mb));
-            asm volatile("" : "+v"(fa[0]), "+v"(fa[1]), "+v"(fa[2]), "+v"(fa[3]), "+v"(fa[4]),
-                         "+v"(fa[5]), "+v"(fb[0]), "+v"(fb[1]), "+v"(fb[2]), "+v"(fb[3]),
-                         "+v"(fb[4]), "+v"(fb[5]));
-            int nrow_it = nrows;   // opaque: 128 hoisted "r < nrows" masks would spill
-            asm volatile("" : "+s"(nrow_it));
+        // One Gauss-Seidel sweep schedule. Per row: J_r . u by a DPP half-wave sum, the
+        // projected lambda update, u += W_r dlambda. The next row's J (readlanes + dot6, no
+        // dependence on u) is built inside the current row's schedule region so it overlaps the
+        // reduction chain. The friction rows of a contact follow its normal row in the same
+        // sweep, so the normal's current lambda is carried in a wave-uniform value.
+        auto sweeps = [&](auto ONE_) {
+            constexpr bool ONE = decltype(ONE_)::value;
+            for (int it = 0; it < p.iters; ++it) {
+                // opaque per sweep: stops the compiler hoisting the loop-invariant readlanes of
+                // every row out of the iteration loop (they would pin hundreds of SGPRs)
+                asm volatile("" : "+v"(b0), "+v"(b1), "+v"(ia0), "+v"(ia1), "+v"(k0), "+v"(k1),
+                             "+v"(ma), "+v"(mb));
+                asm volatile("" : "+v"(fa[0]), "+v"(fa[1]), "+v"(fa[2]), "+v"(fa[3]), "+v"(fa[4]),
+                             "+v"(fa[5]), "+v"(fb[0]), "+v"(fb[1]), "+v"(fb[2]), "+v"(fb[3]),
+                             "+v"(fb[4]), "+v"(fb[5]));
+                int nrow_it = nrows;   // opaque: 128 hoisted "r < nrows" masks would spill
+                asm volatile("" : "+s"(nrow_it));
+                float lamn = 0.0f;
 #pragma unroll
-            for (int h = 0; h < 2; ++h) {
-                if (64 * h >= nrow_it) continue;
-                const float bb = h ? b1 : b0, ii = h ? ia1 : ia0, kk = h ? k1 : k0;
-                const unsigned mm = h ? mb : ma;
-                // fully unrolled (no early exit) so Wr stays register-indexed
+                for (int h = 0; h < (ONE ? 1 : 2); ++h) {
+                    if (64 * h >= nrow_it) continue;
+                    const float bb = h ? b1 : b0, ii = h ? ia1 : ia0, kk = h ? k1 : k0;
+                    const unsigned mm = h ? mb : ma;
+                    auto jrow = [&](int rr, int& kind) -> float {
+                        float fr[6];
 #pragma unroll
-                for (int rr = 0; rr < 64; ++rr) {
-                    const int r = rr + 64 * h;
-                    if (r >= nrow_it) continue;
-                    // keep each row's readlanes inside its own row (no SGPR hoisting)
-                    __builtin_amdgcn_sched_barrier(0);
-                    float fr[6];
+                        for (int q = 0; q < 6; ++q) fr[q] = readlane(h ? fb[q] : fa[q], rr);
+                        const unsigned msk = (unsigned)__builtin_amdgcn_readlane((int)mm, rr);
+                        kind = (int)readlane(kk, rr);
+                        const float jc = kind == 3 ? fr[0] : dot6(S6, fr);
+                        return ((msk >> kl) & 1u) ? jc : 0.0f;
+                    };
+                    int kind_c;
+                    float jc_c = jrow(0, kind_c);
+                    // fully unrolled (no early exit) so Wr stays register-indexed
 #pragma unroll
-                    for (int q = 0; q < 6; ++q) fr[q] = readlane(h ? fb[q] : fa[q], rr);
-                    const unsigned msk = (unsigned)__builtin_amdgcn_readlane((int)mm, rr);
-                    const int kind = (int)readlane(kk, rr);
-                    float jc = kind == 3 ? fr[0] : dot6(S6, fr);
-                    jc = ((msk >> kl) & 1u) ? jc : 0.0f;
-                    const float s = half_sums(jc * u);
-                    const float jv = readlane(s, h ? 63 : 31);
-                    const float br = readlane(bb, rr), iar = readlane(ii, rr);
-                    const float l0 = readlane(h ? lam1 : lam0, rr);
-                    float ln = l0 + (br - jv) * iar;
-                    if (kind == 1 || kind == 2) {
-                        const int rn = r - kind;
-                        const float ln_n = rn >= 64 ? readlane(lam1, rn - 64) : readlane(lam0, rn);
-                        const float lim = mu * ln_n;
-                        ln = ln > lim ? lim : (ln < -lim ? -lim : ln);
-                    } else {
-                        ln = ln > 0.0f ? ln : 0.0f;
+                    for (int rr = 0; rr < 64; ++rr) {
+                        const int r = rr + 64 * h;
+                        if (r >= nrow_it) continue;
+                        __builtin_amdgcn_sched_barrier(0);
+                        int kind_n = 0;
+                        float jc_n = 0.0f;
+                        if (rr + 1 < 64) jc_n = jrow(rr + 1, kind_n);
+                        const float s = half_sums(jc_c * u);
+                        const float jv = readlane(s, h ? 63 : 31);
+                        const float br = readlane(bb, rr), iar = readlane(ii, rr);
+                        const float l0 = readlane(h ? lam1 : lam0, rr);
+                        float ln = l0 + (br - jv) * iar;
+                        const bool fric = kind_c == 1 || kind_c == 2;
+                        const float lim = mu * lamn;
+                        ln = fmaxf(ln, fric ? -lim : 0.0f);     // normal / limit: lambda >= 0
+                        ln = fric ? fminf(ln, lim) : ln;         // friction: |lambda| <= mu lambda_n
+                        lamn = kind_c == 0 ? ln : lamn;
+                        const float dl = ln - l0;
+                        const int ln_id = lane_here(lane);
+                        if constexpr (ONE) {
+                            u += Wr[rr] * dl;
+                        } else {
+                            if ((ln_id >> 5) == h) u += Wr[rr] * dl;
+                        }
+                        if (ln_id == rr) { if (h) lam1 = ln; else lam0 = ln; }
+                        jc_c = jc_n;
+                        kind_c = kind_n;
                     }
-                    const float dl = ln - l0;
-                    const int ln_id = lane_here(lane);
-                    if ((ln_id >> 5) == h) u += Wr[rr] * dl;
-                    if (ln_id == rr) { if (h) lam1 = ln; else lam0 = ln; }
+                    // hand u to the other half for its sub-sweep
+                    if constexpr (!ONE) u = __shfl(u, kl + 32 * h, 64);
                 }
-                // hand u to the other half for its sub-sweep
-                u = __shfl(u, kl + 32 * h, 64);
             }
-        }
+        };
+        if (one_bank) sweeps(std::true_type{});
+        else sweeps(std::false_type{});
         if (lane < nv) us[lane] = u;
         if (lane < nrows) sm[t.s_ad + lane] = lam0;          // reuse: lambda of row lane
         if (lane + 64 < nrows) sm[t.s_ad + lane + 64] = lam1;
