@@ -293,7 +293,7 @@ __global__ __launch_bounds__(64) void k_sim_step_wave(const KParams* __restrict_
     stage_model_constants(t, smem);
     for (int s = 0; s < substeps; ++s) {
         const KParams* k = opaque_kp(kp);
-        wave_artic_substep<T>(k->m, k->t, k->st, k->p, i, smem, gW);
+        wave_artic_substep<T>(k->m, k->t, k->st, k->p, i, smem, gW, s == 0);
     }
 }
 
@@ -313,29 +313,21 @@ __global__ __launch_bounds__(64) void k_env_step_wave(const KParams* __restrict_
     const int i = blockIdx.x;
     const int lane = threadIdx.x;
     // 1. clamp + pre_physics_step (scalar task math on lane 0); model constants into LDS
-    if (lane == 0)
-        task_pre_env(m, st, tp, i, actions, reset_buf, progress_buf, pot, prev, actions_out, true);
+    STAMP_BEGIN();
+    wave_task_pre(m, t, st, tp, i, actions, reset_buf, progress_buf, pot, prev, actions_out);
     stage_model_constants(t, smem);
+    STAMP(13);
     // 2. controlFrequencyInv x World.step, wave-cooperative
     float* gW = rows + (size_t)i * t.g_row_stride;
     for (int s = 0; s < substeps; ++s) {
         const KParams* k = opaque_kp(kp);
-        wave_artic_substep<T>(k->m, k->t, k->st, k->p, i, smem, gW);
+        wave_artic_substep<T>(k->m, k->t, k->st, k->p, i, smem, gW, s == 0);
     }
-    // 3. post_physics_step + obs clamp (lane 0)
-    if (lane == 0) {
-        const int O = tp.O;
-        float* R = (obs_task ? obs_task : obs_out) + (size_t)O * i;
-        loco_post(m, st, tp, i, actions + (size_t)tp.A * i, tp.clip_actions, R, rew, reset_buf,
-                  progress_buf, pot, prev);
-        const float co = tp.clip_obs;
-        float* OUT = obs_out + (size_t)O * i;
-        if (obs_task) {
-            for (int k = 0; k < O; ++k) OUT[k] = clampf(R[k], -co, co);
-        } else if (co < INFINITY) {
-            for (int k = 0; k < O; ++k) OUT[k] = clampf(OUT[k], -co, co);
-        }
-    }
+    // 3. post_physics_step + obs clamp, wave-cooperative from the LDS-resident state
+    STAMP_RESET();
+    wave_loco_post(m, t, st, tp, i, smem, actions, obs_out, obs_task, rew, reset_buf, progress_buf,
+                   pot, prev);
+    STAMP(14);
 }
 
 __global__ void k_reset_idx(DevModel m, DevState st, DevTask tp, const int64_t* ids, int n,
@@ -397,7 +389,15 @@ int mi_abi_version(void) { return MI_ABI_VERSION; }
 int mi_debug_stamps(unsigned long long* out, int n) {
     if (!out || n <= 0 || n > 32) return MI_E_ARG;
     HIP_TRY(hipDeviceSynchronize());
-    HIP_TRY(hipMemcpyFromSymbol(out, HIP_SYMBOL(g_stamps), sizeof(unsigned long long) * n));
+    std::vector<unsigned long long> all((size_t)MI_STAMP_SLOTS * 32);
+    HIP_TRY(hipMemcpyFromSymbol(all.data(), HIP_SYMBOL(g_phase), all.size() * sizeof(unsigned long long)));
+    for (int k = 0; k < n; ++k) {
+        unsigned long long acc = 0;
+        for (size_t b = 0; b < (size_t)MI_STAMP_SLOTS; ++b) acc += all[b * 32 + k];
+        out[k] = acc;
+    }
+    std::fill(all.begin(), all.end(), 0ull);   // read-and-reset
+    HIP_TRY(hipMemcpyToSymbol(HIP_SYMBOL(g_phase), all.data(), all.size() * sizeof(unsigned long long)));
     return MI_OK;
 }
 #endif
@@ -511,8 +511,9 @@ int mi_sim_create(const mi_model_desc* md, const mi_sim_params* prm, int32_t N, 
     {
         const char* path = getenv("MI_SIM_PATH");
         const bool want_thread = path && std::string(path) == "thread";
+        // (the post-step keeps sensor wrenches + reward terms in the row-bias region)
         s->wave = m.dyn == MI_DYN_ARTICULATION && !want_thread && m.nv <= WNV && m.npts <= 64 &&
-                  m.max_rows <= 128 && L <= 64;
+                  m.max_rows <= 128 && L <= 64 && m.max_rows >= 6 * m.S + 3 * m.D;
     }
     if (s->wave) {
         const char* tsel = getenv("MI_SIM_TOPO");
@@ -626,6 +627,12 @@ int mi_sim_create(const mi_model_desc* md, const mi_sim_params* prm, int32_t N, 
             };
             t.mc_chs = put_ints(chain_start); t.mc_chl = put_ints(chain_list);
             t.mc_dss = put_ints(desc_start); t.mc_dsl = put_ints(desc_list);
+            std::vector<int> lim;
+            for (int l = 1; l < L; ++l)
+                if (md->lower[l] < md->upper[l]) lim.push_back(l - 1);
+            t.nlimc = (int)lim.size();
+            if (lim.empty()) lim.push_back(0);
+            t.mc_lim = put_ints(lim);
             pad4();
             t.mc_len = (int)mcb.size();
             t.npts = np; t.nsens = ns;
@@ -633,31 +640,51 @@ int mi_sim_create(const mi_model_desc* md, const mi_sim_params* prm, int32_t N, 
         }
 #undef UPW
         auto al4 = [](int x) { return (x + 3) & ~3; };
+        const bool ct = s->topo != 0;
         int so = 0;
         auto take = [&](int n) { const int at = so; so += al4(n); return at; };
         t.s_mc = take(t.mc_len);
         t.s_R = take(9 * L); t.s_o = take(3 * L); t.s_S = take(6 * m.nv);
+        // P1..P4 working span: link inertias / forces, M, aux (local transforms, composites).
+        // On the compiled-topology path it is dead once P4 has moved M into registers, and
+        // P8/P9 reuse it for the contact and row data and the first W rows.
+        const int span0 = so;
         t.s_F = take(6 * L); t.s_Ic = take(10 * L); t.s_M = take(m.nv * m.nv);
-        t.s_X = take(16 * L);  // aux: local transforms (P1), composite inertia / force (P2)
-        t.s_D = take(WNV); t.s_r = take(WNV); t.s_us = take(WNV);
-        t.s_q = take(WNV); t.s_rp = take(8); t.s_cp = take(3 * m.npts); t.s_cl = take(m.npts);
-        t.s_rl = take(m.max_rows); t.s_rf = take(6 * m.max_rows); t.s_rb = take(m.max_rows);
-        t.s_rk = take(m.max_rows); t.s_ad = take(m.max_rows);
+        t.s_X = take(16 * L);
+        const int span1 = so;
+        t.s_D = take(ct ? 4 : WNV); t.s_r = take(WNV); t.s_us = take(WNV);
+        t.s_q = take(WNV); t.s_rp = take(8);
+        const int R = m.max_rows;
+        const int rows_len = al4(3 * m.npts) + al4(m.npts) + 4 * al4(R) + WNV;
+        const bool overlay = ct && rows_len <= span1 - span0;
+        int ro = overlay ? span0 : so;
+        auto take_r = [&](int n) { const int at = ro; ro += al4(n); return at; };
+        t.s_cp = take_r(3 * m.npts); t.s_cl = take_r(m.npts); t.s_rl = take_r(R);
+        t.s_rb = take_r(R); t.s_rk = take_r(R); t.s_ad = take_r(R); t.s_lsg = take_r(WNV);
+        if (!overlay) so = ro;
         // lane-private solve vectors of the runtime-table solves (CT solves run in registers)
-        t.s_xs = take(s->topo ? 4 : WNV * 64);
+        t.s_xs = take(ct ? 4 : WNV * 64);
+        {   // CT path: published factor rows (each padded to 4) + 1/D (DofTree::lrow)
+            int lr = 0;
+            for (int k = 0; k < m.nv; ++k) lr += (anc_start[k + 1] - anc_start[k] + 3) & ~3;
+            t.s_L = take(ct ? lr + m.nv : 4);
+        }
         t.s_total = so;
-        {   // every region must be distinct: offsets strictly increase in declaration order
+        {   // the sequential regions strictly increase; the row data sits inside the dead
+            // span (overlay) or between s_rp and s_xs
             const int offs[] = {t.s_mc, t.s_R, t.s_o, t.s_S, t.s_F, t.s_Ic, t.s_M, t.s_X,
-                                t.s_D, t.s_r, t.s_us, t.s_q, t.s_rp, t.s_cp, t.s_cl, t.s_rl,
-                                t.s_rf, t.s_rb, t.s_rk, t.s_ad, t.s_xs, t.s_total};
+                                t.s_D, t.s_r, t.s_us, t.s_q, t.s_rp, t.s_xs, t.s_L, t.s_total};
             for (size_t c = 1; c < sizeof(offs) / sizeof(offs[0]); ++c)
                 if (offs[c] <= offs[c - 1]) return cleanup(fail(MI_E_STATE, "wave LDS layout: region %zu overlaps", c));
+            const bool rows_ok = overlay ? (t.s_cp == span0 && ro <= span1)
+                                         : (t.s_cp > t.s_rp && ro <= t.s_xs);
+            if (!rows_ok) return cleanup(fail(MI_E_STATE, "wave LDS layout: row data misplaced"));
         }
         t.max_rows = m.max_rows;
         t.g_row_stride = (size_t)m.max_rows * WNV;
-        // CT path: F, Ic, M, aux, D, rhs (contiguous, dead after P7) hold the first W rows
-        t.s_W = t.s_F;
-        t.w_rows_lds = s->topo ? std::min(64, (t.s_us - t.s_F) / m.nv) : 0;
+        // CT path: the rest of the dead span holds the first W rows (P9 -> P10 hand-over)
+        t.s_W = ro;
+        t.w_rows_lds = overlay ? std::min(64, (span1 - ro) / m.nv) : 0;
         s->lds_bytes = (size_t)so * sizeof(float);
     }
     s->lower.assign(md->lower, md->lower + L);

@@ -29,24 +29,44 @@ namespace mi {
 
 constexpr int WNV = 32;  // padded DOF count of the wave path
 
-// Diagnostic phase stamps (built only with -DMI_STAMPS into a separate library; the product
-// build compiles them out). Workgroup MI_STAMP_BLOCK records s_memtime at every phase
-// boundary of its last substep.
+// Diagnostic phase timers (built only with -DMI_STAMPS into a separate library; the product
+// build compiles them out). Every workgroup adds the s_memtime delta of each phase to its own
+// slot g_phase[block % MI_STAMP_SLOTS][id] (lane 0, plain adds: no contention); [31] counts
+// substeps. The host sums the slots. IDs: see tools/phase_stamps.py.
 #ifdef MI_STAMPS
-#define MI_STAMP_BLOCK 7
-__device__ unsigned long long g_stamps[32];
-#define STAMP(k)                                                                          \
+#define MI_STAMP_SLOTS 16384
+__device__ unsigned long long g_phase[MI_STAMP_SLOTS][32];
+#define STAMP_BEGIN()                                                                     \
+    unsigned long long stamp_t_;                                                          \
+    do {                                                                                  \
+        __builtin_amdgcn_sched_barrier(0);                                                \
+        asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(stamp_t_)::"memory");  \
+        __builtin_amdgcn_sched_barrier(0);                                                \
+    } while (0)
+#define STAMP(id)                                                                         \
     do {                                                                                  \
         __builtin_amdgcn_sched_barrier(0);                                                \
         unsigned long long t_;                                                            \
         asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t_)::"memory");         \
-        if (blockIdx.x == MI_STAMP_BLOCK && threadIdx.x == 0) g_stamps[k] = t_;           \
+        if (threadIdx.x == 0) g_phase[blockIdx.x % MI_STAMP_SLOTS][id] += t_ - stamp_t_;  \
+        stamp_t_ = t_;                                                                    \
+        __builtin_amdgcn_sched_barrier(0);                                                \
+    } while (0)
+#define STAMP_END()                                                                       \
+    do {                                                                                  \
+        if (threadIdx.x == 0) g_phase[blockIdx.x % MI_STAMP_SLOTS][31] += 1ull;           \
+    } while (0)
+#define STAMP_RESET()                                                                     \
+    do {                                                                                  \
+        __builtin_amdgcn_sched_barrier(0);                                                \
+        asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(stamp_t_)::"memory");  \
         __builtin_amdgcn_sched_barrier(0);                                                \
     } while (0)
 #else
-#define STAMP(k) \
-    do {         \
-    } while (0)
+#define STAMP_RESET() do { } while (0)
+#define STAMP_BEGIN() do { } while (0)
+#define STAMP(id) do { } while (0)
+#define STAMP_END() do { } while (0)
 #endif
 
 struct WaveTabs {
@@ -66,7 +86,7 @@ struct WaveTabs {
     const unsigned char* tri_q;
     // LDS float offsets
     int s_mc, s_R, s_o, s_S, s_F, s_Ic, s_M, s_X, s_D, s_r, s_us, s_q, s_rp, s_cp, s_cl,
-        s_rl, s_rf, s_rb, s_rk, s_ad, s_xs, s_total;
+        s_rl, s_lsg, s_rb, s_rk, s_ad, s_xs, s_L, s_total;
     int max_rows;
     size_t g_row_stride;  // floats per env in the global W-row slab (max_rows * WNV)
     // W rows [0, w_rows_lds) are handed from P9 to P10 through LDS at s_W (stride nv, in the
@@ -75,8 +95,9 @@ struct WaveTabs {
     // per-model constant block (see McLayout): global copy, staged into LDS at s_mc once per
     // launch by every workgroup
     const float* g_mc;
-    int mc_len, mc_pts, mc_sens, mc_chs, mc_chl, mc_dss, mc_dsl;   // offsets inside the block
+    int mc_len, mc_pts, mc_sens, mc_chs, mc_chl, mc_dss, mc_dsl, mc_lim;   // block offsets
     int npts, nsens;
+    int nlimc;   // joints with a limit (lower < upper): limit-row candidates, joint ids at mc_lim
 };
 
 // Per-model constants in the LDS block, structure-of-arrays so lane-indexed reads (lane = link,
@@ -106,7 +127,19 @@ struct MC {
     MI_D int chain(int j) const { return bi[t->mc_chl + j]; }
     MI_D int desc_start(int l) const { return bi[t->mc_dss + l]; }
     MI_D int desc(int j) const { return bi[t->mc_dsl + j]; }
+    MI_D int lim(int j) const { return bi[t->mc_lim + j]; }
 };
+
+// Spatial force direction of contact row r = 3 ci + tt at contact point pc: normal (tt 0,
+// +z) or friction (tt 1: +x, tt 2: +y), f = (pc x dir, dir). Rebuilt where needed from the
+// contact point instead of stored per row (saves 6 floats x rows of LDS); same arithmetic.
+MI_D void contact_row_f(const float* sm, const WaveTabs& t, int r, float (&f)[6]) {
+    const int ci = r / 3, tt = r - 3 * ci;
+    const float pc[3] = {sm[t.s_cp + 3 * ci], sm[t.s_cp + 3 * ci + 1], sm[t.s_cp + 3 * ci + 2]};
+    const float dir[3] = {tt == 1 ? 1.0f : 0.0f, tt == 2 ? 1.0f : 0.0f, tt == 0 ? 1.0f : 0.0f};
+    cross3(pc, dir, f);
+    f[3] = dir[0]; f[4] = dir[1]; f[5] = dir[2];
+}
 
 MI_D MC make_mc(const WaveTabs& t, float* sm, int L) {
     MC c;
@@ -258,6 +291,61 @@ MI_D void ct_solve(float (&Mc)[T::nvc], float dvec, float (&x)[T::nvc]) {
     });
 }
 
+// Publish the factor for the batched solves: lane j (column j) writes each entry L[i][j]
+// (j an ancestor of i) into row i's compact ancestor list, position = depth(i) - depth(j) - 1
+// (lists run nearest ancestor first); then 1/D. dj = depth of DOF j (its ancestor count).
+template <class T>
+MI_D void ct_publish_factor(int lane, int dj, const float (&Mc)[T::nvc], float dvec, float* Lr) {
+    if (lane < T::nv) {
+        sfor<0, T::nv>([&](auto I) {
+            constexpr int i = I;
+            constexpr int na = T::dof.anc_start[i + 1] - T::dof.anc_start[i];
+            if ((T::dof.anc_mask[i] >> lane) & 1u) Lr[T::dof.lrow[i] + na - 1 - dj] = Mc[i];
+        });
+        Lr[T::dof.lrow[T::nv] + lane] = dvec;
+    }
+}
+
+// x <- M~^-1 x on a lane-private register vector (a: see below), factor entries read from the published
+// LDS rows: every read is a wave-uniform broadcast (no VALU readlanes; adjacent entries
+// merge into wide LDS reads). Same operation order as ct_solve / tree_solve_lds.
+template <class T>
+MI_D void ct_solve_l(const float* Lr, float (&x)[T::nvc], float& a) {
+    sfor_down<0, T::nv>([&](auto I) {                 // x <- L^-T x (leaves -> root)
+        constexpr int i = I;
+        constexpr int a0 = T::dof.anc_start[i], na = T::dof.anc_start[i + 1] - a0;
+        constexpr int off = T::dof.lrow[i];
+#pragma unroll
+        for (int c = 0; c < T::nv; ++c) asm volatile("" : "+v"(x[c]));   // step fence
+        const float xi = x[i];
+        sfor<0, na>([&](auto A) {
+            constexpr int j = T::dof.anc[a0 + A];
+            x[j] -= Lr[off + A] * xi;
+        });
+    });
+    // x <- D^-1 x; a = y^T D^-1 y with y = L^-T x_in, i.e. x_in^T M~^-1 x_in (for x_in = J_r^T
+    // this is A_rr = J_r W_r, computed before the second pass needs no copy of J_r)
+    a = 0.0f;
+    sfor<0, T::nv>([&](auto I) {
+        const float y = x[I];
+        x[I] = y * Lr[T::dof.lrow[T::nv] + I];
+        a += y * x[I];
+    });
+    sfor<0, T::nv>([&](auto I) {                      // x <- L^-1 x (root -> leaves)
+        constexpr int i = I;
+        constexpr int a0 = T::dof.anc_start[i], na = T::dof.anc_start[i + 1] - a0;
+        constexpr int off = T::dof.lrow[i];
+#pragma unroll
+        for (int c = 0; c < T::nv; ++c) asm volatile("" : "+v"(x[c]));
+        float xi = x[i];
+        sfor<0, na>([&](auto A) {
+            constexpr int j = T::dof.anc[a0 + A];
+            xi -= Lr[off + A] * x[j];
+        });
+        x[i] = xi;
+    });
+}
+
 // P1a: local joint transform of link l >= 1 (independent of every other link):
 // aux[15 l ..] = {Rloc = Rq Rot(axis, q) (9), tloc (3), aloc = Rq axis (3)}
 MI_D void wave_link_local(const MC& mc, const WaveTabs& t, float* sm, int l) {
@@ -401,7 +489,7 @@ MI_D void wave_link_forward(const MC& mc, int nr, const WaveTabs& t, float* sm, 
 // sm: this env's LDS region; gW: this env's global slab of W rows [max_rows][WNV].
 template <class TP>
 MI_D void wave_artic_substep(const DevModel& m, const WaveTabs& t, const DevState& st,
-                             const SimP& p, int i, float* sm, float* gW) {
+                             const SimP& p, int i, float* sm, float* gW, bool load_state) {
     const int lane = threadIdx.x;
     const int N = st.N, L = m.L, D = m.D, nv = m.nv, nr = m.nr;
     const float dt = p.dt;
@@ -412,13 +500,16 @@ MI_D void wave_artic_substep(const DevModel& m, const WaveTabs& t, const DevStat
     float* Ss = sm + t.s_S;
     const MC mc = make_mc(t, sm, L);
 
-    STAMP(0);
-    // ---- load state into LDS
-    if (lane < 3) sm[t.s_rp + lane] = st.root_pos[(size_t)lane * N + i];
-    if (lane < 4) sm[t.s_rp + 4 + lane] = st.root_quat[(size_t)lane * N + i];
-    if (lane < nr) us[lane] = st.root_vel[(size_t)lane * N + i];
-    else if (lane < nv) us[lane] = st.qd[(size_t)(lane - nr) * N + i];
-    if (lane < D) sm[t.s_q + lane] = st.q[(size_t)lane * N + i];
+    STAMP_BEGIN();
+    // ---- load state into LDS (later substeps of a launch start from the state the previous
+    // substep's P11 left in LDS)
+    if (load_state) {
+        if (lane < 3) sm[t.s_rp + lane] = st.root_pos[(size_t)lane * N + i];
+        if (lane < 4) sm[t.s_rp + 4 + lane] = st.root_quat[(size_t)lane * N + i];
+        if (lane < nr) us[lane] = st.root_vel[(size_t)lane * N + i];
+        else if (lane < nv) us[lane] = st.qd[(size_t)(lane - nr) * N + i];
+        if (lane < D) sm[t.s_q + lane] = st.q[(size_t)lane * N + i];
+    }
     if (nr && lane < 6) {
         float s[6] = {0, 0, 0, 0, 0, 0};
         if (lane < 3) s[3 + lane] = 1.0f; else s[lane - 3] = 1.0f;
@@ -427,7 +518,7 @@ MI_D void wave_artic_substep(const DevModel& m, const WaveTabs& t, const DevStat
     }
     __syncthreads();
 
-    STAMP(1);
+    STAMP(0);   // load
     // ---- P1a: local joint transforms, every link at once
     for (int l = 1 + lane; l < L; l += 64) wave_link_local(mc, t, sm, l);
     __syncthreads();
@@ -435,7 +526,7 @@ MI_D void wave_artic_substep(const DevModel& m, const WaveTabs& t, const DevStat
     // link's inertia and Newton-Euler force (same lane: no barrier in between)
     for (int l = lane; l < L; l += 64) wave_link_forward(mc, nr, t, sm, l, p);
     __syncthreads();
-    STAMP(2);
+    STAMP(1);   // P1
     // ---- P2: composite inertia / force = own + sum over the subtree (fixed descendant order,
     // every link at once; results into the aux region: Ic at 16 l, F at 16 l + 10)
     float* aux = sm + t.s_X;
@@ -458,7 +549,7 @@ MI_D void wave_artic_substep(const DevModel& m, const WaveTabs& t, const DevStat
         for (int q = 0; q < 6; ++q) aux[16 * l + 10 + q] = F[q];
     }
     __syncthreads();
-    STAMP(3);
+    STAMP(2);   // P2
     // ---- P3: bias + CRBA (lane k = dof k)
     if (lane < nv) {
         const int k = lane, l = k < nr ? 0 : k - nr + 1;
@@ -501,7 +592,7 @@ MI_D void wave_artic_substep(const DevModel& m, const WaveTabs& t, const DevStat
         }
     }
     __syncthreads();
-    STAMP(4);
+    STAMP(3);   // P3
     // ---- P4: LTDL in place (M = L^T D L, L strictly below the diagonal)
     float Mc[TP::nvc];     // CT path: column `lane` of M~, then of its factor (rows 0..nv-1)
     float dvec = 1.0f;    // CT path: lane c holds 1 / D_c
@@ -509,6 +600,8 @@ MI_D void wave_artic_substep(const DevModel& m, const WaveTabs& t, const DevStat
         ct_load_columns<TP>(Mx, lane, Mc);
         ct_ltdl<TP>(lane, Mc);
         dvec = ct_dinv<TP>(lane, Mc);
+        const int dj = lane < nr ? lane : __builtin_popcount(mc.mask(lane < nv ? lane - nr + 1 : 0)) - 1;
+        ct_publish_factor<TP>(lane, dj, Mc, dvec, sm + t.s_L);
     } else {
         for (int k = nv - 1; k >= 0; --k) {
             const int a0 = t.anc_start[k], na = t.anc_start[k + 1] - a0;
@@ -526,34 +619,15 @@ MI_D void wave_artic_substep(const DevModel& m, const WaveTabs& t, const DevStat
             __syncthreads();
         }
     }
-    STAMP(5);
+    STAMP(4);   // P4 (+ factor publish)
     // ---- P5: 1/D of the factor
     if constexpr (!TP::kCT) {
         if (lane < nv) Dv[lane] = 1.0f / Mx[lane * nv + lane];
         __syncthreads();
     }
-    STAMP(6);
-    STAMP(7);
-    // ---- P7: u* = u + dt M~^-1 rhs
-    float* xs = sm + t.s_xs + lane;   // generic path: this lane's private solve vector (stride 64)
-    if constexpr (TP::kCT) {
-        float x[TP::nvc];              // every lane solves the same vector (LDS broadcasts)
-        sfor<0, TP::nv>([&](auto I) { x[I] = rhs[I]; });
-        // opaque: a provably uniform vector would be solved in SGPRs (and spill)
-#pragma unroll
-        for (int c = 0; c < TP::nv; ++c) asm volatile("" : "+v"(x[c]));
-        ct_solve<TP>(Mc, dvec, x);
-        if (lane == 0) sfor<0, TP::nv>([&](auto I) { us[I] = us[I] + dt * x[I]; });
-    } else {
-        if (lane == 0) {
-            for (int c = 0; c < nv; ++c) xs[c * 64] = rhs[c];
-            tree_solve_lds(t, Mx, Dv, nv, xs);
-            for (int c = 0; c < nv; ++c) us[c] = us[c] + dt * xs[c * 64];
-        }
-    }
-    __syncthreads();
+    STAMP(5);   // P5
 
-    STAMP(8);
+
     // ---- P8: candidate contact points (lane c), ballot compaction in candidate order
     int ncon = 0;
     {
@@ -588,20 +662,38 @@ MI_D void wave_artic_substep(const DevModel& m, const WaveTabs& t, const DevStat
 #pragma unroll
             for (int tt = 0; tt < 3; ++tt) {
                 const int r = 3 * ci + tt;
-                const float dir[3] = {tt == 1 ? 1.0f : 0.0f, tt == 2 ? 1.0f : 0.0f, tt == 0 ? 1.0f : 0.0f};
-                float f[6];
-                cross3(pc, dir, f);
-                f[3] = dir[0]; f[4] = dir[1]; f[5] = dir[2];
-#pragma unroll
-                for (int q = 0; q < 6; ++q) sm[t.s_rf + 6 * r + q] = f[q];
                 sm[t.s_rl + r] = (float)l;
                 sm[t.s_rb + r] = tt == 0 ? bn : 0.0f;
                 sm[t.s_rk + r] = (float)tt;
             }
         }
     }
-    int nrows = 3 * ncon;
-    {
+    const int nc = 3 * ncon;
+    __syncthreads();
+
+    STAMP(6);   // P8 contacts
+    // ---- P7+P9: one batch, lanes over solve vectors b (64 per pass):
+    //   b = 0                 rhs          -> u* = u + dt M~^-1 rhs
+    //   b = 1 .. nlim         e_k of each limited DOF k (limit-row candidates; the row's
+    //                         sign +-1 is applied once the limit test has run: exact)
+    //   b = 1 + nlim + r      contact row r: J_r, W_r = M~^-1 J_r^T, A_rr = J_r . W_r
+    // The limit test needs u*, so it runs inside the first pass (uniform barrier); limit rows
+    // follow the contact rows in DOF order, as in the oracle.
+    const int nlim = t.nlimc;
+    const int total = 1 + nlim + nc;
+    int nrows = nc;
+    unsigned long long limact = 0ull;   // bit d: joint d has an active limit row
+    float* xs = sm + t.s_xs + lane;     // generic path: this lane's private solve vector
+    // u* (lane 0's solution) and the limit rows: first pass only, uniform barriers
+    auto limit_rows = [&](const auto& res) {
+        constexpr int NR = sizeof(res) / sizeof(res[0]);
+        if (lane == 0) {
+#pragma unroll
+            for (int c = 0; c < NR; ++c)
+                if (c < nv) us[c] = us[c] + dt * res[c];
+        }
+        __syncthreads();
+        // limit rows from u* (lane = joint), compacted after the contact rows
         bool act = false;
         float bl = 0.0f, sg = 0.0f;
         if (lane < D) {
@@ -617,79 +709,133 @@ MI_D void wave_artic_substep(const DevModel& m, const WaveTabs& t, const DevStat
                 if (bl > p.max_depen) bl = p.max_depen;
             }
         }
-        const unsigned long long mask = __ballot(act);
+        limact = __ballot(act);
         if (act) {
-            const int r = nrows + __popcll(mask & ((1ull << lane) - 1ull));
-            sm[t.s_rl + r] = -(float)(nr + lane) - 1.0f;  // negative: limit row on dof
-            sm[t.s_rf + 6 * r] = sg;
-            sm[t.s_rb + r] = bl;
-            sm[t.s_rk + r] = 3.0f;
+            const int rl = nc + __popcll(limact & ((1ull << lane) - 1ull));
+            sm[t.s_rl + rl] = -(float)(nr + lane) - 1.0f;  // negative: limit row on dof
+            sm[t.s_lsg + lane] = sg;   // sign of joint lane's limit row
+            sm[t.s_rb + rl] = bl;
+            sm[t.s_rk + rl] = 3.0f;
         }
-        nrows += __popcll(mask);
-    }
-    __syncthreads();
-
-    STAMP(9);
-    // ---- P9: lanes over rows: J_r, W_r = M~^-1 J_r^T (tree solve in registers), A_rr
-    for (int r = lane; r < nrows; r += 64) {
-        float jr[WNV];
-        const float lk = sm[t.s_rl + r];
-        if (lk >= 0.0f) {
-            const int l = (int)lk;
-            const unsigned long long msk = mc.mask(l);
-            float f[6];
+        nrows = __builtin_amdgcn_readfirstlane(nc + __popcll(limact));   // wave-uniform
+        __syncthreads();
+    };
+    // file this lane's W row: contact row r (A_rr given), or an active limit row with its sign
+    auto file_row = [&](const auto& res, bool on, int r, int kd, float a_contact) {
+        constexpr int NR = sizeof(res) / sizeof(res[0]);
+        int slot = -1;
+        float sc = 1.0f, a = 0.0f;
+        if (on && r >= 0) {
+            slot = r;
+            a = a_contact;
+        } else if (kd >= 0) {
+            const int d = kd - nr;
+            if ((limact >> d) & 1ull) {
+                slot = nc + __popcll(limact & ((1ull << d) - 1ull));
+                sc = sm[t.s_lsg + d];
+                float wk = 0.0f;
 #pragma unroll
-            for (int q = 0; q < 6; ++q) f[q] = sm[t.s_rf + 6 * r + q];
-#pragma unroll
-            for (int c = 0; c < WNV; ++c) {
-                float v = 0.0f;
-                if ((msk >> c) & 1ull) {
-                    float s[6];
-#pragma unroll
-                    for (int q = 0; q < 6; ++q) s[q] = Ss[6 * c + q];
-                    v = dot6(s, f);
-                }
-                jr[c] = v;
+                for (int c = 0; c < NR; ++c) wk = c == kd ? res[c] : wk;
+                a = wk;                          // J.W = sg^2 (M~^-1)_kk
             }
-        } else {
-            const int kd = (int)(-lk - 1.0f);
-            const float sg = sm[t.s_rf + 6 * r];
-#pragma unroll
-            for (int c = 0; c < WNV; ++c) jr[c] = c == kd ? sg : 0.0f;
         }
-        float wr[WNV];
-        if constexpr (TP::kCT) {
-            float x[TP::nvc];
-            sfor<0, TP::nv>([&](auto I) { x[I] = jr[I]; });
-            ct_solve<TP>(Mc, dvec, x);          // W_r = M~^-1 J_r^T, registers only
+        if (slot >= 0) {
+            sm[t.s_ad + slot] = a > 1e-12f ? a : 1e-12f;
+            if (nrows <= t.w_rows_lds) {   // uniform: every row of this substep fits in LDS
+                float* wl = sm + t.s_W + slot * nv;
 #pragma unroll
-            for (int c = 0; c < WNV; ++c) wr[c] = 0.0f;
-            sfor<0, TP::nv>([&](auto I) { wr[I] = x[I]; });
+                for (int c = 0; c < NR; ++c)
+                    if (c < nv) wl[c] = res[c] * sc;
+            } else {
+#pragma unroll
+                for (int c = 0; c < WNV; ++c) gW[(size_t)slot * WNV + c] = c < NR ? res[c] * sc : 0.0f;
+            }
+        }
+    };
+    for (int base = 0; base < total; base += 64) {
+        const int bv = base + lane;
+        const bool on = bv < total;
+        const int r = bv - 1 - nlim;    // contact row (valid when r >= 0)
+        const int kd = (on && bv > 0 && r < 0) ? nr + mc.lim(bv - 1) : -1;   // limit candidate
+        if constexpr (TP::kCT) {
+            // solve vector built in place: J_r, e_kd or the rhs
+            float x[TP::nvc];
+            if (on && r >= 0) {
+                const int l = (int)sm[t.s_rl + r];
+                const unsigned msk = mc.mask(l);
+                float f[6];
+                contact_row_f(sm, t, r, f);
+                sfor<0, TP::nv>([&](auto C) {
+                    constexpr int c = C;
+                    float v = 0.0f;
+                    if ((msk >> c) & 1u) {
+                        float sv[6];
+#pragma unroll
+                        for (int q = 0; q < 6; ++q) sv[q] = Ss[6 * c + q];
+                        v = dot6(sv, f);
+                    }
+                    x[c] = v;
+                });
+            } else {
+                sfor<0, TP::nv>([&](auto C) {
+                    constexpr int c = C;
+                    x[c] = bv == 0 ? rhs[c] : (kd == c ? 1.0f : 0.0f);
+                });
+            }
+            STAMP(7);   // P9 J build
+            float a;                              // J M~^-1 J^T from the half solve
+            ct_solve_l<TP>(sm + t.s_L, x, a);     // factor rows from LDS broadcasts
+            STAMP(8);   // P9 solves
+            if (base == 0) {
+                limit_rows(x);
+                STAMP(9);   // P9 u* + limit rows
+            }
+            file_row(x, on, r, kd, a);
         } else {
+            float jr[WNV];
+#pragma unroll
+            for (int c = 0; c < WNV; ++c) jr[c] = 0.0f;
+            if (on && r >= 0) {
+                const int l = (int)sm[t.s_rl + r];
+                const unsigned long long msk = mc.mask(l);
+                float f[6];
+                contact_row_f(sm, t, r, f);
+#pragma unroll
+                for (int c = 0; c < WNV; ++c) {
+                    float v = 0.0f;
+                    if ((msk >> c) & 1ull) {
+                        float sv[6];
+#pragma unroll
+                        for (int q = 0; q < 6; ++q) sv[q] = Ss[6 * c + q];
+                        v = dot6(sv, f);
+                    }
+                    jr[c] = v;
+                }
+            }
+            STAMP(7);
+            float wr[WNV];
 #pragma unroll
             for (int c = 0; c < WNV; ++c)
-                if (c < nv) xs[c * 64] = jr[c];
-            tree_solve_lds(t, Mx, Dv, nv, xs);   // W_r = M~^-1 J_r^T
+                if (c < nv) xs[c * 64] = bv == 0 ? rhs[c] : (r >= 0 ? jr[c] : (kd == c ? 1.0f : 0.0f));
+            tree_solve_lds(t, Mx, Dv, nv, xs);
 #pragma unroll
             for (int c = 0; c < WNV; ++c) wr[c] = c < nv ? xs[c * 64] : 0.0f;
+            STAMP(8);
+            if (base == 0) {
+                limit_rows(wr);
+                STAMP(9);
+            }
+            float a = 0.0f;
+#pragma unroll
+            for (int c = 0; c < WNV; ++c) a += jr[c] * wr[c];
+            file_row(wr, on, r, kd, a);
         }
-        float a = 0.0f;
-#pragma unroll
-        for (int c = 0; c < WNV; ++c) a += jr[c] * wr[c];
-        sm[t.s_ad + r] = a > 1e-12f ? a : 1e-12f;
-        if (nrows <= t.w_rows_lds) {   // uniform: every row of this substep fits in LDS
-            float* wl = sm + t.s_W + r * nv;
-#pragma unroll
-            for (int c = 0; c < WNV; ++c)
-                if (c < nv) wl[c] = wr[c];
-        } else {
-#pragma unroll
-            for (int c = 0; c < WNV; ++c) gW[(size_t)r * WNV + c] = wr[c];
-        }
+        STAMP(10);
     }
+    nrows = __builtin_amdgcn_readfirstlane(nrows);
     __syncthreads();
 
-    STAMP(10);
+    STAMP(10);  // P9 row filing + trailing barrier
     // ---- P10: projected Gauss-Seidel. Lane k (mod 32) owns dof k; the wave's lower half
     // holds J / W of rows 0..63 in registers, the upper half rows 64..127. Rows are swept in
     // order; only the half owning the current row is active and u is copied across halves
@@ -739,10 +885,15 @@ MI_D void wave_artic_substep(const DevModel& m, const WaveTabs& t, const DevStat
                 b = sm[t.s_rb + r];
                 ia = 1.0f / sm[t.s_ad + r];
                 k = sm[t.s_rk + r];
-#pragma unroll
-                for (int q = 0; q < 6; ++q) f[q] = sm[t.s_rf + 6 * r + q];
                 const float lk = sm[t.s_rl + r];
-                msk = lk >= 0.0f ? mc.mask((int)lk) : 1u << (int)(-lk - 1.0f);
+                if (lk >= 0.0f) {
+                    contact_row_f(sm, t, r, f);
+                    msk = mc.mask((int)lk);
+                } else {
+                    const int kdof = (int)(-lk - 1.0f);
+                    f[0] = sm[t.s_lsg + kdof - nr];      // limit row: J = sg e_k
+                    msk = 1u << kdof;
+                }
             };
             if (lane < nrows) load_row(lane, b0, ia0, k0, fa, ma);
             if (lane + 64 < nrows) load_row(lane + 64, b1, ia1, k1, fb, mb);
@@ -827,7 +978,7 @@ MI_D void wave_artic_substep(const DevModel& m, const WaveTabs& t, const DevStat
 #endif
     __syncthreads();
 
-    STAMP(11);
+    STAMP(11);  // P10 PGS
     // ---- P11a: force sensors (lane s)
     if (lane < m.S) {
         const int si = lane, l = (int)mc.sf(MS_LINK, si);
@@ -856,6 +1007,8 @@ MI_D void wave_artic_substep(const DevModel& m, const WaveTabs& t, const DevStat
         for (int q = 0; q < 3; ++q) {
             st.sens[(size_t)(6 * si + q) * N + i] = Fl[q];
             st.sens[(size_t)(6 * si + 3 + q) * N + i] = Tl[q];
+            sm[t.s_rb + 6 * si + q] = Fl[q];         // LDS copy for the post-step (rb is
+            sm[t.s_rb + 6 * si + 3 + q] = Tl[q];     // dead after the PGS)
         }
     }
     // ---- P11b: integrate; non-finite -> nan flag
@@ -865,6 +1018,7 @@ MI_D void wave_artic_substep(const DevModel& m, const WaveTabs& t, const DevStat
         const float qn = sm[t.s_q + lane] + dt * v;
         st.qd[(size_t)lane * N + i] = v;
         st.q[(size_t)lane * N + i] = qn;
+        sm[t.s_q + lane] = qn;                       // final state stays in LDS (post-step)
         finite = isfinite(v) && isfinite(qn);
     }
     if (nr && lane == 0) {
@@ -900,6 +1054,12 @@ MI_D void wave_artic_substep(const DevModel& m, const WaveTabs& t, const DevStat
             for (int k = 0; k < 4; ++k) rq[k] = nq[k] * nn;
         }
 #pragma unroll
+        for (int k = 0; k < 3; ++k) sm[t.s_rp + k] = rp[k];
+#pragma unroll
+        for (int k = 0; k < 4; ++k) sm[t.s_rp + 4 + k] = rq[k];
+#pragma unroll
+        for (int k = 0; k < 6; ++k) us[k] = u6[k];
+#pragma unroll
         for (int k = 0; k < 3; ++k) { st.root_pos[(size_t)k * N + i] = rp[k]; finite &= isfinite(rp[k]); }
 #pragma unroll
         for (int k = 0; k < 4; ++k) { st.root_quat[(size_t)k * N + i] = rq[k]; finite &= isfinite(rq[k]); }
@@ -908,7 +1068,173 @@ MI_D void wave_artic_substep(const DevModel& m, const WaveTabs& t, const DevStat
     }
     if (__any(!finite) && lane == 0) st.nan_flag[i] = 1;
     __syncthreads();
-    STAMP(12);
+    STAMP(12);  // P11
+    STAMP_END();
+}
+
+// ---------------------------------------------------------------------------------------
+// Wave-cooperative task layer of the fused env step (locomotion tasks). Same formulas, same
+// evaluation order and the same Philox streams as the one-lane versions in mi_task.hpp; the
+// work is spread over lanes (lane j = DOF j) and reads the LDS-resident physics state.
+// ---------------------------------------------------------------------------------------
+
+// pre_physics_step (locomotion.py:103-145): mask-driven reset_idx, clamp, efforts
+MI_D void wave_task_pre(const DevModel& m, const WaveTabs& t, const DevState& st,
+                        const DevTask& tp, int i, const float* actions, int64_t* reset_buf,
+                        int64_t* progress_buf, float* potentials, float* prev_potentials,
+                        float* actions_out) {
+#pragma clang fp contract(off)
+    const int lane = threadIdx.x, N = st.N, D = m.D, A = tp.A;
+    if (reset_buf[i] != 0) {                     // wave-uniform
+        const uint64_t gid = (uint64_t)(st.off + i);
+        const uint32_t cnt = st.reset_count[i];
+        const float pn = tp.dof_pos_noise, vn = tp.dof_vel_noise;
+        const float pw = (float)((double)pn - (double)(-pn));
+        const float vw = (float)((double)vn - (double)(-vn));
+        if (lane < D) {
+            const int j = lane;
+            float u[4];
+            uniform4(st.seed, gid, cnt, (uint32_t)(j >> 2), 0, u);
+            float v = tp.init_dof[j] + (pw * u[j & 3] + (-pn));
+            const float lo = m.lower[j + 1], hi = m.upper[j + 1];
+            if (lo < hi) { v = v < hi ? v : hi; v = v > lo ? v : lo; }
+            st.q[(size_t)j * N + i] = v;
+            const int s = D + j;
+            uniform4(st.seed, gid, cnt, (uint32_t)(s >> 2), 0, u);
+            st.qd[(size_t)j * N + i] = vw * u[s & 3] + (-vn);
+        }
+        if (lane < 3) {
+            const float rp = st.origins[(size_t)lane * N + i] + tp.init_root_pos[lane];
+            st.root_pos[(size_t)lane * N + i] = rp;
+        }
+        if (lane < 4) st.root_quat[(size_t)lane * N + i] = tp.init_root_quat[lane];
+        if (lane < 6) st.root_vel[(size_t)lane * N + i] = 0.0f;
+        if (lane == 0) {
+            float rp[3];
+#pragma unroll
+            for (int k = 0; k < 3; ++k) rp[k] = st.origins[(size_t)k * N + i] + tp.init_root_pos[k];
+            float tx = tp.target[0] - rp[0], ty = tp.target[1] - rp[1];
+            float pot = -sqrtf(tx * tx + ty * ty + 0.0f * 0.0f) / tp.task_dt;
+            prev_potentials[i] = pot;
+            potentials[i] = pot;
+            st.reset_count[i] = cnt + 1;
+            reset_buf[i] = 0;
+            progress_buf[i] = 0;
+        }
+    }
+    if (lane < A) {
+        const int j = lane;
+        float a = clampf(actions[(size_t)A * i + j], -tp.clip_actions, tp.clip_actions);
+        if (actions_out) actions_out[(size_t)A * i + j] = a;
+        st.eff[(size_t)j * N + i] = a * tp.gears[j] * tp.power_scale;
+    }
+}
+
+// post_physics_step (rl_task.py:231-251 -> locomotion.py:80-101,173-183) + _process_data's obs
+// clamp, from the final physics state the last substep left in LDS. Writes the unclamped row
+// to obs_task (when given) and the clamped row to obs_out.
+MI_D void wave_loco_post(const DevModel& m, const WaveTabs& t, const DevState& st,
+                         const DevTask& tp, int i, float* sm, const float* actions,
+                         float* obs_out, float* obs_task, float* rew, int64_t* reset_buf,
+                         int64_t* progress_buf, float* potentials, float* prev_potentials) {
+#pragma clang fp contract(off)
+    const int lane = threadIdx.x, D = m.D, S = m.S, O = tp.O;
+    const float co = tp.clip_obs;
+    const float* us = sm + t.s_us;
+    float* out = obs_out + (size_t)O * i;
+    float* raw = obs_task ? obs_task + (size_t)O * i : nullptr;
+    auto put = [&](int k, float v) {
+        if (raw) raw[k] = v;
+        out[k] = clampf(v, -co, co);
+    };
+    float* terms = sm + t.s_rb + 6 * S;          // [3][D]: act^2, |a v| ratio, limit term
+    // per-DOF entries (lane j)
+    if (lane < D) {
+        const int j = lane;
+        const float pos = ref_unscale(sm[t.s_q + j], m.lower[j + 1], m.upper[j + 1]);
+        const float vel = us[m.nr + j] * tp.dof_vel_scale;
+        const float a = clampf(actions[(size_t)tp.A * i + j], -tp.clip_actions, tp.clip_actions);
+        put(12 + j, pos);
+        put(12 + D + j, vel);
+        put(12 + 2 * D + 6 * S + j, a);
+        terms[j] = a * a;
+        terms[D + j] = fabsf(a * vel) * tp.ratio[j];
+        if (tp.kind == MI_TASK_HUMANOID) {
+            const float aa = fabsf(pos);
+            const float sc = tp.joints_at_limit_cost * (aa - 0.98f) / 0.02f;
+            terms[2 * D + j] = (aa > 0.98f ? 1.0f : 0.0f) * sc * tp.ratio[j];
+        } else {
+            terms[2 * D + j] = pos > 0.99f ? 1.0f : 0.0f;
+        }
+    }
+    if (lane < 6 * S) put(12 + 2 * D + lane, sm[t.s_rb + lane] * tp.contact_force_scale);
+    __syncthreads();
+    if (lane == 0) {
+        float rp[3], rq[4], rv[6];
+#pragma unroll
+        for (int k = 0; k < 3; ++k) rp[k] = sm[t.s_rp + k];
+#pragma unroll
+        for (int k = 0; k < 4; ++k) rq[k] = sm[t.s_rp + 4 + k];
+#pragma unroll
+        for (int k = 0; k < 6; ++k) rv[k] = us[k];
+        float tt[3] = {tp.target[0] - rp[0], tp.target[1] - rp[1], tp.target[2] - rp[2]};
+        tt[2] = 0.0f;
+        const float prev_p = potentials[i];
+        const float nrm = sqrtf(tt[0] * tt[0] + tt[1] * tt[1] + tt[2] * tt[2]);
+        const float new_p = -nrm / tp.task_dt;
+        const float inv_start[4] = {1.0f, -0.0f, -0.0f, -0.0f};
+        float tq[4];
+        ref_quat_mul(rq, inv_start, tq);
+        const float b0[3] = {1.0f, 0.0f, 0.0f}, b1[3] = {0.0f, 0.0f, 1.0f};
+        float up[3], hd[3];
+        ref_quat_rotate<false>(tq, b1, up);
+        ref_quat_rotate<false>(tq, b0, hd);
+        float tn = sqrtf(tt[0] * tt[0] + tt[1] * tt[1] + tt[2] * tt[2]);
+        tn = tn > 1e-9f ? tn : 1e-9f;
+        const float td[3] = {tt[0] / tn, tt[1] / tn, tt[2] / tn};
+        const float heading_proj = hd[0] * td[0] + hd[1] * td[1] + hd[2] * td[2];
+        float vl[3], al[3];
+        ref_quat_rotate<true>(tq, rv, vl);
+        ref_quat_rotate<true>(tq, rv + 3, al);
+        float roll, pitch, yaw;
+        ref_get_euler_xyz(tq, roll, pitch, yaw);
+        const float walk = atan2f(tp.target[2] - rp[2], tp.target[0] - rp[0]);
+        const float angle_to_target = walk - yaw;
+        const float o10 = up[2], o11 = heading_proj;
+        put(0, rp[2]);
+        put(1, vl[0]); put(2, vl[1]); put(3, vl[2]);
+        put(4, al[0] * tp.angular_velocity_scale);
+        put(5, al[1] * tp.angular_velocity_scale);
+        put(6, al[2] * tp.angular_velocity_scale);
+        put(7, ref_normalize_angle(yaw));
+        put(8, ref_normalize_angle(roll));
+        put(9, ref_normalize_angle(angle_to_target));
+        put(10, o10);
+        put(11, o11);
+        potentials[i] = new_p;
+        prev_potentials[i] = prev_p;
+        // calculate_metrics: sums in DOF order, as loco_reward
+        float limit_cost = 0.0f, act_cost = 0.0f, elec = 0.0f;
+        if (tp.kind == MI_TASK_HUMANOID) {
+            for (int j = 0; j < D; ++j) limit_cost += terms[2 * D + j];
+        } else {
+            int64_t cnt = 0;
+            for (int j = 0; j < D; ++j) cnt += terms[2 * D + j] != 0.0f;
+            limit_cost = (float)cnt;
+        }
+        const float heading = o11 > 0.8f ? tp.heading_weight : tp.heading_weight * o11 / 0.8f;
+        const float upr = o10 > 0.93f ? 0.0f + tp.up_weight : 0.0f;
+        for (int j = 0; j < D; ++j) act_cost += terms[j];
+        for (int j = 0; j < D; ++j) elec += terms[D + j];
+        float total = (new_p - prev_p) + tp.alive_reward_scale + upr + heading -
+                      tp.actions_cost * act_cost - tp.energy_cost * elec - limit_cost;
+        if (rp[2] < tp.termination_height) total = tp.death_cost;
+        rew[i] = total;
+        // is_done + NaN guard; progress_buf += 1 (rl_task.py:242)
+        const int64_t progress = progress_buf[i] + 1;
+        reset_buf[i] = nan_guard(st, i, loco_done(tp, rp[2], reset_buf[i], progress));
+        progress_buf[i] = progress;
+    }
 }
 
 }  // namespace mi

@@ -1,9 +1,10 @@
 #!/usr/bin/env python3
 """Per-phase cycle breakdown of the wavefront-per-env substep (diagnostic build only).
 
-Loads libmi_sim_stamps.so (built with -DMI_STAMPS: s_memtime at each phase boundary of
-workgroup 7's last substep), runs a few fused env steps and prints the share of each phase.
-Stamps forbid overlaps the real kernel has: read the SHARES, never the absolute time."""
+Loads libmi_sim_stamps.so (built with -DMI_STAMPS: every workgroup adds the s_memtime delta of
+each phase to a device counter), runs fused env steps and prints the mean cycles per env-substep
+of each phase over ALL envs. Timers add a barrier-like fence at every phase boundary, so read
+the SHARES, not the absolute time."""
 import ctypes as C
 import json
 import os
@@ -13,8 +14,10 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
 os.environ["MI_SIM_LIB"] = os.path.join(ROOT, "omniisaacgymenvs_amd", "libmi_sim_stamps.so")
 
-PHASES = ["load", "P1 fk/levels", "P2 composite", "P3 crba", "P4 ltdl", "P5 L^-1", "P6 Minv",
-          "P7 u*", "P8 contacts", "P9 rows J/W", "P10 pgs", "P11 sensors+integrate"]
+PHASES = {0: "load", 1: "P1 fk+link dynamics", 2: "P2 composite", 3: "P3 crba", 4: "P4 ltdl+publish",
+          5: "P5 1/D (runtime path)", 6: "P8 contacts", 7: "P9 J build", 8: "P9 solves",
+          9: "P9 u* + limit rows", 10: "P9 row filing", 11: "P10 pgs", 12: "P11 sensors+integrate",
+          13: "task pre-step (per env-step)", 14: "task post-step (per env-step)"}
 
 
 def main():
@@ -30,24 +33,24 @@ def main():
     lib.mi_debug_stamps.argtypes = [C.POINTER(C.c_ulonglong), C.c_int]
     g = torch.Generator(device="cuda:0").manual_seed(0)
     env.reset()
-    out = {}
-    for step in range(40):
-        env.step(torch.rand((n, env.num_actions), device="cuda:0", generator=g) * 2 - 1)
-        if step >= 20 and step % 5 == 0:
+    buf = (C.c_ulonglong * 32)()
+    for step in range(60):
+        if step == 20:
             torch.cuda.synchronize()
-            buf = (C.c_ulonglong * 32)()
-            assert lib.mi_debug_stamps(buf, 32) == 0
-            st = list(buf)[:13]
-            d = [st[k + 1] - st[k] for k in range(12)]
-            tot = st[12] - st[0]
-            out[step] = {"total_cycles": tot, **{PHASES[k]: d[k] for k in range(12)}}
+            assert lib.mi_debug_stamps(buf, 32) == 0   # read-and-reset: drop the warm-up
+        env.step(torch.rand((n, env.num_actions), device="cuda:0", generator=g) * 2 - 1)
+    torch.cuda.synchronize()
+    assert lib.mi_debug_stamps(buf, 32) == 0
     env.close()
-    print(json.dumps(out))
-    last = out[max(out)]
-    tot = last["total_cycles"]
-    for k in PHASES:
-        print(f"{k:24s} {last[k]:9d}  {100.0 * last[k] / tot:5.1f}%")
-    print(f"{'total (1 substep)':24s} {tot:9d}")
+    cnt = max(1, buf[31])
+    # per env-substep; the task phases (once per env-step) are amortised over its substeps
+    per = {PHASES[k]: buf[k] / cnt for k in PHASES}
+    tot = sum(per.values())
+    print(json.dumps({"task": task, "envs": n, "substeps_measured": cnt,
+                      "cycles_per_env_substep": {k: round(v, 1) for k, v in per.items()}}))
+    for k, v in per.items():
+        print(f"{k:26s} {v:9.0f}  {100.0 * v / tot:5.1f}%")
+    print(f"{'total (1 env-substep)':26s} {tot:9.0f}")
 
 
 if __name__ == "__main__":
