@@ -649,7 +649,9 @@ int mi_sim_create(const mi_model_desc* md, const mi_sim_params* prm, int32_t N, 
         // On the compiled-topology path it is dead once P4 has moved M into registers, and
         // P8/P9 reuse it for the contact and row data and the first W rows.
         const int span0 = so;
-        t.s_F = take(6 * L); t.s_Ic = take(10 * L); t.s_M = take(m.nv * m.nv);
+        t.s_F = take(16 * L);   // per-link records: inertia (10) + Newton-Euler force (6)
+        t.s_Ic = take(4);       // (kept for the layout order; records live at s_F)
+        t.s_M = take(m.nv * m.nv);
         t.s_X = take(16 * L);
         const int span1 = so;
         t.s_D = take(ct ? 4 : WNV); t.s_r = take(WNV); t.s_us = take(WNV);

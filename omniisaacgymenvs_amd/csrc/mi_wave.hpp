@@ -228,7 +228,9 @@ MI_D void ct_ltdl(int lane, float (&Mc)[T::nvc]) {
         constexpr int k = K;
         __builtin_amdgcn_sched_barrier(0);
         const int ln = lane_here(lane);
-        const float inv = 1.0f / readlane(Mc[k], k);
+        // hardware reciprocal (1 ulp) instead of the ~10-instruction IEEE division on the
+        // factorisation's dependent chain
+        const float inv = __builtin_amdgcn_rcpf(readlane(Mc[k], k));
         sfor<T::dof.anc_start[k], T::dof.anc_start[k + 1]>([&](auto A) {
             constexpr int ii = T::dof.anc[A];
             const float s = readlane(Mc[k], ii) * inv;
@@ -243,7 +245,7 @@ template <class T>
 MI_D float ct_dinv(int lane, const float (&Mc)[T::nvc]) {
     float dg = 1.0f;
     sfor<0, T::nv>([&](auto I) { dg = lane_here(lane) == I ? Mc[I] : dg; });
-    return 1.0f / dg;
+    return __builtin_amdgcn_rcpf(dg);
 }
 
 template <class T>
@@ -479,10 +481,12 @@ MI_D void wave_link_forward(const MC& mc, int nr, const WaveTabs& t, float* sm, 
 #pragma unroll
         for (int c = 0; c < 6; ++c) F[c] = IA[c] + tt[c];
     }
-#pragma unroll
-    for (int c = 0; c < 10; ++c) sm[t.s_Ic + 10 * l + c] = I[c];
-#pragma unroll
-    for (int c = 0; c < 6; ++c) sm[t.s_F + 6 * l + c] = F[c];
+    // one 16-float record per link (inertia 10, force 6): 4 aligned 16-B LDS accesses
+    float4* rec = reinterpret_cast<float4*>(sm + t.s_F) + 4 * l;
+    rec[0] = make_float4(I[0], I[1], I[2], I[3]);
+    rec[1] = make_float4(I[4], I[5], I[6], I[7]);
+    rec[2] = make_float4(I[8], I[9], F[0], F[1]);
+    rec[3] = make_float4(F[2], F[3], F[4], F[5]);
 }
 
 // One articulated substep of env i, executed by the whole 64-lane workgroup.
@@ -530,23 +534,21 @@ MI_D void wave_artic_substep(const DevModel& m, const WaveTabs& t, const DevStat
     // ---- P2: composite inertia / force = own + sum over the subtree (fixed descendant order,
     // every link at once; results into the aux region: Ic at 16 l, F at 16 l + 10)
     float* aux = sm + t.s_X;
-    for (int l = lane; l < L; l += 64) {
-        float I[10], F[6];
-#pragma unroll
-        for (int q = 0; q < 10; ++q) I[q] = sm[t.s_Ic + 10 * l + q];
-#pragma unroll
-        for (int q = 0; q < 6; ++q) F[q] = sm[t.s_F + 6 * l + q];
-        for (int di = mc.desc_start(l); di < mc.desc_start(l + 1); ++di) {
-            const int d = mc.desc(di);
-#pragma unroll
-            for (int q = 0; q < 10; ++q) I[q] += sm[t.s_Ic + 10 * d + q];
-#pragma unroll
-            for (int q = 0; q < 6; ++q) F[q] += sm[t.s_F + 6 * d + q];
+    {
+        const float4* recs = reinterpret_cast<const float4*>(sm + t.s_F);
+        for (int l = lane; l < L; l += 64) {
+            float4 a0 = recs[4 * l], a1 = recs[4 * l + 1], a2 = recs[4 * l + 2], a3 = recs[4 * l + 3];
+            for (int di = mc.desc_start(l); di < mc.desc_start(l + 1); ++di) {
+                const int d = mc.desc(di);
+                const float4 b0 = recs[4 * d], b1 = recs[4 * d + 1], b2 = recs[4 * d + 2], b3 = recs[4 * d + 3];
+                a0.x += b0.x; a0.y += b0.y; a0.z += b0.z; a0.w += b0.w;
+                a1.x += b1.x; a1.y += b1.y; a1.z += b1.z; a1.w += b1.w;
+                a2.x += b2.x; a2.y += b2.y; a2.z += b2.z; a2.w += b2.w;
+                a3.x += b3.x; a3.y += b3.y; a3.z += b3.z; a3.w += b3.w;
+            }
+            float4* o = reinterpret_cast<float4*>(aux) + 4 * l;   // Ic at 16 l, F at 16 l + 10
+            o[0] = a0; o[1] = a1; o[2] = a2; o[3] = a3;
         }
-#pragma unroll
-        for (int q = 0; q < 10; ++q) aux[16 * l + q] = I[q];
-#pragma unroll
-        for (int q = 0; q < 6; ++q) aux[16 * l + 10 + q] = F[q];
     }
     __syncthreads();
     STAMP(2);   // P2
@@ -555,9 +557,15 @@ MI_D void wave_artic_substep(const DevModel& m, const WaveTabs& t, const DevStat
         const int k = lane, l = k < nr ? 0 : k - nr + 1;
         float s[6], I[10], f[6], F[6];
 #pragma unroll
-        for (int c = 0; c < 6; ++c) { s[c] = Ss[6 * k + c]; F[c] = aux[16 * l + 10 + c]; }
-#pragma unroll
-        for (int c = 0; c < 10; ++c) I[c] = aux[16 * l + c];
+        for (int c = 0; c < 6; ++c) s[c] = Ss[6 * k + c];
+        {
+            const float4* rec = reinterpret_cast<const float4*>(aux) + 4 * l;
+            const float4 a0 = rec[0], a1 = rec[1], a2 = rec[2], a3 = rec[3];
+            I[0] = a0.x; I[1] = a0.y; I[2] = a0.z; I[3] = a0.w;
+            I[4] = a1.x; I[5] = a1.y; I[6] = a1.z; I[7] = a1.w;
+            I[8] = a2.x; I[9] = a2.y; F[0] = a2.z; F[1] = a2.w;
+            F[2] = a3.x; F[3] = a3.y; F[4] = a3.z; F[5] = a3.w;
+        }
         inertia_mul(I, s, f);
         float diag = dot6(s, f);
         float r = -dot6(s, F);
