@@ -671,11 +671,16 @@ int mi_sim_create(const mi_model_desc* md, const mi_sim_params* prm, int32_t N, 
             for (int k = 0; k < m.nv; ++k) lr += (anc_start[k + 1] - anc_start[k] + 3) & ~3;
             t.s_L = take(ct ? lr + m.nv : 4);
         }
+        // CT path: J rows of up to 64 constraint rows for the PGS (LDS is not the occupancy
+        // limit here: registers cap the wave path at 2 waves/SIMD = 8 envs/CU = 20 KB each)
+        t.j_rows_lds = ct ? std::min(64, m.max_rows) : 0;
+        t.s_J = take(ct ? t.j_rows_lds * m.nv : 4);
         t.s_total = so;
         {   // the sequential regions strictly increase; the row data sits inside the dead
             // span (overlay) or between s_rp and s_xs
             const int offs[] = {t.s_mc, t.s_R, t.s_o, t.s_S, t.s_F, t.s_Ic, t.s_M, t.s_X,
-                                t.s_D, t.s_r, t.s_us, t.s_q, t.s_rp, t.s_xs, t.s_L, t.s_total};
+                                t.s_D, t.s_r, t.s_us, t.s_q, t.s_rp, t.s_xs, t.s_L, t.s_J,
+                                t.s_total};
             for (size_t c = 1; c < sizeof(offs) / sizeof(offs[0]); ++c)
                 if (offs[c] <= offs[c - 1]) return cleanup(fail(MI_E_STATE, "wave LDS layout: region %zu overlaps", c));
             const bool rows_ok = overlay ? (t.s_cp == span0 && ro <= span1)

@@ -92,6 +92,8 @@ struct WaveTabs {
     // W rows [0, w_rows_lds) are handed from P9 to P10 through LDS at s_W (stride nv, in the
     // span that is dead by then); rows beyond go through the global slab
     int s_W, w_rows_lds;
+    // J rows [0, j_rows_lds) kept in LDS at s_J (stride nv) for the PGS sweeps
+    int s_J, j_rows_lds;
     // per-model constant block (see McLayout): global copy, staged into LDS at s_mc once per
     // launch by every workgroup
     const float* g_mc;
@@ -749,6 +751,12 @@ MI_D void wave_artic_substep(const DevModel& m, const WaveTabs& t, const DevStat
         }
         if (slot >= 0) {
             sm[t.s_ad + slot] = a > 1e-12f ? a : 1e-12f;
+            if (kd >= 0 && slot < t.j_rows_lds) {    // limit row: J = sg e_kd
+                float* jl = sm + t.s_J + slot * nv;
+#pragma unroll
+                for (int c = 0; c < WNV; ++c)
+                    if (c < nv) jl[c] = c == kd ? sc : 0.0f;
+            }
             if (nrows <= t.w_rows_lds) {   // uniform: every row of this substep fits in LDS
                 float* wl = sm + t.s_W + slot * nv;
 #pragma unroll
@@ -789,6 +797,10 @@ MI_D void wave_artic_substep(const DevModel& m, const WaveTabs& t, const DevStat
                     constexpr int c = C;
                     x[c] = bv == 0 ? rhs[c] : (kd == c ? 1.0f : 0.0f);
                 });
+            }
+            if (on && r >= 0 && r < t.j_rows_lds) {   // keep J_r for the PGS sweeps
+                float* jl = sm + t.s_J + r * TP::nv;
+                sfor<0, TP::nv>([&](auto C) { jl[C] = x[C]; });
             }
             STAMP(7);   // P9 J build
             float a;                              // J M~^-1 J^T from the half solve
@@ -913,8 +925,11 @@ MI_D void wave_artic_substep(const DevModel& m, const WaveTabs& t, const DevStat
         // dependence on u) is built inside the current row's schedule region so it overlaps the
         // reduction chain. The friction rows of a contact follow its normal row in the same
         // sweep, so the normal's current lambda is carried in a wave-uniform value.
-        auto sweeps = [&](auto ONE_) {
+        const float* sJl = sm + t.s_J + (kl < nv ? kl : 0);
+        const float kin = kl < nv ? 1.0f : 0.0f;
+        auto sweeps = [&](auto ONE_, auto JL_) {
             constexpr bool ONE = decltype(ONE_)::value;
+            constexpr bool JL = decltype(JL_)::value;   // J rows from LDS (one bank only)
             for (int it = 0; it < p.iters; ++it) {
                 // opaque per sweep: stops the compiler hoisting the loop-invariant readlanes of
                 // every row out of the iteration loop (they would pin hundreds of SGPRs)
@@ -932,6 +947,10 @@ MI_D void wave_artic_substep(const DevModel& m, const WaveTabs& t, const DevStat
                     const float bb = h ? b1 : b0, ii = h ? ia1 : ia0, kk = h ? k1 : k0;
                     const unsigned mm = h ? mb : ma;
                     auto jrow = [&](int rr, int& kind) -> float {
+                        if constexpr (JL) {
+                            kind = (int)readlane(kk, rr);
+                            return sJl[rr * nv] * kin;
+                        }
                         float fr[6];
 #pragma unroll
                         for (int q = 0; q < 6; ++q) fr[q] = readlane(h ? fb[q] : fa[q], rr);
@@ -977,8 +996,9 @@ MI_D void wave_artic_substep(const DevModel& m, const WaveTabs& t, const DevStat
                 }
             }
         };
-        if (one_bank) sweeps(std::true_type{});
-        else sweeps(std::false_type{});
+        if (one_bank && nrows <= t.j_rows_lds) sweeps(std::true_type{}, std::true_type{});
+        else if (one_bank) sweeps(std::true_type{}, std::false_type{});
+        else sweeps(std::false_type{}, std::false_type{});
         if (lane < nv) us[lane] = u;
         if (lane < nrows) sm[t.s_ad + lane] = lam0;          // reuse: lambda of row lane
         if (lane + 64 < nrows) sm[t.s_ad + lane + 64] = lam1;
