@@ -203,7 +203,9 @@ int mi_env_step(mi_sim* sim, const float* actions /*[N,A]*/, int32_t substeps,
                 float* obs_out /*[N,O] clamped*/, float* obs_task /*[N,O]|NULL*/,
                 float* rew /*[N]*/, int64_t* reset_buf, int64_t* progress_buf,
                 float* potentials, float* prev_potentials, float* actions_out /*[N,A]|NULL*/,
-                void* stream);
+                float* rew_out /*[N]|NULL*/, int64_t* reset_out /*[N]|NULL*/, void* stream);
+/* rew_out / reset_out: the fresh copies VecEnvRLGames._process_data returns
+ * (vec_env_rlgames.py:41-46), written by the same launch instead of two clone kernels. */
 
 /* --- utilities --------------------------------------------------------------------- */
 /* U(lo,hi) Philox4x32-10 actions for the random-policy driver (scripts/random_policy.py:57),

@@ -194,7 +194,7 @@ __global__ void k_is_done(DevState st, DevTask tp, const float* obs, int64_t* re
 __global__ void k_env_step(DevModel m, DevState st, SimP p, DevTask tp, const float* actions,
                            int substeps, float* obs_out, float* obs_task, float* rew,
                            int64_t* reset_buf, int64_t* progress_buf, float* pot, float* prev,
-                           float* actions_out) {
+                           float* actions_out, float* rew_out, int64_t* reset_out) {
     const int i = blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= st.N) return;
     // 1. VecEnvRLGames.step:57 action clamp + pre_physics_step (reset_idx, efforts)
@@ -216,6 +216,8 @@ __global__ void k_env_step(DevModel m, DevState st, SimP p, DevTask tp, const fl
     } else if (co < INFINITY) {
         for (int k = 0; k < O; ++k) OUT[k] = clampf(OUT[k], -co, co);
     }
+    if (rew_out) rew_out[i] = rew[i];
+    if (reset_out) reset_out[i] = reset_buf[i];
 }
 
 // ---- wavefront-per-env articulation path (one 64-lane workgroup = one env) -------------
@@ -302,7 +304,8 @@ __global__ __launch_bounds__(64) void k_env_step_wave(const KParams* __restrict_
                                                       const float* actions, int substeps,
                                                       float* obs_out, float* obs_task, float* rew,
                                                       int64_t* reset_buf, int64_t* progress_buf,
-                                                      float* pot, float* prev, float* actions_out) {
+                                                      float* pot, float* prev, float* actions_out,
+                                                      float* rew_out, int64_t* reset_out) {
     extern __shared__ __attribute__((aligned(16))) float smem[];
     const DevModel& m = kp->m;
     const WaveTabs& t = kp->t;
@@ -326,7 +329,7 @@ __global__ __launch_bounds__(64) void k_env_step_wave(const KParams* __restrict_
     // 3. post_physics_step + obs clamp, wave-cooperative from the LDS-resident state
     STAMP_RESET();
     wave_loco_post(m, t, st, tp, i, smem, actions, obs_out, obs_task, rew, reset_buf, progress_buf,
-                   pot, prev);
+                   pot, prev, rew_out, reset_out);
     STAMP(14);
 }
 
@@ -964,7 +967,8 @@ int mi_task_is_done(mi_sim* s, const float* obs, int64_t* reset_buf, const int64
 
 int mi_env_step(mi_sim* s, const float* actions, int32_t substeps, float* obs_out, float* obs_task,
                 float* rew, int64_t* reset_buf, int64_t* progress_buf, float* potentials,
-                float* prev_potentials, float* actions_out, void* stream) {
+                float* prev_potentials, float* actions_out, float* rew_out, int64_t* reset_out,
+                void* stream) {
     NEED(s); NEED_TASK(s); NEED(actions); NEED(obs_out); NEED(rew); NEED(reset_buf); NEED(progress_buf);
     if (s->tp.kind != MI_TASK_CARTPOLE) { NEED(potentials); NEED(prev_potentials); }
     if (substeps < 0 || substeps > 64) return fail(MI_E_ARG, "substeps %d out of range", substeps);
@@ -974,12 +978,12 @@ int mi_env_step(mi_sim* s, const float* actions, int32_t substeps, float* obs_ou
             hipLaunchKernelGGL(k_env_step_wave<decltype(T)>, dim3(s->N), dim3(64), s->lds_bytes,
                                STREAM(stream), (const KParams*)s->kp_dev, actions, substeps,
                                obs_out, obs_task, rew, reset_buf, progress_buf, potentials,
-                               prev_potentials, actions_out);
+                               prev_potentials, actions_out, rew_out, reset_out);
         });
     else
         hipLaunchKernelGGL(k_env_step, grid_for(s, s->N), dim3(s->block), 0, STREAM(stream), s->dm,
                            s->ds, s->sp, s->tp, actions, substeps, obs_out, obs_task, rew, reset_buf,
-                           progress_buf, potentials, prev_potentials, actions_out);
+                           progress_buf, potentials, prev_potentials, actions_out, rew_out, reset_out);
     LAUNCH_CHECK();
     return MI_OK;
 }

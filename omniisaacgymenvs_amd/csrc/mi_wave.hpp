@@ -1164,7 +1164,8 @@ MI_D void wave_task_pre(const DevModel& m, const WaveTabs& t, const DevState& st
 MI_D void wave_loco_post(const DevModel& m, const WaveTabs& t, const DevState& st,
                          const DevTask& tp, int i, float* sm, const float* actions,
                          float* obs_out, float* obs_task, float* rew, int64_t* reset_buf,
-                         int64_t* progress_buf, float* potentials, float* prev_potentials) {
+                         int64_t* progress_buf, float* potentials, float* prev_potentials,
+                         float* rew_out, int64_t* reset_out) {
 #pragma clang fp contract(off)
     const int lane = threadIdx.x, D = m.D, S = m.S, O = tp.O;
     const float co = tp.clip_obs;
@@ -1260,8 +1261,11 @@ MI_D void wave_loco_post(const DevModel& m, const WaveTabs& t, const DevState& s
         rew[i] = total;
         // is_done + NaN guard; progress_buf += 1 (rl_task.py:242)
         const int64_t progress = progress_buf[i] + 1;
-        reset_buf[i] = nan_guard(st, i, loco_done(tp, rp[2], reset_buf[i], progress));
+        const int64_t done = nan_guard(st, i, loco_done(tp, rp[2], reset_buf[i], progress));
+        reset_buf[i] = done;
         progress_buf[i] = progress;
+        if (rew_out) rew_out[i] = total;          // _process_data's returned copies
+        if (reset_out) reset_out[i] = done;
     }
 }
 

@@ -93,15 +93,17 @@ class VecEnvRLGames:
             if ev is not None:
                 k = self._ev_i % len(ev[0])
                 ev[0][k].record()
-                obs = t.fused_step(actions)
+                obs, rew, resets = t.fused_step(actions)
                 ev[1][k].record()
                 self._ev_i += 1
             else:
-                obs = t.fused_step(actions)
+                obs, rew, resets = t.fused_step(actions)
             self.sim_frame_count += t.control_frequency_inv
-            self._obs = obs if str(t.rl_device) == str(obs.device) else obs.to(t.rl_device)
-            self._rew = t.rew_buf.to(t.rl_device).clone()
-            self._resets = t.reset_buf.to(t.rl_device).clone()
+            # fresh tensors written by the launch itself (= _process_data's clones)
+            rl = str(t.rl_device)
+            self._obs = obs if rl == str(obs.device) else obs.to(t.rl_device)
+            self._rew = rew if rl == str(rew.device) else rew.to(t.rl_device)
+            self._resets = resets if rl == str(resets.device) else resets.to(t.rl_device)
             self._extras = t.extras.copy()
             self._states = torch.clamp(t.get_states(), -t.clip_obs, t.clip_obs).to(t.rl_device).clone()
             return {"obs": self._obs, "states": self._states}, self._rew, self._resets, self._extras

@@ -100,7 +100,7 @@ _SIGS = {
     "mi_task_observations": (C.c_int, [C.c_void_p] + [C.c_void_p] * 5),
     "mi_task_metrics": (C.c_int, [C.c_void_p] + [C.c_void_p] * 6),
     "mi_task_is_done": (C.c_int, [C.c_void_p] + [C.c_void_p] * 4),
-    "mi_env_step": (C.c_int, [C.c_void_p, C.c_void_p, C.c_int32] + [C.c_void_p] * 9),
+    "mi_env_step": (C.c_int, [C.c_void_p, C.c_void_p, C.c_int32] + [C.c_void_p] * 11),
     "mi_fill_uniform": (C.c_int, [C.c_void_p, C.c_void_p, C.c_int32, C.c_uint64, C.c_uint64,
                                   C.c_float, C.c_float, C.c_void_p]),
     "mi_get_reset_count": (C.c_int, [C.c_void_p, C.c_void_p]),

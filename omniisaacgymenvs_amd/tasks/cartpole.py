@@ -95,11 +95,14 @@ class CartpoleTask(RLTask):
     def fused_step(self, actions: torch.Tensor):
         a = actions.to(self._device, dtype=torch.float32).contiguous()
         obs_out = torch.empty_like(self.obs_buf)
+        rew_out = torch.empty_like(self.rew_buf)
+        reset_out = torch.empty_like(self.reset_buf)
         N.check(N.lib().mi_env_step(self._h(), a.data_ptr(), int(self.control_frequency_inv),
                                     obs_out.data_ptr(), self.obs_buf.data_ptr(), self.rew_buf.data_ptr(),
                                     self.reset_buf.data_ptr(), self.progress_buf.data_ptr(), None, None,
-                                    None, self._stream()), "mi_env_step")
-        return obs_out
+                                    None, rew_out.data_ptr(), reset_out.data_ptr(), self._stream()),
+                "mi_env_step")
+        return obs_out, rew_out, reset_out
 
 
 CartpoleTask._native_task_class = CartpoleTask

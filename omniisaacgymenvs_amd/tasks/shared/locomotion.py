@@ -160,13 +160,17 @@ class LocomotionTask(RLTask):
 
     # ------------------------------------------------------------------ fused path
     def fused_step(self, actions: torch.Tensor):
-        """VecEnvRLGames.step in one launch; returns a fresh (clamped) obs tensor."""
+        """VecEnvRLGames.step in one launch; returns fresh (obs clamped, rew, resets) tensors,
+        the copies _process_data hands back (vec_env_rlgames.py:41-46)."""
         a = actions.to(self._device, dtype=torch.float32).contiguous()
         obs_out = torch.empty_like(self.obs_buf)
+        rew_out = torch.empty_like(self.rew_buf)
+        reset_out = torch.empty_like(self.reset_buf)
         N.check(N.lib().mi_env_step(self._h(), a.data_ptr(), int(self.control_frequency_inv),
                                     obs_out.data_ptr(), self.obs_buf.data_ptr(), self.rew_buf.data_ptr(),
                                     self.reset_buf.data_ptr(), self.progress_buf.data_ptr(),
                                     self.potentials.data_ptr(), self.prev_potentials.data_ptr(),
-                                    self.actions.data_ptr(), self._stream()), "mi_env_step")
-        return obs_out
+                                    self.actions.data_ptr(), rew_out.data_ptr(), reset_out.data_ptr(),
+                                    self._stream()), "mi_env_step")
+        return obs_out, rew_out, reset_out
 

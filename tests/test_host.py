@@ -129,7 +129,7 @@ def test_abi_rejects_bad_input_without_touching_a_gpu():
     assert lib.mi_sim_create(bad.ref(), C.byref(p), 4, 0, 0, org.ctypes.data, 0, C.byref(out)) == -4
     if not torch.cuda.is_available():
         assert lib.mi_sim_create(d.ref(), C.byref(p), 4, 0, 0, org.ctypes.data, 0, C.byref(out)) == -6
-    for fn, args in [("mi_sim_step", (None, 1, None)), ("mi_env_step", (None, None, 2) + (None,) * 9),
+    for fn, args in [("mi_sim_step", (None, 1, None)), ("mi_env_step", (None, None, 2) + (None,) * 11),
                      ("mi_task_pre_step", (None,) * 8), ("mi_get_dof_state", (None,) * 4)]:
         assert getattr(lib, fn)(*args) == -1
 
