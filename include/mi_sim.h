@@ -139,6 +139,12 @@ typedef struct mi_task_params {
     float reset_dist, max_push_effort;
 } mi_task_params;
 
+/* Constraint-row budget per env-substep (every path, and the oracle): ground contact and joint-
+ * limit rows always fit (3 * candidate points + D <= MI_MAX_ROWS is required); self-contacts
+ * take what is left, (MI_MAX_ROWS - 3 * ground_contacts - limited_joints) / 3 of them, in pair
+ * order. */
+#define MI_MAX_ROWS 128
+
 typedef struct mi_sim mi_sim;
 
 /* --- lifecycle: replaces World/SimulationContext + GridCloner + ArticulationView init

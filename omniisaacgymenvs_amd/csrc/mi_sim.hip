@@ -433,6 +433,10 @@ int mi_sim_create(const mi_model_desc* md, const mi_sim_params* prm, int32_t N, 
         if (md->geom_link[g] < 0 || md->geom_link[g] >= L) return fail(MI_E_MODEL, "geom_link[%d] out of range", g);
     for (int s = 0; s < md->num_sensors; ++s)
         if (md->sensor_link[s] < 0 || md->sensor_link[s] >= L) return fail(MI_E_MODEL, "sensor_link[%d] out of range", s);
+    if (md->num_pairs && !md->pairs) return fail(MI_E_NULL, "pairs must not be null");
+    for (int q = 0; q < 2 * md->num_pairs; ++q)
+        if (md->pairs[q] < 0 || md->pairs[q] >= md->num_geoms)
+            return fail(MI_E_MODEL, "pairs[%d]=%d is not a geom index", q, md->pairs[q]);
     int ndev = 0;
     if (hipGetDeviceCount(&ndev) != hipSuccess || ndev == 0) return fail(MI_E_NODEV, "no HIP device visible");
     if (device_id < 0 || device_id >= ndev) return fail(MI_E_NODEV, "device_id %d out of range (%d devices)", device_id, ndev);
@@ -469,7 +473,14 @@ int mi_sim_create(const mi_model_desc* md, const mi_sim_params* prm, int32_t N, 
         if (md->geom_type[g] == MI_GEOM_CAPSULE) { pt_geom.push_back(g); pt_end.push_back(1); }
     }
     m.npts = (int)pt_geom.size();
+    // self-collision rows share the MI_MAX_ROWS budget (mi_sim.h); ground + limit rows must fit
+    const bool self_on = prm->enable_self_collisions && md->num_pairs > 0 &&
+                         md->dyn_kind == MI_DYN_ARTICULATION;
     m.max_rows = 3 * m.npts + m.D;
+    if (m.max_rows > MI_MAX_ROWS)
+        return cleanup(fail(MI_E_MODEL, "%d contact points + %d joints exceed the %d-row budget",
+                            m.npts, m.D, MI_MAX_ROWS));
+    if (self_on) m.max_rows = std::min(MI_MAX_ROWS, 3 * (m.npts + md->num_pairs) + m.D);
     int rc = 0;
 #define UP(field, src, cnt) if ((rc = upload(s, src, (size_t)(cnt), &m.field))) return cleanup(rc)
     UP(parent, md->parent, L); UP(jtype, md->jtype, L); UP(axis, md->axis, 3 * L);
@@ -517,6 +528,9 @@ int mi_sim_create(const mi_model_desc* md, const mi_sim_params* prm, int32_t N, 
         // (the post-step keeps sensor wrenches + reward terms in the row-bias region)
         s->wave = m.dyn == MI_DYN_ARTICULATION && !want_thread && m.nv <= WNV && m.npts <= 64 &&
                   m.max_rows <= 128 && L <= 64 && m.max_rows >= 6 * m.S + 3 * m.D;
+        if (self_on && !s->wave)
+            return cleanup(fail(MI_E_MODEL, "self-collision needs the wavefront-per-env path "
+                                            "(one-lane-per-env path %s)", want_thread ? "forced by MI_SIM_PATH" : "selected"));
     }
     if (s->wave) {
         const char* tsel = getenv("MI_SIM_TOPO");
@@ -640,6 +654,20 @@ int mi_sim_create(const mi_model_desc* md, const mi_sim_params* prm, int32_t N, 
             t.mc_len = (int)mcb.size();
             t.npts = np; t.nsens = ns;
             UPW(g_mc, mcb);
+            // self-collision geometry: per geom (link, p0, p1, radius) and the geom pairs
+            std::vector<float> geo((size_t)8 * std::max(1, md->num_geoms), 0.0f);
+            for (int g = 0; g < md->num_geoms; ++g) {
+                geo[8 * g] = (float)md->geom_link[g];
+                for (int q = 0; q < 3; ++q) {
+                    geo[8 * g + 1 + q] = md->geom_p0[3 * g + q];
+                    geo[8 * g + 4 + q] = md->geom_p1[3 * g + q];
+                }
+                geo[8 * g + 7] = md->geom_radius[g];
+            }
+            std::vector<int> prs(md->pairs ? md->pairs : nullptr,
+                                 md->pairs ? md->pairs + 2 * md->num_pairs : nullptr);
+            if (prs.empty()) prs.assign(2, 0);
+            UPW(g_geo, geo); UPW(g_pairs, prs);
         }
 #undef UPW
         auto al4 = [](int x) { return (x + 3) & ~3; };
@@ -660,11 +688,17 @@ int mi_sim_create(const mi_model_desc* md, const mi_sim_params* prm, int32_t N, 
         t.s_D = take(ct ? 4 : WNV); t.s_r = take(WNV); t.s_us = take(WNV);
         t.s_q = take(WNV); t.s_rp = take(8);
         const int R = m.max_rows;
-        const int rows_len = al4(3 * m.npts) + al4(m.npts) + 4 * al4(R) + WNV;
+        // contacts: ground points + self pairs, at most MI_MAX_ROWS / 3 in total
+        t.self_on = self_on ? 1 : 0;
+        t.npairs = self_on ? md->num_pairs : 0;
+        t.ncmax = std::min(m.npts + t.npairs, MI_MAX_ROWS / 3);
+        const int C = t.ncmax;
+        const int rows_len = 8 * al4(C) + 4 * al4(R) + WNV;
         const bool overlay = ct && rows_len <= span1 - span0;
         int ro = overlay ? span0 : so;
         auto take_r = [&](int n) { const int at = ro; ro += al4(n); return at; };
-        t.s_cp = take_r(3 * m.npts); t.s_cl = take_r(m.npts); t.s_rl = take_r(R);
+        t.s_cp = take_r(3 * C); t.s_cl = take_r(C); t.s_cl2 = take_r(C); t.s_cn = take_r(3 * C);
+        t.s_rl = take_r(R);
         t.s_rb = take_r(R); t.s_rk = take_r(R); t.s_ad = take_r(R); t.s_lsg = take_r(WNV);
         if (!overlay) so = ro;
         // lane-private solve vectors of the runtime-table solves (CT solves run in registers)

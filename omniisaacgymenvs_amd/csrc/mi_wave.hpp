@@ -24,6 +24,7 @@
 #include "mi_artic.hpp"
 #include "mi_device.hpp"
 #include "mi_topo_gen.hpp"
+#include "../../include/mi_geom.h"
 
 namespace mi {
 
@@ -100,6 +101,12 @@ struct WaveTabs {
     int mc_len, mc_pts, mc_sens, mc_chs, mc_chl, mc_dss, mc_dsl, mc_lim;   // block offsets
     int npts, nsens;
     int nlimc;   // joints with a limit (lower < upper): limit-row candidates, joint ids at mc_lim
+    // self-collision (mi_geom.h): geom table [G][8] = link, p0 (3), p1 (3), radius and the
+    // geom pairs [P][2], global (lane-indexed, cache-resident); contact capacity ncmax
+    int self_on, npairs, ncmax;
+    const float* g_geo;
+    const int* g_pairs;
+    int s_cl2, s_cn;   // per contact: second link (-1: ground), normal (3)
 };
 
 // Per-model constants in the LDS block, structure-of-arrays so lane-indexed reads (lane = link,
@@ -135,10 +142,24 @@ struct MC {
 // Spatial force direction of contact row r = 3 ci + tt at contact point pc: normal (tt 0,
 // +z) or friction (tt 1: +x, tt 2: +y), f = (pc x dir, dir). Rebuilt where needed from the
 // contact point instead of stored per row (saves 6 floats x rows of LDS); same arithmetic.
+// Contact ci's directions (normal, t1, t2): ground +z / +x / +y, self-contact the stored
+// normal and mi_contact_basis (same as the oracle).
+MI_D void contact_dirs(const float* sm, const WaveTabs& t, int ci, float (&d)[9]) {
+    if (sm[t.s_cl2 + ci] < 0.0f) {
+#pragma unroll
+        for (int k = 0; k < 9; ++k) d[k] = (k == 2 || k == 3 || k == 7) ? 1.0f : 0.0f;
+    } else {
+        d[0] = sm[t.s_cn + 3 * ci]; d[1] = sm[t.s_cn + 3 * ci + 1]; d[2] = sm[t.s_cn + 3 * ci + 2];
+        mi_contact_basis(d, d + 3, d + 6);
+    }
+}
+
 MI_D void contact_row_f(const float* sm, const WaveTabs& t, int r, float (&f)[6]) {
     const int ci = r / 3, tt = r - 3 * ci;
     const float pc[3] = {sm[t.s_cp + 3 * ci], sm[t.s_cp + 3 * ci + 1], sm[t.s_cp + 3 * ci + 2]};
-    const float dir[3] = {tt == 1 ? 1.0f : 0.0f, tt == 2 ? 1.0f : 0.0f, tt == 0 ? 1.0f : 0.0f};
+    float d[9];
+    contact_dirs(sm, t, ci, d);
+    const float dir[3] = {d[3 * tt], d[3 * tt + 1], d[3 * tt + 2]};
     cross3(pc, dir, f);
     f[3] = dir[0]; f[4] = dir[1]; f[5] = dir[2];
 }
@@ -669,6 +690,7 @@ MI_D void wave_artic_substep(const DevModel& m, const WaveTabs& t, const DevStat
 #pragma unroll
             for (int q = 0; q < 3; ++q) sm[t.s_cp + 3 * ci + q] = pc[q];
             sm[t.s_cl + ci] = (float)l;
+            sm[t.s_cl2 + ci] = -1.0f;
 #pragma unroll
             for (int tt = 0; tt < 3; ++tt) {
                 const int r = 3 * ci + tt;
@@ -677,6 +699,58 @@ MI_D void wave_artic_substep(const DevModel& m, const WaveTabs& t, const DevStat
                 sm[t.s_rk + r] = (float)tt;
             }
         }
+    }
+    // self-contacts (Humanoid.yaml:80): lanes over geom pairs, compacted in pair order within
+    // the MI_MAX_ROWS budget, after the ground contacts (as the oracle)
+    if (t.self_on) {
+        int budget = (MI_MAX_ROWS - 3 * ncon - t.nlimc) / 3;
+        for (int pb = 0; pb < t.npairs && budget > 0; pb += 64) {
+            const int pi = pb + lane;
+            bool act = false;
+            float pc[3], n[3], bn = 0.0f;
+            int la = 0, lb = 0;
+            if (pi < t.npairs) {
+                const int ga = t.g_pairs[2 * pi], gb = t.g_pairs[2 * pi + 1];
+                const float* A = t.g_geo + 8 * ga;
+                const float* B = t.g_geo + 8 * gb;
+                la = (int)A[0]; lb = (int)B[0];
+                float Ra[9], Rb[9], a0[3], a1[3], b0[3], b1[3];
+#pragma unroll
+                for (int q = 0; q < 9; ++q) { Ra[q] = sm[t.s_R + 9 * la + q]; Rb[q] = sm[t.s_R + 9 * lb + q]; }
+                m3_vec(Ra, A + 1, a0); m3_vec(Ra, A + 4, a1);
+                m3_vec(Rb, B + 1, b0); m3_vec(Rb, B + 4, b1);
+#pragma unroll
+                for (int q = 0; q < 3; ++q) {
+                    a0[q] += sm[t.s_o + 3 * la + q]; a1[q] += sm[t.s_o + 3 * la + q];
+                    b0[q] += sm[t.s_o + 3 * lb + q]; b1[q] += sm[t.s_o + 3 * lb + q];
+                }
+                const float gap = mi_pair_contact(a0, a1, A[7], b0, b1, B[7], pc, n);
+                act = gap < p.contact_offset;
+                const float d = gap - p.rest_offset;
+                bn = d >= 0.0f ? -d / dt : -p.erp * d / dt;
+                if (bn > p.max_depen) bn = p.max_depen;
+            }
+            const unsigned long long mask = __ballot(act);
+            const int rank = __popcll(mask & ((1ull << lane) - 1ull));
+            if (act && rank < budget) {
+                const int ci = ncon + rank;
+#pragma unroll
+                for (int q = 0; q < 3; ++q) { sm[t.s_cp + 3 * ci + q] = pc[q]; sm[t.s_cn + 3 * ci + q] = n[q]; }
+                sm[t.s_cl + ci] = (float)la;
+                sm[t.s_cl2 + ci] = (float)lb;
+#pragma unroll
+                for (int tt = 0; tt < 3; ++tt) {
+                    const int r = 3 * ci + tt;
+                    sm[t.s_rl + r] = (float)la;
+                    sm[t.s_rb + r] = tt == 0 ? bn : 0.0f;
+                    sm[t.s_rk + r] = (float)tt;
+                }
+            }
+            const int took = min(__popcll(mask), budget);
+            ncon += took;
+            budget -= took;
+        }
+        ncon = __builtin_amdgcn_readfirstlane(ncon);
     }
     const int nc = 3 * ncon;
     __syncthreads();
@@ -777,20 +851,23 @@ MI_D void wave_artic_substep(const DevModel& m, const WaveTabs& t, const DevStat
             // solve vector built in place: J_r, e_kd or the rhs
             float x[TP::nvc];
             if (on && r >= 0) {
+                // J_r = J_a^T f - J_b^T f (b: the second body of a self-contact, else none)
                 const int l = (int)sm[t.s_rl + r];
-                const unsigned msk = mc.mask(l);
+                const float l2 = sm[t.s_cl2 + r / 3];
+                const unsigned msk = mc.mask(l), msk2 = l2 >= 0.0f ? mc.mask((int)l2) : 0u;
                 float f[6];
                 contact_row_f(sm, t, r, f);
                 sfor<0, TP::nv>([&](auto C) {
                     constexpr int c = C;
+                    const bool ia = (msk >> c) & 1u, ib = (msk2 >> c) & 1u;
                     float v = 0.0f;
-                    if ((msk >> c) & 1u) {
+                    if (ia || ib) {
                         float sv[6];
 #pragma unroll
                         for (int q = 0; q < 6; ++q) sv[q] = Ss[6 * c + q];
                         v = dot6(sv, f);
                     }
-                    x[c] = v;
+                    x[c] = (ia ? v : 0.0f) - (ib ? v : 0.0f);
                 });
             } else {
                 sfor<0, TP::nv>([&](auto C) {
@@ -817,19 +894,21 @@ MI_D void wave_artic_substep(const DevModel& m, const WaveTabs& t, const DevStat
             for (int c = 0; c < WNV; ++c) jr[c] = 0.0f;
             if (on && r >= 0) {
                 const int l = (int)sm[t.s_rl + r];
-                const unsigned long long msk = mc.mask(l);
+                const float l2 = sm[t.s_cl2 + r / 3];
+                const unsigned msk = mc.mask(l), msk2 = l2 >= 0.0f ? mc.mask((int)l2) : 0u;
                 float f[6];
                 contact_row_f(sm, t, r, f);
 #pragma unroll
                 for (int c = 0; c < WNV; ++c) {
+                    const bool ia = (msk >> c) & 1u, ib = (msk2 >> c) & 1u;
                     float v = 0.0f;
-                    if ((msk >> c) & 1ull) {
+                    if (ia || ib) {
                         float sv[6];
 #pragma unroll
                         for (int q = 0; q < 6; ++q) sv[q] = Ss[6 * c + q];
                         v = dot6(sv, f);
                     }
-                    jr[c] = v;
+                    jr[c] = (ia ? v : 0.0f) - (ib ? v : 0.0f);
                 }
             }
             STAMP(7);
@@ -899,9 +978,10 @@ MI_D void wave_artic_substep(const DevModel& m, const WaveTabs& t, const DevStat
         // row r's data in lane r % 64, bank r / 64: b, 1/A_rr, kind, DOF mask, f (6)
         float b0 = 0, b1 = 0, ia0 = 1, ia1 = 1, k0 = 0, k1 = 0, lam0 = 0.0f, lam1 = 0.0f;
         float fa[6] = {0, 0, 0, 0, 0, 0}, fb[6] = {0, 0, 0, 0, 0, 0};
-        unsigned ma = 0u, mb = 0u;
+        unsigned ma = 0u, mb = 0u, ma2 = 0u, mb2 = 0u;   // DOF masks of body a / body b
         {
-            auto load_row = [&](int r, float& b, float& ia, float& k, float (&f)[6], unsigned& msk) {
+            auto load_row = [&](int r, float& b, float& ia, float& k, float (&f)[6], unsigned& msk,
+                                unsigned& msk2) {
                 b = sm[t.s_rb + r];
                 ia = 1.0f / sm[t.s_ad + r];
                 k = sm[t.s_rk + r];
@@ -909,14 +989,16 @@ MI_D void wave_artic_substep(const DevModel& m, const WaveTabs& t, const DevStat
                 if (lk >= 0.0f) {
                     contact_row_f(sm, t, r, f);
                     msk = mc.mask((int)lk);
+                    const float l2 = sm[t.s_cl2 + r / 3];
+                    msk2 = l2 >= 0.0f ? mc.mask((int)l2) : 0u;
                 } else {
                     const int kdof = (int)(-lk - 1.0f);
                     f[0] = sm[t.s_lsg + kdof - nr];      // limit row: J = sg e_k
                     msk = 1u << kdof;
                 }
             };
-            if (lane < nrows) load_row(lane, b0, ia0, k0, fa, ma);
-            if (lane + 64 < nrows) load_row(lane + 64, b1, ia1, k1, fb, mb);
+            if (lane < nrows) load_row(lane, b0, ia0, k0, fa, ma, ma2);
+            if (lane + 64 < nrows) load_row(lane + 64, b1, ia1, k1, fb, mb, mb2);
         }
         const float mu = p.friction;
         float u = kl < nv ? us[kl] : 0.0f;
@@ -934,7 +1016,7 @@ MI_D void wave_artic_substep(const DevModel& m, const WaveTabs& t, const DevStat
                 // opaque per sweep: stops the compiler hoisting the loop-invariant readlanes of
                 // every row out of the iteration loop (they would pin hundreds of SGPRs)
                 asm volatile("" : "+v"(b0), "+v"(b1), "+v"(ia0), "+v"(ia1), "+v"(k0), "+v"(k1),
-                             "+v"(ma), "+v"(mb));
+                             "+v"(ma), "+v"(mb), "+v"(ma2), "+v"(mb2));
                 asm volatile("" : "+v"(fa[0]), "+v"(fa[1]), "+v"(fa[2]), "+v"(fa[3]), "+v"(fa[4]),
                              "+v"(fa[5]), "+v"(fb[0]), "+v"(fb[1]), "+v"(fb[2]), "+v"(fb[3]),
                              "+v"(fb[4]), "+v"(fb[5]));
@@ -945,7 +1027,7 @@ MI_D void wave_artic_substep(const DevModel& m, const WaveTabs& t, const DevStat
                 for (int h = 0; h < (ONE ? 1 : 2); ++h) {
                     if (64 * h >= nrow_it) continue;
                     const float bb = h ? b1 : b0, ii = h ? ia1 : ia0, kk = h ? k1 : k0;
-                    const unsigned mm = h ? mb : ma;
+                    const unsigned mm = h ? mb : ma, mm2 = h ? mb2 : ma2;
                     auto jrow = [&](int rr, int& kind) -> float {
                         if constexpr (JL) {
                             kind = (int)readlane(kk, rr);
@@ -955,9 +1037,10 @@ MI_D void wave_artic_substep(const DevModel& m, const WaveTabs& t, const DevStat
 #pragma unroll
                         for (int q = 0; q < 6; ++q) fr[q] = readlane(h ? fb[q] : fa[q], rr);
                         const unsigned msk = (unsigned)__builtin_amdgcn_readlane((int)mm, rr);
+                        const unsigned msk2 = (unsigned)__builtin_amdgcn_readlane((int)mm2, rr);
                         kind = (int)readlane(kk, rr);
                         const float jc = kind == 3 ? fr[0] : dot6(S6, fr);
-                        return ((msk >> kl) & 1u) ? jc : 0.0f;
+                        return (((msk >> kl) & 1u) ? jc : 0.0f) - (((msk2 >> kl) & 1u) ? jc : 0.0f);
                     };
                     int kind_c;
                     float jc_c = jrow(0, kind_c);
@@ -1018,9 +1101,17 @@ MI_D void wave_artic_substep(const DevModel& m, const WaveTabs& t, const DevStat
 #pragma unroll
         for (int q = 0; q < 3; ++q) xs[q] += sm[t.s_o + 3 * l + q];
         for (int c = 0; c < ncon; ++c) {
-            if ((int)sm[t.s_cl + c] != l) continue;
+#pragma clang fp contract(off)
+            // contact wrench on link l: +f on body a, -f on body b of a self-contact
+            const float sgn = (int)sm[t.s_cl + c] == l ? 1.0f : ((int)sm[t.s_cl2 + c] == l ? -1.0f : 0.0f);
+            if (sgn == 0.0f) continue;
             const float* lam = sm + t.s_ad;
-            const float fc[3] = {lam[3 * c + 1] / dt, lam[3 * c + 2] / dt, lam[3 * c] / dt};
+            const float fn = lam[3 * c] / dt, f1 = lam[3 * c + 1] / dt, f2 = lam[3 * c + 2] / dt;
+            float d[9];
+            contact_dirs(sm, t, c, d);
+            float fc[3];
+#pragma unroll
+            for (int q = 0; q < 3; ++q) fc[q] = sgn * (fn * d[q] + f1 * d[3 + q] + f2 * d[6 + q]);
             float rr[3], tc[3];
 #pragma unroll
             for (int q = 0; q < 3; ++q) rr[q] = sm[t.s_cp + 3 * c + q] - xs[q];

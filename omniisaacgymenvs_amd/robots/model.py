@@ -383,10 +383,65 @@ def _weld_all(b: _Body) -> None:
         _weld_all(ch)
 
 
+def segment_distance(a0, a1, b0, b1):
+    """Closest distance between segments [a0, a1] and [b0, b1] (points allowed), numpy."""
+    d1, d2, r = a1 - a0, b1 - b0, a0 - b0
+    a, e, f = d1 @ d1, d2 @ d2, d2 @ r
+    if a <= 1e-12 and e <= 1e-12:
+        return float(np.linalg.norm(r))
+    if a <= 1e-12:
+        s, t = 0.0, np.clip(f / e, 0.0, 1.0)
+    else:
+        c = d1 @ r
+        if e <= 1e-12:
+            s, t = np.clip(-c / a, 0.0, 1.0), 0.0
+        else:
+            b = d1 @ d2
+            den = a * e - b * b
+            s = np.clip((b * f - c * e) / den, 0.0, 1.0) if den > 1e-12 else 0.0
+            t = (b * s + f) / e
+            if t < 0.0:
+                s, t = np.clip(-c / a, 0.0, 1.0), 0.0
+            elif t > 1.0:
+                s, t = np.clip((b - c) / a, 0.0, 1.0), 1.0
+    return float(np.linalg.norm((a0 + d1 * s) - (b0 + d2 * t)))
+
+
+def _self_collision_pairs(order, min_gap: float) -> List[tuple]:
+    """Geom pairs that may self-collide, in compiled geom order: geoms of different bodies that
+    are not joint-connected (PhysX does not collide a link with its parent), minus pairs whose
+    surfaces are closer than ``min_gap`` in the default pose (initial-overlap filter)."""
+    Rw, pw = {}, {}
+    for b in order:
+        if b.parent is None:
+            Rw[b.name], pw[b.name] = np.eye(3), np.zeros(3)
+        else:
+            Rp, pp = Rw[b.parent.name], pw[b.parent.name]
+            Rw[b.name] = Rp @ quat_to_mat(b.quat)
+            pw[b.name] = pp + Rp @ b.pos
+    geoms = []   # (body, world p0, world p1, radius) in compiled geom order
+    for b in order:
+        for g in b.geoms:
+            geoms.append((b, pw[b.name] + Rw[b.name] @ g.p0, pw[b.name] + Rw[b.name] @ g.p1, g.radius))
+    pairs = []
+    for i in range(len(geoms)):
+        for j in range(i + 1, len(geoms)):
+            bi, bj = geoms[i][0], geoms[j][0]
+            if bi is bj or bi.parent is bj or bj.parent is bi:
+                continue
+            gap = segment_distance(geoms[i][1], geoms[i][2], geoms[j][1], geoms[j][2]) - \
+                geoms[i][3] - geoms[j][3]
+            if gap >= min_gap:
+                pairs.append((i, j))
+    return pairs
+
+
 def compile_mjcf(path: str, sensor_bodies: Optional[List[str]] = None,
-                 self_collision_pairs: Optional[List[tuple]] = None) -> CompiledModel:
+                 self_collision_pairs: Optional[List[tuple]] = None,
+                 self_collision: bool = False, self_collision_min_gap: float = 0.05) -> CompiledModel:
     """Compile an MJCF-subset file. ``sensor_bodies`` lists force-sensor bodies in output
-    order (the wrench reference is the body's first site, else its frame origin)."""
+    order (the wrench reference is the body's first site, else its frame origin).
+    ``self_collision``: generate the self-collision geom pairs (see _self_collision_pairs)."""
     p = _Parser(path)
     root = p.root
     _weld_all(root)
@@ -452,6 +507,8 @@ def compile_mjcf(path: str, sensor_bodies: Optional[List[str]] = None,
         site = next(iter(b.sites.values())) if b.sites else np.zeros(3)
         sl.append(last_link[name])
         sp.append(site - last_anchor[name])
+    if self_collision and self_collision_pairs is None:
+        self_collision_pairs = _self_collision_pairs(order, self_collision_min_gap)
     pairs = np.array(self_collision_pairs or [], dtype=np.int32).reshape(-1, 2)
 
     def sym6(I):
@@ -476,7 +533,10 @@ def compile_mjcf(path: str, sensor_bodies: Optional[List[str]] = None,
 def load_robot(name: str) -> CompiledModel:
     """The three robots of the hot path with their task-side sensor lists."""
     if name == "Humanoid":
-        return compile_mjcf(asset_path("humanoid.xml"), sensor_bodies=["right_foot", "left_foot"])
+        # Humanoid.yaml:80 enable_self_collisions: True -> generate the pair list (used only
+        # when the sim params enable self-collisions)
+        return compile_mjcf(asset_path("humanoid.xml"), sensor_bodies=["right_foot", "left_foot"],
+                            self_collision=True)
     if name == "Ant":
         return compile_mjcf(asset_path("ant.xml"), sensor_bodies=[
             "front_left_foot", "front_right_foot", "left_back_foot", "right_back_foot"])

@@ -14,6 +14,7 @@
  * OpenMP parallelises over envs (the cpu_baseline leg of bench.py).
  */
 #include "oracle.h"
+#include "../include/mi_geom.h"   /* contact geometry, shared as source with the device */
 #include <math.h>
 #include <stdlib.h>
 #include <string.h>
@@ -187,7 +188,7 @@ static void m6_vec(const float* A, const float* v, float* o) {
 /* model + sim                                                                           */
 /* ------------------------------------------------------------------------------------ */
 typedef struct {
-    int dyn, root_free, L, G, S, P, D, nv, nr, npts, max_rows;
+    int dyn, root_free, L, G, S, P, D, nv, nr, npts, max_rows, nlimc, self_on;
     int *parent, *jtype, *geom_link, *geom_type, *sensor_link, *pairs;
     float *axis, *pos, *quat, *mass, *com, *inertia, *lower, *upper, *damping, *armature;
     float *geom_p0, *geom_p1, *geom_radius, *sensor_pos;
@@ -264,7 +265,14 @@ orc_sim* orc_sim_create(const mi_model_desc* md, const mi_sim_params* params, in
         m->pt_geom[k] = g; m->pt_end[k++] = 0;
         if (m->geom_type[g] == MI_GEOM_CAPSULE) { m->pt_geom[k] = g; m->pt_end[k++] = 1; }
     }
+    m->nlimc = 0;
+    for (int l = 1; l < m->L; ++l) m->nlimc += md->lower[l] < md->upper[l];
+    m->self_on = params->enable_self_collisions && m->P > 0;
     m->max_rows = 3 * m->npts + m->D;
+    if (m->self_on) {
+        int r = 3 * (m->npts + m->P) + m->D;
+        m->max_rows = r < MI_MAX_ROWS ? r : MI_MAX_ROWS;
+    }
     s->p = *params;
     s->N = N; s->off = off; s->seed = seed;
     int D = m->D > 0 ? m->D : 1, S = m->S > 0 ? m->S : 1;
@@ -359,8 +367,8 @@ static void cartpole_substep(const model_t* m, const mi_sim_params* p, float* q,
 /* ------------------------------------------------------------------------------------ */
 typedef struct {
     float *R, *o, *aw, *I6, *S, *V, *A, *J, *M, *Gc, *C, *u, *rhs, *ud;
-    float *Jr, *W, *b, *lam, *Ad, *cpt;
-    int *rkind, *rcon, *clink;
+    float *Jr, *W, *b, *lam, *Ad, *cpt, *cdir, *tmp;
+    int *rkind, *rcon, *clink, *clink2;
     int nrows, ncon;
     float margin; /* min distance of any activation decision from its threshold (test aid) */
 } ws_t;
@@ -378,13 +386,16 @@ static ws_t* ws_new(const model_t* m) {
     w->Jr = (float*)calloc((size_t)R * nv + 1, 4); w->W = (float*)calloc((size_t)R * nv + 1, 4);
     w->b = (float*)calloc(R, 4); w->lam = (float*)calloc(R, 4); w->Ad = (float*)calloc(R, 4);
     w->rkind = (int*)calloc(R, 4); w->rcon = (int*)calloc(R, 4);
-    w->cpt = (float*)calloc(m->npts * 3 + 3, 4); w->clink = (int*)calloc(m->npts + 1, 4);
+    const int nc = m->npts + (m->self_on ? m->P : 0) + 1;   /* contact capacity */
+    w->cpt = (float*)calloc((size_t)nc * 3, 4); w->clink = (int*)calloc(nc, 4);
+    w->clink2 = (int*)calloc(nc, 4); w->cdir = (float*)calloc((size_t)nc * 9, 4);
+    w->tmp = (float*)calloc(nv + 1, 4);
     return w;
 }
 static void ws_free(ws_t* w) {
     void* p[] = {w->R, w->o, w->aw, w->I6, w->S, w->V, w->A, w->J, w->M, w->Gc, w->C, w->u,
                  w->rhs, w->ud, w->Jr, w->W, w->b, w->lam, w->Ad, w->rkind, w->rcon, w->cpt,
-                 w->clink};
+                 w->clink, w->clink2, w->cdir, w->tmp};
     for (size_t i = 0; i < sizeof p / sizeof p[0]; ++i) free(p[i]);
     free(w);
 }
@@ -627,7 +638,9 @@ static void artic_substep(const model_t* m, const mi_sim_params* p, ws_t* w, flo
         if (bn > p->max_depenetration_velocity) bn = p->max_depenetration_velocity;
         memcpy(w->cpt + 3 * ncon, pc, 12);
         w->clink[ncon] = l;
+        w->clink2[ncon] = -1;
         static const float dirs[3][3] = {{0, 0, 1}, {1, 0, 0}, {0, 1, 0}};
+        memcpy(w->cdir + 9 * ncon, dirs, 36);
         for (int t = 0; t < 3; ++t) {
             float f[6];
             cross3(pc, dirs[t], f);
@@ -639,6 +652,51 @@ static void artic_substep(const model_t* m, const mi_sim_params* p, ws_t* w, flo
             ++nrows;
         }
         ++ncon;
+    }
+    /* self-contacts (Humanoid.yaml:80), pair order, within the MI_MAX_ROWS budget */
+    if (m->self_on) {
+        int budget = (MI_MAX_ROWS - 3 * ncon - m->nlimc) / 3;
+        for (int pi = 0; pi < m->P && budget > 0; ++pi) {
+            const int ga = m->pairs[2 * pi], gb = m->pairs[2 * pi + 1];
+            const int la = m->geom_link[ga], lb = m->geom_link[gb];
+            float a0[3], a1[3], b0[3], b1[3];
+            m3_vec(w->R + 9 * la, m->geom_p0 + 3 * ga, a0);
+            m3_vec(w->R + 9 * la, m->geom_p1 + 3 * ga, a1);
+            m3_vec(w->R + 9 * lb, m->geom_p0 + 3 * gb, b0);
+            m3_vec(w->R + 9 * lb, m->geom_p1 + 3 * gb, b1);
+            for (int k = 0; k < 3; ++k) {
+                a0[k] += w->o[3 * la + k]; a1[k] += w->o[3 * la + k];
+                b0[k] += w->o[3 * lb + k]; b1[k] += w->o[3 * lb + k];
+            }
+            float pc[3], n[3];
+            const float gap = mi_pair_contact(a0, a1, m->geom_radius[ga], b0, b1, m->geom_radius[gb], pc, n);
+            w->margin = fminf(w->margin, fabsf(gap - p->contact_offset));
+            if (!(gap < p->contact_offset)) continue;
+            --budget;
+            const float d = gap - p->rest_offset;
+            float bn = d >= 0.0f ? -d / dt : -p->erp * d / dt;
+            if (bn > p->max_depenetration_velocity) bn = p->max_depenetration_velocity;
+            memcpy(w->cpt + 3 * ncon, pc, 12);
+            w->clink[ncon] = la;
+            w->clink2[ncon] = lb;
+            float* dirs = w->cdir + 9 * ncon;
+            memcpy(dirs, n, 12);
+            mi_contact_basis(n, dirs + 3, dirs + 6);
+            for (int t = 0; t < 3; ++t) {
+                float f[6];
+                cross3(pc, dirs + 3 * t, f);
+                f[3] = dirs[3 * t]; f[4] = dirs[3 * t + 1]; f[5] = dirs[3 * t + 2];
+                float* row = w->Jr + (size_t)nrows * nv;
+                spatial_to_dof_row(m, w, la, f, row);          /* J_a - J_b */
+                spatial_to_dof_row(m, w, lb, f, w->tmp);
+                for (int k = 0; k < nv; ++k) row[k] = row[k] - w->tmp[k];
+                w->rkind[nrows] = t;
+                w->rcon[nrows] = nrows - t;
+                w->b[nrows] = t == 0 ? bn : 0.0f;
+                ++nrows;
+            }
+            ++ncon;
+        }
     }
     for (int j = 0; j < D; ++j) {
         int l = j + 1, k = nr + j;
@@ -697,9 +755,12 @@ static void artic_substep(const model_t* m, const mi_sim_params* p, ws_t* w, flo
         m3_vec(w->R + 9 * l, m->sensor_pos + 3 * si, xs);
         for (int k = 0; k < 3; ++k) xs[k] += w->o[3 * l + k];
         for (int c = 0; c < ncon; ++c) {
-            if (w->clink[c] != l) continue;
+            const float sgn = w->clink[c] == l ? 1.0f : (w->clink2[c] == l ? -1.0f : 0.0f);
+            if (sgn == 0.0f) continue;
             float fn = w->lam[3 * c] / dt, f1 = w->lam[3 * c + 1] / dt, f2 = w->lam[3 * c + 2] / dt;
-            float fc[3] = {f1, f2, fn}, rr[3], tc[3];
+            const float* dd = w->cdir + 9 * c;     /* normal, t1, t2 */
+            float fc[3], rr[3], tc[3];
+            for (int k = 0; k < 3; ++k) fc[k] = sgn * (fn * dd[k] + f1 * dd[3 + k] + f2 * dd[6 + k]);
             for (int k = 0; k < 3; ++k) rr[k] = w->cpt[3 * c + k] - xs[k];
             cross3(rr, fc, tc);
             for (int k = 0; k < 3; ++k) { F[k] += fc[k]; T[k] += tc[k]; }
@@ -1195,6 +1256,34 @@ void orc_momentum(orc_sim* s, int env, double* out) {
     cross3(s->root_pos + 3 * env, h + 3, pxP);
     for (int k = 0; k < 3; ++k) { out[k] = (double)h[k] + pxP[k]; out[3 + k] = h[3 + k]; }
     ws_free(w);
+}
+
+/* min surface gap over the self-collision pairs of env at its current state (test aid) */
+float orc_self_min_gap(orc_sim* s, int env) {
+    const model_t* m = &s->m;
+    if (m->P == 0 || m->dyn != MI_DYN_ARTICULATION) return INFINITY;
+    ws_t* w = ws_new(m);
+    int D = m->D;
+    float u[64] = {0};
+    kinematics(m, w, s->root_quat + 4 * env, s->q + (size_t)D * env, u);
+    float best = INFINITY;
+    for (int pi = 0; pi < m->P; ++pi) {
+        const int ga = m->pairs[2 * pi], gb = m->pairs[2 * pi + 1];
+        const int la = m->geom_link[ga], lb = m->geom_link[gb];
+        float a0[3], a1[3], b0[3], b1[3], pc[3], n[3];
+        m3_vec(w->R + 9 * la, m->geom_p0 + 3 * ga, a0);
+        m3_vec(w->R + 9 * la, m->geom_p1 + 3 * ga, a1);
+        m3_vec(w->R + 9 * lb, m->geom_p0 + 3 * gb, b0);
+        m3_vec(w->R + 9 * lb, m->geom_p1 + 3 * gb, b1);
+        for (int k = 0; k < 3; ++k) {
+            a0[k] += w->o[3 * la + k]; a1[k] += w->o[3 * la + k];
+            b0[k] += w->o[3 * lb + k]; b1[k] += w->o[3 * lb + k];
+        }
+        const float gap = mi_pair_contact(a0, a1, m->geom_radius[ga], b0, b1, m->geom_radius[gb], pc, n);
+        best = gap < best ? gap : best;
+    }
+    ws_free(w);
+    return best;
 }
 
 int orc_contact_count(orc_sim* s, int env) {

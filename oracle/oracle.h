@@ -78,6 +78,7 @@ void orc_aba(orc_sim* s, int env, const float* tau /*[n]*/, float* udot /*[n]*/)
 double orc_energy(orc_sim* s, int env);
 void orc_momentum(orc_sim* s, int env, double* out6 /* angular about world origin, linear */);
 int orc_contact_count(orc_sim* s, int env);
+float orc_self_min_gap(orc_sim* s, int env);
 void orc_decision_margin(const orc_sim* s, float* out /*[N]*/);
 
 #ifdef __cplusplus

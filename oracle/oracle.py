@@ -66,6 +66,7 @@ def lib() -> C.CDLL:
             "orc_energy": (C.c_double, [C.c_void_p, C.c_int]),
             "orc_momentum": (None, [C.c_void_p, C.c_int, C.POINTER(C.c_double)]),
             "orc_contact_count": (C.c_int, [C.c_void_p, C.c_int]),
+            "orc_self_min_gap": (C.c_float, [C.c_void_p, C.c_int]),
             "orc_decision_margin": (None, [C.c_void_p, C.c_void_p]),
         }
         for name, (res, args) in sig.items():
@@ -215,6 +216,10 @@ class OracleSim:
 
     def contact_count(self, env: int) -> int:
         return int(lib().orc_contact_count(self.h, env))
+
+    def self_min_gap(self, env: int) -> float:
+        """Smallest surface gap over the model's self-collision pairs (current state)."""
+        return float(lib().orc_self_min_gap(self.h, env))
 
     def decision_margin(self) -> np.ndarray:
         """[N] min |x - threshold| over every contact / limit activation test of the last

@@ -185,11 +185,13 @@ def test_fused_equals_modular(gpu):
 
 
 def test_wave_path_matches_thread_path(gpu, monkeypatch):
-    """Wavefront-per-env kernel (default) vs the one-lane-per-env reference kernel."""
+    """Wavefront-per-env kernel (default) vs the one-lane-per-env reference kernel. The
+    one-lane kernel has no self-collision (it refuses it), so Humanoid runs without it here."""
     for name in ("Ant", "Humanoid"):
-        ea = make_env(name, num_envs=128, device="cuda:0", seed=31)
+        ov = [f"task.sim.{name}.enable_self_collisions=False"]
+        ea = make_env(name, num_envs=128, device="cuda:0", seed=31, overrides=ov)
         monkeypatch.setenv("MI_SIM_PATH", "thread")
-        eb = make_env(name, num_envs=128, device="cuda:0", seed=31)
+        eb = make_env(name, num_envs=128, device="cuda:0", seed=31, overrides=ov)
         monkeypatch.delenv("MI_SIM_PATH")
         orc = oracle_twin(ea, 31)   # only to measure decision margins of the same state
         for step in range(3):
@@ -229,3 +231,36 @@ def test_compiled_topology_matches_runtime_tables(gpu, monkeypatch):
             assert torch.equal(da, db)
         ea.close()
         eb.close()
+
+
+def test_self_collision_thread_path_refused(gpu, monkeypatch):
+    """The one-lane-per-env kernel has no self-collision: asking for it fails loudly."""
+    monkeypatch.setenv("MI_SIM_PATH", "thread")
+    with pytest.raises(RuntimeError, match="self-collision"):
+        make_env("Humanoid", num_envs=8, device="cuda:0", seed=1)
+
+
+def test_self_collision_active_on_device(gpu):
+    """Humanoid (self-collision on) vs the oracle over a longer random rollout, re-synced each
+    step; the oracle confirms self-contacts occur in the sampled states."""
+    env = make_env("Humanoid", num_envs=256, device="cuda:0", seed=5)
+    task = env.task
+    assert task.get_robot().sim_params.enable_self_collisions == 1
+    orc = oracle_twin(env, 5)
+    env.reset()
+    torch.cuda.synchronize()
+    sync_oracle(env, orc)
+    touching = 0
+    for step in range(12):
+        b = task_buffers(env)
+        acts = rand_actions(256, task.num_actions, 300 + step)
+        obs_dict, rew, resets, _ = env.step(acts.to("cuda:0"))
+        torch.cuda.synchronize()
+        orc.env_step(acts.numpy(), task.control_frequency_inv, b)
+        check_pair("Humanoid", task, obs_dict["obs"].cpu().numpy(), rew.cpu().numpy(), b["obs"],
+                   b["rew"], 2e-3, orc.decision_margin())
+        assert np.array_equal(resets.cpu().numpy(), b["reset"])
+        sync_oracle(env, orc)
+        touching += sum(orc.self_min_gap(e) < 0.02 for e in range(0, 256, 8))
+    assert touching > 0
+    env.close()

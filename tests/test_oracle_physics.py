@@ -134,3 +134,32 @@ def test_humanoid_settles_without_nan():
     assert np.abs(v).max() < 1.0
     s = sim.sensors()
     assert np.isfinite(s).all()
+
+
+def test_self_collision_limits_penetration():
+    """Humanoid self-collision (Humanoid.yaml:80): with the pair contacts on, limbs stay
+    (nearly) apart under random actions; with them off they pass through each other."""
+    from oracle.oracle import OracleSim, make_buffers
+    from omniisaacgymenvs_amd.robots.model import load_robot
+    from tests.helpers import sim_params, task_params_from_cfg
+
+    m = load_robot("Humanoid")
+    assert m.pairs.shape[0] > 100
+    worst = {}
+    for esc in (1, 0):
+        n = 32
+        orc = OracleSim(m, sim_params(enable_self_collisions=esc), n, np.zeros((n, 3), np.float32), seed=3)
+        tp, _, keep = task_params_from_cfg("Humanoid")
+        orc.configure(tp, keep=keep)
+        b = make_buffers(n, tp.num_obs, tp.num_actions)
+        b["reset"][:] = 1
+        rng = np.random.default_rng(0)
+        w = np.inf
+        for step in range(120):
+            orc.env_step(rng.uniform(-1, 1, (n, tp.num_actions)).astype(np.float32), 2, b)
+            if step % 10 == 9:
+                w = min(w, min(orc.self_min_gap(e) for e in range(n)))
+        assert orc.nan_count() == 0
+        worst[esc] = w
+    assert worst[1] > -0.06, worst
+    assert worst[0] < worst[1] - 0.03, worst
