@@ -650,11 +650,8 @@ int mi_sim_create(const mi_model_desc* md, const mi_sim_params* prm, int32_t N, 
             t.nlimc = (int)lim.size();
             if (lim.empty()) lim.push_back(0);
             t.mc_lim = put_ints(lim);
-            pad4();
-            t.mc_len = (int)mcb.size();
-            t.npts = np; t.nsens = ns;
-            UPW(g_mc, mcb);
-            // self-collision geometry: per geom (link, p0, p1, radius) and the geom pairs
+            // self-collision geometry: per geom (link, p0, p1, radius) and the geom pairs;
+            // global copies, and inside the LDS block when self-collision is on
             std::vector<float> geo((size_t)8 * std::max(1, md->num_geoms), 0.0f);
             for (int g = 0; g < md->num_geoms; ++g) {
                 geo[8 * g] = (float)md->geom_link[g];
@@ -667,6 +664,17 @@ int mi_sim_create(const mi_model_desc* md, const mi_sim_params* prm, int32_t N, 
             std::vector<int> prs(md->pairs ? md->pairs : nullptr,
                                  md->pairs ? md->pairs + 2 * md->num_pairs : nullptr);
             if (prs.empty()) prs.assign(2, 0);
+            t.mc_geo = t.mc_pairs = -1;
+            if (self_on) {
+                pad4();
+                t.mc_geo = (int)mcb.size();
+                mcb.insert(mcb.end(), geo.begin(), geo.begin() + 8 * md->num_geoms);
+                t.mc_pairs = put_ints(prs);
+            }
+            pad4();
+            t.mc_len = (int)mcb.size();
+            t.npts = np; t.nsens = ns;
+            UPW(g_mc, mcb);
             UPW(g_geo, geo); UPW(g_pairs, prs);
         }
 #undef UPW
@@ -710,7 +718,7 @@ int mi_sim_create(const mi_model_desc* md, const mi_sim_params* prm, int32_t N, 
         }
         // CT path: J rows of up to 64 constraint rows for the PGS (LDS is not the occupancy
         // limit here: registers cap the wave path at 2 waves/SIMD = 8 envs/CU = 20 KB each)
-        t.j_rows_lds = ct ? std::min(64, m.max_rows) : 0;
+        t.j_rows_lds = ct ? std::min(48, m.max_rows) : 0;
         t.s_J = take(ct ? t.j_rows_lds * m.nv : 4);
         t.s_total = so;
         {   // the sequential regions strictly increase; the row data sits inside the dead
@@ -729,6 +737,13 @@ int mi_sim_create(const mi_model_desc* md, const mi_sim_params* prm, int32_t N, 
         // CT path: the rest of the dead span holds the first W rows (P9 -> P10 hand-over)
         t.s_W = ro;
         t.w_rows_lds = overlay ? std::min(64, (span1 - ro) / m.nv) : 0;
+        // P8 self-collision scratch (segments + broad-phase survivors) in the same free span
+        t.ngeoms = md->num_geoms;
+        t.s_seg = -1; t.s_surv = -1;
+        if (overlay && self_on && al4(8 * md->num_geoms) + al4(md->num_pairs) <= span1 - ro) {
+            t.s_seg = ro;
+            t.s_surv = ro + al4(8 * md->num_geoms);
+        }
         s->lds_bytes = (size_t)so * sizeof(float);
     }
     s->lower.assign(md->lower, md->lower + L);

@@ -99,6 +99,7 @@ struct WaveTabs {
     // launch by every workgroup
     const float* g_mc;
     int mc_len, mc_pts, mc_sens, mc_chs, mc_chl, mc_dss, mc_dsl, mc_lim;   // block offsets
+    int mc_geo, mc_pairs;   // self-collision geom table [G][8] and pairs [P][2] (or -1)
     int npts, nsens;
     int nlimc;   // joints with a limit (lower < upper): limit-row candidates, joint ids at mc_lim
     // self-collision (mi_geom.h): geom table [G][8] = link, p0 (3), p1 (3), radius and the
@@ -107,6 +108,9 @@ struct WaveTabs {
     const float* g_geo;
     const int* g_pairs;
     int s_cl2, s_cn;   // per contact: second link (-1: ground), normal (3)
+    int s_seg, s_surv; // P8 scratch (in the W span, free until P9): world segments [G][8] and
+                       // broad-phase survivors [P]; s_seg < 0: not enough room, direct path
+    int ngeoms;
 };
 
 // Per-model constants in the LDS block, structure-of-arrays so lane-indexed reads (lane = link,
@@ -702,7 +706,93 @@ MI_D void wave_artic_substep(const DevModel& m, const WaveTabs& t, const DevStat
     }
     // self-contacts (Humanoid.yaml:80): lanes over geom pairs, compacted in pair order within
     // the MI_MAX_ROWS budget, after the ground contacts (as the oracle)
-    if (t.self_on) {
+    if (t.self_on && t.s_seg >= 0) {
+        // world segments of every geom, once (lanes over geoms)
+        float* seg = sm + t.s_seg;
+        const float* geo = sm + t.s_mc + t.mc_geo;                        // LDS copies
+        const int* prs = reinterpret_cast<const int*>(sm + t.s_mc + t.mc_pairs);
+        for (int g = lane; g < t.ngeoms; g += 64) {
+            const float* A = geo + 8 * g;
+            const int l = (int)A[0];
+            float R[9], a0[3], a1[3];
+#pragma unroll
+            for (int q = 0; q < 9; ++q) R[q] = sm[t.s_R + 9 * l + q];
+            m3_vec(R, A + 1, a0); m3_vec(R, A + 4, a1);
+#pragma unroll
+            for (int q = 0; q < 3; ++q) {
+                seg[8 * g + q] = a0[q] + sm[t.s_o + 3 * l + q];
+                seg[8 * g + 3 + q] = a1[q] + sm[t.s_o + 3 * l + q];
+            }
+            seg[8 * g + 6] = A[7];
+            seg[8 * g + 7] = (float)l;
+        }
+        __syncthreads();
+        // broad phase (conservative bounding spheres), survivors compacted in pair order
+        int* surv = reinterpret_cast<int*>(sm + t.s_surv);
+        int nsv = 0;
+        for (int pb = 0; pb < t.npairs; pb += 64) {
+            const int pi = pb + lane;
+            bool keep = false;
+            if (pi < t.npairs) {
+                const float* A = seg + 8 * prs[2 * pi];
+                const float* B = seg + 8 * prs[2 * pi + 1];
+                float d2 = 0.0f, ha = 0.0f, hb = 0.0f;
+#pragma unroll
+                for (int q = 0; q < 3; ++q) {
+                    const float c = 0.5f * (A[q] + A[3 + q]) - 0.5f * (B[q] + B[3 + q]);
+                    const float ea = A[3 + q] - A[q], eb = B[3 + q] - B[q];
+                    d2 += c * c; ha += ea * ea; hb += eb * eb;
+                }
+                const float reach = 0.5f * sqrtf(ha) + 0.5f * sqrtf(hb) + A[6] + B[6] +
+                                    p.contact_offset + 1e-3f;
+                keep = d2 < reach * reach;
+            }
+            const unsigned long long mask = __ballot(keep);
+            if (keep) surv[nsv + __popcll(mask & ((1ull << lane) - 1ull))] = pi;
+            nsv += __popcll(mask);
+        }
+        nsv = __builtin_amdgcn_readfirstlane(nsv);
+        __syncthreads();
+        // narrow phase on the survivors (mi_geom.h, as the oracle)
+        int budget = (MI_MAX_ROWS - 3 * ncon - t.nlimc) / 3;
+        for (int sb = 0; sb < nsv && budget > 0; sb += 64) {
+            const int sidx = sb + lane;
+            bool act = false;
+            float pc[3], n[3], bn = 0.0f;
+            int la = 0, lb = 0;
+            if (sidx < nsv) {
+                const int pi = surv[sidx];
+                const float* A = seg + 8 * prs[2 * pi];
+                const float* B = seg + 8 * prs[2 * pi + 1];
+                la = (int)A[7]; lb = (int)B[7];
+                const float gap = mi_pair_contact(A, A + 3, A[6], B, B + 3, B[6], pc, n);
+                act = gap < p.contact_offset;
+                const float d = gap - p.rest_offset;
+                bn = d >= 0.0f ? -d / dt : -p.erp * d / dt;
+                if (bn > p.max_depen) bn = p.max_depen;
+            }
+            const unsigned long long mask = __ballot(act);
+            const int rank = __popcll(mask & ((1ull << lane) - 1ull));
+            if (act && rank < budget) {
+                const int ci = ncon + rank;
+#pragma unroll
+                for (int q = 0; q < 3; ++q) { sm[t.s_cp + 3 * ci + q] = pc[q]; sm[t.s_cn + 3 * ci + q] = n[q]; }
+                sm[t.s_cl + ci] = (float)la;
+                sm[t.s_cl2 + ci] = (float)lb;
+#pragma unroll
+                for (int tt = 0; tt < 3; ++tt) {
+                    const int r = 3 * ci + tt;
+                    sm[t.s_rl + r] = (float)la;
+                    sm[t.s_rb + r] = tt == 0 ? bn : 0.0f;
+                    sm[t.s_rk + r] = (float)tt;
+                }
+            }
+            const int took = min(__popcll(mask), budget);
+            ncon += took;
+            budget -= took;
+        }
+        ncon = __builtin_amdgcn_readfirstlane(ncon);
+    } else if (t.self_on) {
         int budget = (MI_MAX_ROWS - 3 * ncon - t.nlimc) / 3;
         for (int pb = 0; pb < t.npairs && budget > 0; pb += 64) {
             const int pi = pb + lane;
