@@ -740,9 +740,9 @@ int mi_sim_create(const mi_model_desc* md, const mi_sim_params* prm, int32_t N, 
         // P8 self-collision scratch (segments + broad-phase survivors) in the same free span
         t.ngeoms = md->num_geoms;
         t.s_seg = -1; t.s_surv = -1;
-        if (overlay && self_on && al4(8 * md->num_geoms) + al4(md->num_pairs) <= span1 - ro) {
+        if (overlay && self_on && al4(12 * md->num_geoms) + al4(md->num_pairs) <= span1 - ro) {
             t.s_seg = ro;
-            t.s_surv = ro + al4(8 * md->num_geoms);
+            t.s_surv = ro + al4(12 * md->num_geoms);
         }
         s->lds_bytes = (size_t)so * sizeof(float);
     }

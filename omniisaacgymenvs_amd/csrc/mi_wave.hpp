@@ -108,8 +108,9 @@ struct WaveTabs {
     const float* g_geo;
     const int* g_pairs;
     int s_cl2, s_cn;   // per contact: second link (-1: ground), normal (3)
-    int s_seg, s_surv; // P8 scratch (in the W span, free until P9): world segments [G][8] and
-                       // broad-phase survivors [P]; s_seg < 0: not enough room, direct path
+    int s_seg, s_surv; // P8 scratch (in the W span, free until P9): world segments [G][8],
+                       // bounding spheres [G][4] at s_seg + 8G, broad-phase survivors [P];
+                       // s_seg < 0: not enough room, direct path
     int ngeoms;
 };
 
@@ -709,6 +710,7 @@ MI_D void wave_artic_substep(const DevModel& m, const WaveTabs& t, const DevStat
     if (t.self_on && t.s_seg >= 0) {
         // world segments of every geom, once (lanes over geoms)
         float* seg = sm + t.s_seg;
+        float* bnd = seg + 8 * t.ngeoms;   // bounding sphere: centre (3), half-length + radius
         const float* geo = sm + t.s_mc + t.mc_geo;                        // LDS copies
         const int* prs = reinterpret_cast<const int*>(sm + t.s_mc + t.mc_pairs);
         for (int g = lane; g < t.ngeoms; g += 64) {
@@ -725,27 +727,30 @@ MI_D void wave_artic_substep(const DevModel& m, const WaveTabs& t, const DevStat
             }
             seg[8 * g + 6] = A[7];
             seg[8 * g + 7] = (float)l;
+            float e2 = 0.0f;
+#pragma unroll
+            for (int q = 0; q < 3; ++q) {
+                bnd[4 * g + q] = sm[t.s_o + 3 * l + q] + 0.5f * (a0[q] + a1[q]);
+                e2 += (a1[q] - a0[q]) * (a1[q] - a0[q]);
+            }
+            bnd[4 * g + 3] = 0.5f * sqrtf(e2) + A[7];
         }
         __syncthreads();
-        // broad phase (conservative bounding spheres), survivors compacted in pair order
+        // broad phase (conservative bounding spheres: the segments' distance is at least the
+        // centre distance minus both half-lengths), survivors compacted in pair order
         int* surv = reinterpret_cast<int*>(sm + t.s_surv);
         int nsv = 0;
+        const float slack = p.contact_offset + 1e-3f;
         for (int pb = 0; pb < t.npairs; pb += 64) {
             const int pi = pb + lane;
             bool keep = false;
             if (pi < t.npairs) {
-                const float* A = seg + 8 * prs[2 * pi];
-                const float* B = seg + 8 * prs[2 * pi + 1];
-                float d2 = 0.0f, ha = 0.0f, hb = 0.0f;
-#pragma unroll
-                for (int q = 0; q < 3; ++q) {
-                    const float c = 0.5f * (A[q] + A[3 + q]) - 0.5f * (B[q] + B[3 + q]);
-                    const float ea = A[3 + q] - A[q], eb = B[3 + q] - B[q];
-                    d2 += c * c; ha += ea * ea; hb += eb * eb;
-                }
-                const float reach = 0.5f * sqrtf(ha) + 0.5f * sqrtf(hb) + A[6] + B[6] +
-                                    p.contact_offset + 1e-3f;
-                keep = d2 < reach * reach;
+                const int2 gp = *reinterpret_cast<const int2*>(prs + 2 * pi);
+                const float4 A = *reinterpret_cast<const float4*>(bnd + 4 * gp.x);
+                const float4 B = *reinterpret_cast<const float4*>(bnd + 4 * gp.y);
+                const float cx = A.x - B.x, cy = A.y - B.y, cz = A.z - B.z;
+                const float reach = A.w + B.w + slack;
+                keep = cx * cx + cy * cy + cz * cz < reach * reach;
             }
             const unsigned long long mask = __ballot(keep);
             if (keep) surv[nsv + __popcll(mask & ((1ull << lane) - 1ull))] = pi;
