@@ -244,10 +244,11 @@ static void with_topo(int id, F&& f) {
 }
 
 // id of the generated topology whose link tree equals the model's (0: none)
-static int match_topology(const mi_model_desc* md) {
+static int match_topology(const mi_model_desc* md, bool self_on) {
     const int nr = md->root_free ? 6 : 0;
     for (const GenTopo& g : kGenTopos) {
         if (g.L != md->num_links || g.nr != nr) continue;
+        if (self_on && !g.self) continue;   // compiled without self-collision: runtime tables
         bool same = true;
         for (int l = 1; l < g.L && same; ++l) same = g.link_parent[l] == md->parent[l];
         if (same) return g.id;
@@ -534,7 +535,7 @@ int mi_sim_create(const mi_model_desc* md, const mi_sim_params* prm, int32_t N, 
     }
     if (s->wave) {
         const char* tsel = getenv("MI_SIM_TOPO");
-        s->topo = (tsel && std::string(tsel) == "runtime") ? 0 : match_topology(md);
+        s->topo = (tsel && std::string(tsel) == "runtime") ? 0 : match_topology(md, self_on);
         WaveTabs& t = s->wt;
         std::vector<int> depth(L, 0);
         int maxd = 0;

@@ -149,8 +149,10 @@ struct MC {
 // contact point instead of stored per row (saves 6 floats x rows of LDS); same arithmetic.
 // Contact ci's directions (normal, t1, t2): ground +z / +x / +y, self-contact the stored
 // normal and mi_contact_basis (same as the oracle).
+// SELF = false (a model compiled without self-collision pairs): every contact is a ground contact.
+template <bool SELF>
 MI_D void contact_dirs(const float* sm, const WaveTabs& t, int ci, float (&d)[9]) {
-    if (sm[t.s_cl2 + ci] < 0.0f) {
+    if (!SELF || sm[t.s_cl2 + ci] < 0.0f) {
 #pragma unroll
         for (int k = 0; k < 9; ++k) d[k] = (k == 2 || k == 3 || k == 7) ? 1.0f : 0.0f;
     } else {
@@ -159,11 +161,12 @@ MI_D void contact_dirs(const float* sm, const WaveTabs& t, int ci, float (&d)[9]
     }
 }
 
+template <bool SELF>
 MI_D void contact_row_f(const float* sm, const WaveTabs& t, int r, float (&f)[6]) {
     const int ci = r / 3, tt = r - 3 * ci;
     const float pc[3] = {sm[t.s_cp + 3 * ci], sm[t.s_cp + 3 * ci + 1], sm[t.s_cp + 3 * ci + 2]};
     float d[9];
-    contact_dirs(sm, t, ci, d);
+    contact_dirs<SELF>(sm, t, ci, d);
     const float dir[3] = {d[3 * tt], d[3 * tt + 1], d[3 * tt + 2]};
     cross3(pc, dir, f);
     f[3] = dir[0]; f[4] = dir[1]; f[5] = dir[2];
@@ -707,7 +710,7 @@ MI_D void wave_artic_substep(const DevModel& m, const WaveTabs& t, const DevStat
     }
     // self-contacts (Humanoid.yaml:80): lanes over geom pairs, compacted in pair order within
     // the MI_MAX_ROWS budget, after the ground contacts (as the oracle)
-    if (t.self_on && t.s_seg >= 0) {
+    if (TP::kSelf && t.self_on && t.s_seg >= 0) {
         // world segments of every geom, once (lanes over geoms)
         float* seg = sm + t.s_seg;
         float* bnd = seg + 8 * t.ngeoms;   // bounding sphere: centre (3), half-length + radius
@@ -797,7 +800,7 @@ MI_D void wave_artic_substep(const DevModel& m, const WaveTabs& t, const DevStat
             budget -= took;
         }
         ncon = __builtin_amdgcn_readfirstlane(ncon);
-    } else if (t.self_on) {
+    } else if (TP::kSelf && t.self_on) {
         int budget = (MI_MAX_ROWS - 3 * ncon - t.nlimc) / 3;
         for (int pb = 0; pb < t.npairs && budget > 0; pb += 64) {
             const int pi = pb + lane;
@@ -948,10 +951,10 @@ MI_D void wave_artic_substep(const DevModel& m, const WaveTabs& t, const DevStat
             if (on && r >= 0) {
                 // J_r = J_a^T f - J_b^T f (b: the second body of a self-contact, else none)
                 const int l = (int)sm[t.s_rl + r];
-                const float l2 = sm[t.s_cl2 + r / 3];
+                const float l2 = TP::kSelf ? sm[t.s_cl2 + r / 3] : -1.0f;
                 const unsigned msk = mc.mask(l), msk2 = l2 >= 0.0f ? mc.mask((int)l2) : 0u;
                 float f[6];
-                contact_row_f(sm, t, r, f);
+                contact_row_f<TP::kSelf>(sm, t, r, f);
                 sfor<0, TP::nv>([&](auto C) {
                     constexpr int c = C;
                     const bool ia = (msk >> c) & 1u, ib = (msk2 >> c) & 1u;
@@ -989,10 +992,10 @@ MI_D void wave_artic_substep(const DevModel& m, const WaveTabs& t, const DevStat
             for (int c = 0; c < WNV; ++c) jr[c] = 0.0f;
             if (on && r >= 0) {
                 const int l = (int)sm[t.s_rl + r];
-                const float l2 = sm[t.s_cl2 + r / 3];
+                const float l2 = TP::kSelf ? sm[t.s_cl2 + r / 3] : -1.0f;
                 const unsigned msk = mc.mask(l), msk2 = l2 >= 0.0f ? mc.mask((int)l2) : 0u;
                 float f[6];
-                contact_row_f(sm, t, r, f);
+                contact_row_f<TP::kSelf>(sm, t, r, f);
 #pragma unroll
                 for (int c = 0; c < WNV; ++c) {
                     const bool ia = (msk >> c) & 1u, ib = (msk2 >> c) & 1u;
@@ -1082,9 +1085,9 @@ MI_D void wave_artic_substep(const DevModel& m, const WaveTabs& t, const DevStat
                 k = sm[t.s_rk + r];
                 const float lk = sm[t.s_rl + r];
                 if (lk >= 0.0f) {
-                    contact_row_f(sm, t, r, f);
+                    contact_row_f<TP::kSelf>(sm, t, r, f);
                     msk = mc.mask((int)lk);
-                    const float l2 = sm[t.s_cl2 + r / 3];
+                    const float l2 = TP::kSelf ? sm[t.s_cl2 + r / 3] : -1.0f;
                     msk2 = l2 >= 0.0f ? mc.mask((int)l2) : 0u;
                 } else {
                     const int kdof = (int)(-lk - 1.0f);
@@ -1198,12 +1201,13 @@ MI_D void wave_artic_substep(const DevModel& m, const WaveTabs& t, const DevStat
         for (int c = 0; c < ncon; ++c) {
 #pragma clang fp contract(off)
             // contact wrench on link l: +f on body a, -f on body b of a self-contact
-            const float sgn = (int)sm[t.s_cl + c] == l ? 1.0f : ((int)sm[t.s_cl2 + c] == l ? -1.0f : 0.0f);
+            const float sgn = (int)sm[t.s_cl + c] == l ? 1.0f :
+                              ((TP::kSelf && (int)sm[t.s_cl2 + c] == l) ? -1.0f : 0.0f);
             if (sgn == 0.0f) continue;
             const float* lam = sm + t.s_ad;
             const float fn = lam[3 * c] / dt, f1 = lam[3 * c + 1] / dt, f2 = lam[3 * c + 2] / dt;
             float d[9];
-            contact_dirs(sm, t, c, d);
+            contact_dirs<TP::kSelf>(sm, t, c, d);
             float fc[3];
 #pragma unroll
             for (int q = 0; q < 3; ++q) fc[q] = sgn * (fn * d[q] + f1 * d[3 + q] + f2 * d[6 + q]);

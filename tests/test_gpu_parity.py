@@ -233,6 +233,36 @@ def test_compiled_topology_matches_runtime_tables(gpu, monkeypatch):
         eb.close()
 
 
+def test_self_collision_on_uncompiled_model_uses_runtime_tables(gpu, monkeypatch):
+    """The compiled Ant topology carries no self-collision code (the shipped Ant has no pairs).
+    An Ant given self-collision pairs runs on the runtime-table kernel, which has it, and still
+    matches the oracle."""
+    import omniisaacgymenvs_amd.tasks.ant as ant_mod
+    from omniisaacgymenvs_amd.robots.model import asset_path, compile_mjcf
+
+    monkeypatch.setattr(ant_mod, "Ant", lambda: compile_mjcf(asset_path("ant.xml"), sensor_bodies=[
+        "front_left_foot", "front_right_foot", "left_back_foot", "right_back_foot"],
+        self_collision=True))
+    env = make_env("Ant", num_envs=64, device="cuda:0", seed=9,
+                   overrides=["task.sim.Ant.enable_self_collisions=True"])
+    rob = env.task.get_robot()
+    assert rob.model.pairs.shape[0] > 0 and rob.sim_params.enable_self_collisions == 1
+    assert rob.sim_topology() == 0
+    orc = oracle_twin(env, 9)
+    env.reset()
+    torch.cuda.synchronize()
+    for step in range(3):
+        sync_oracle(env, orc)
+        b = task_buffers(env)
+        acts = rand_actions(64, env.num_actions, 90 + step)
+        o, r, d, _ = env.step(acts.to("cuda:0"))
+        torch.cuda.synchronize()
+        orc.env_step(acts.numpy(), env.task.control_frequency_inv, b)
+        check_pair("Ant", env.task, o["obs"].cpu().numpy(), r.cpu().numpy(), b["obs"], b["rew"],
+                   2e-3, orc.decision_margin())
+    env.close()
+
+
 def test_self_collision_thread_path_refused(gpu, monkeypatch):
     """The one-lane-per-env kernel has no self-collision: asking for it fails loudly."""
     monkeypatch.setenv("MI_SIM_PATH", "thread")
