@@ -102,6 +102,9 @@ def kernel_name(view, task) -> str:
     return "k_env_step"
 
 
+BASELINE_METRIC = "env-steps/s (physics+obs+reward) Humanoid 4096 envs @1/2/4/8 MI355X"
+
+
 def read_traffic(task_name: str):
     """HBM bytes per launch from the committed PMC pass (profiles/traffic_<task>.json), if any."""
     p = os.path.join(ROOT, "profiles", f"traffic_{task_name}.json")
@@ -194,7 +197,8 @@ def main():
                     "kernel_ms": round(kernel_ms, 4),
                     "algo_bytes_per_launch": ALGO_BYTES[args.task] * n_local}
         out = {
-            "metric": "env-steps/s (physics+obs+reward) Humanoid 4096 envs @1/2/4/8 MI355X",
+            "metric": BASELINE_METRIC if args.task == "Humanoid" else
+                      f"env-steps/s (physics+obs+reward) {args.task} {args.num_envs} envs (side run)",
             "value": round(value, 1), "unit": "env-steps/s", "n_gpus": world, "steps": args.steps,
             "warmup": args.warmup, "ms_per_step": round(elapsed / args.steps * 1e3, 4),
             "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "f32",

@@ -97,11 +97,11 @@ MI_D void artic_substep(const DevModel& m, const DevState& st, const SimP& p, in
     WS w(st.ws, m.slots, i);
     float rp[3], rq[4];
 #pragma unroll
-    for (int k = 0; k < 3; ++k) rp[k] = st.root_pos[(size_t)k * N + i];
+    for (int k = 0; k < 3; ++k) rp[k] = st.root_pos[sx(st, k, i)];
 #pragma unroll
-    for (int k = 0; k < 4; ++k) rq[k] = st.root_quat[(size_t)k * N + i];
-    for (int k = 0; k < nr; ++k) w[m.o_u + k] = st.root_vel[(size_t)k * N + i];
-    for (int j = 0; j < D; ++j) w[m.o_u + nr + j] = st.qd[(size_t)j * N + i];
+    for (int k = 0; k < 4; ++k) rq[k] = st.root_quat[sx(st, k, i)];
+    for (int k = 0; k < nr; ++k) w[m.o_u + k] = st.root_vel[sx(st, k, i)];
+    for (int j = 0; j < D; ++j) w[m.o_u + nr + j] = st.qd[sx(st, j, i)];
 
     // ---------------- pass 1: root -> leaves ----------------
     for (int l = 0; l < L; ++l) {
@@ -136,7 +136,7 @@ MI_D void artic_substep(const DevModel& m, const DevState& st, const SimP& p, in
             m3_mul(RP, Rq, Rj);
             m3_vec(Rj, m.axis + 3 * l, a);
             m3_vec(RP, m.pos + 3 * l, op);
-            const float qj = st.q[(size_t)(l - 1) * N + i];
+            const float qj = st.q[sx(st, l - 1, i)];
             float s[6];
             if (m.jtype[l] == MI_JOINT_HINGE) {
                 float Ra[9];
@@ -237,7 +237,7 @@ MI_D void artic_substep(const DevModel& m, const DevState& st, const SimP& p, in
         float rhs = -Ck;
         if (k >= nr) {
             diag += m.armature[l] + dt * m.damping[l];
-            rhs += st.eff[(size_t)(k - nr) * N + i] - m.damping[l] * w[m.o_u + k];
+            rhs += st.eff[sx(st, k - nr, i)] - m.damping[l] * w[m.o_u + k];
         }
         w[m.o_M + k * nv + k] = diag;
         w[m.o_r + k] = rhs;
@@ -306,7 +306,7 @@ MI_D void artic_substep(const DevModel& m, const DevState& st, const SimP& p, in
         const int l = j + 1, k = nr + j;
         const float lo = m.lower[l], hi = m.upper[l];
         if (!(lo < hi)) continue;
-        const float qj = st.q[(size_t)j * N + i];
+        const float qj = st.q[sx(st, j, i)];
         const float qp = qj + dt * w[m.o_u + k];
         float d, sg;
         if (qj < lo || qp < lo) { d = qj - lo; sg = 1.0f; }
@@ -377,8 +377,8 @@ MI_D void artic_substep(const DevModel& m, const DevState& st, const SimP& p, in
         m3_tvec(R, T, Tl);
 #pragma unroll
         for (int q = 0; q < 3; ++q) {
-            st.sens[(size_t)(6 * si + q) * N + i] = Fl[q];
-            st.sens[(size_t)(6 * si + 3 + q) * N + i] = Tl[q];
+            st.sens[sx(st, 6 * si + q, i)] = Fl[q];
+            st.sens[sx(st, 6 * si + 3 + q, i)] = Tl[q];
         }
     }
     // ---------------- integrate ----------------
@@ -412,17 +412,17 @@ MI_D void artic_substep(const DevModel& m, const DevState& st, const SimP& p, in
             for (int k = 0; k < 4; ++k) rq[k] = nq[k] * nn;
         }
 #pragma unroll
-        for (int k = 0; k < 3; ++k) { st.root_pos[(size_t)k * N + i] = rp[k]; finite &= isfinite(rp[k]); }
+        for (int k = 0; k < 3; ++k) { st.root_pos[sx(st, k, i)] = rp[k]; finite &= isfinite(rp[k]); }
 #pragma unroll
-        for (int k = 0; k < 4; ++k) { st.root_quat[(size_t)k * N + i] = rq[k]; finite &= isfinite(rq[k]); }
+        for (int k = 0; k < 4; ++k) { st.root_quat[sx(st, k, i)] = rq[k]; finite &= isfinite(rq[k]); }
 #pragma unroll
-        for (int k = 0; k < 6; ++k) { st.root_vel[(size_t)k * N + i] = u[k]; finite &= isfinite(u[k]); }
+        for (int k = 0; k < 6; ++k) { st.root_vel[sx(st, k, i)] = u[k]; finite &= isfinite(u[k]); }
     }
     for (int j = 0; j < D; ++j) {
         const float v = w[m.o_u + nr + j];
-        const float qn = st.q[(size_t)j * N + i] + dt * v;
-        st.qd[(size_t)j * N + i] = v;
-        st.q[(size_t)j * N + i] = qn;
+        const float qn = st.q[sx(st, j, i)] + dt * v;
+        st.qd[sx(st, j, i)] = v;
+        st.q[sx(st, j, i)] = qn;
         finite &= isfinite(v) && isfinite(qn);
     }
     if (!finite) st.nan_flag[i] = 1;

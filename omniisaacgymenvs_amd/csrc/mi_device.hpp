@@ -53,23 +53,34 @@ struct DevModel {
         o_rk, o_cp, o_cl;
 };
 
+// Physics state element (field k, env i) lives at k * fs + i * es floats from the field's
+// base pointer. Two layouts (chosen at mi_sim_create):
+//   per-env records (wavefront-per-env kernels): fs = 1, es = record length (a multiple of
+//     32 floats = whole 128-B lines); the wave reads / writes its env's state with one
+//     coalesced access per field group;
+//   field-major SoA (one-lane-per-env kernels): fs = N, es = 1; lane-consecutive envs.
 struct DevState {
     int N;
+    int fs, es;           // field stride, env stride (floats)
     int64_t off;          // global id of env 0 (multi-GPU shard offset)
     uint64_t seed;
     const float* origins; // [3][N]
-    float* root_pos;      // [3][N] world
-    float* root_quat;     // [4][N] wxyz
-    float* root_vel;      // [6][N] lin, ang (world)
-    float* q;             // [D][N]
-    float* qd;            // [D][N]
-    float* eff;           // [D][N]
-    float* sens;          // [S*6][N]
+    float* root_pos;      // 3 fields, world
+    float* root_quat;     // 4 fields, wxyz
+    float* root_vel;      // 6 fields: lin, ang (world)
+    float* q;             // D fields
+    float* qd;            // D fields
+    float* eff;           // D fields
+    float* sens;          // 6 S fields
     uint32_t* reset_count;// [N]
     int32_t* nan_flag;    // [N]
     unsigned long long* nan_total;
     float* ws;            // workspace [N/64][slots][64]
 };
+
+MI_D size_t sx(const DevState& st, int k, int i) {
+    return (size_t)k * (size_t)st.fs + (size_t)i * (size_t)st.es;
+}
 
 struct DevTask {
     int kind, O, A;

@@ -99,10 +99,10 @@ __device__ __forceinline__ void physics_env(const DevModel& m, const DevState& s
                                             int i, int substeps) {
     if (m.dyn == MI_DYN_CARTPOLE) {
         const int N = st.N;
-        float x = st.q[i], th = st.q[N + i], xd = st.qd[i], thd = st.qd[N + i];
-        const float F0 = st.eff[i], F1 = st.eff[N + i];
+        float x = st.q[sx(st, 0, i)], th = st.q[sx(st, 1, i)], xd = st.qd[sx(st, 0, i)], thd = st.qd[sx(st, 1, i)];
+        const float F0 = st.eff[sx(st, 0, i)], F1 = st.eff[sx(st, 1, i)];
         for (int s = 0; s < substeps; ++s) cartpole_substep(m, p, x, th, xd, thd, F0, F1);
-        st.q[i] = x; st.q[N + i] = th; st.qd[i] = xd; st.qd[N + i] = thd;
+        st.q[sx(st, 0, i)] = x; st.q[sx(st, 1, i)] = th; st.qd[sx(st, 0, i)] = xd; st.qd[sx(st, 1, i)] = thd;
         if (!(isfinite(x) && isfinite(th) && isfinite(xd) && isfinite(thd))) st.nan_flag[i] = 1;
     } else {
         for (int s = 0; s < substeps; ++s) artic_substep(m, st, p, i);
@@ -296,7 +296,7 @@ __global__ __launch_bounds__(64) void k_sim_step_wave(const KParams* __restrict_
     stage_model_constants(t, smem);
     for (int s = 0; s < substeps; ++s) {
         const KParams* k = opaque_kp(kp);
-        wave_artic_substep<T>(k->m, k->t, k->st, k->p, i, smem, gW, s == 0);
+        wave_artic_substep<T>(k->m, k->t, k->st, k->p, i, smem, gW, s == 0, s == substeps - 1);
     }
 }
 
@@ -325,7 +325,7 @@ __global__ __launch_bounds__(64) void k_env_step_wave(const KParams* __restrict_
     float* gW = rows + (size_t)i * t.g_row_stride;
     for (int s = 0; s < substeps; ++s) {
         const KParams* k = opaque_kp(kp);
-        wave_artic_substep<T>(k->m, k->t, k->st, k->p, i, smem, gW, s == 0);
+        wave_artic_substep<T>(k->m, k->t, k->st, k->p, i, smem, gW, s == 0, s == substeps - 1);
     }
     // 3. post_physics_step + obs clamp, wave-cooperative from the LDS-resident state
     STAMP_RESET();
@@ -345,27 +345,29 @@ __global__ void k_reset_idx(DevModel m, DevState st, DevTask tp, const int64_t* 
     if (progress_buf) progress_buf[i] = 0;
 }
 
-// SoA [C][N] <-> row-major [N,C] (gather / scatter with optional indices)
-__global__ void k_soa_to_rows(const float* src, int N, int C, float* dst) {
+// state fields (field stride fs, env stride es: DevState) <-> row-major [N,C] torch tensors
+// (gather / scatter with optional indices)
+__global__ void k_soa_to_rows(const float* src, int N, int C, int fs, int es, float* dst) {
     const int i = blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= N) return;
-    for (int c = 0; c < C; ++c) dst[(size_t)i * C + c] = src[(size_t)c * N + i];
+    for (int c = 0; c < C; ++c) dst[(size_t)i * C + c] = src[(size_t)c * fs + (size_t)i * es];
 }
 template <typename IDX>
-__global__ void k_rows_to_soa(const float* src, int n, int C, const IDX* idx, int N, float* dst) {
+__global__ void k_rows_to_soa(const float* src, int n, int C, const IDX* idx, int N, int fs, int es,
+                              float* dst) {
     const int t = blockIdx.x * blockDim.x + threadIdx.x;
     if (t >= n) return;
     const int64_t i = idx ? (int64_t)idx[t] : t;
     if (i < 0 || i >= N) return;
-    for (int c = 0; c < C; ++c) dst[(size_t)c * N + i] = src[(size_t)t * C + c];
+    for (int c = 0; c < C; ++c) dst[(size_t)c * fs + (size_t)i * es] = src[(size_t)t * C + c];
 }
 
 __global__ void k_init_state(DevState st, int D) {
     const int i = blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= st.N) return;
     const int N = st.N;
-    for (int k = 0; k < 3; ++k) st.root_pos[(size_t)k * N + i] = st.origins[(size_t)k * N + i];
-    st.root_quat[i] = 1.0f;
+    for (int k = 0; k < 3; ++k) st.root_pos[sx(st, k, i)] = st.origins[(size_t)k * N + i];
+    st.root_quat[sx(st, 0, i)] = 1.0f;
 }
 
 __global__ void k_fill_uniform(int N, int64_t off, float* out, int cols, uint64_t seed,
@@ -721,6 +723,20 @@ int mi_sim_create(const mi_model_desc* md, const mi_sim_params* prm, int32_t N, 
         // limit here: registers cap the wave path at 2 waves/SIMD = 8 envs/CU = 20 KB each)
         t.j_rows_lds = ct ? std::min(48, m.max_rows) : 0;
         t.s_J = take(ct ? t.j_rows_lds * m.nv : 4);
+        // CT path: W rows for the P9 -> P10 hand-over. First choice: the rest of the dead
+        // span; when that holds fewer rows than a one-bank PGS can use and the LDS budget of
+        // the wave path (8 envs / CU, 20 KB each) has room, a dedicated region instead, so
+        // the global slab is only the fallback of rare row-heavy substeps.
+        t.s_W = ro;
+        t.w_rows_lds = overlay ? std::min(64, (span1 - ro) / m.nv) : 0;
+        {
+            const int want = std::min(64, m.max_rows);
+            const int lds_budget_floats = (160 * 1024 / 8) / (int)sizeof(float);
+            if (ct && t.w_rows_lds < want && so + al4(want * m.nv) <= lds_budget_floats) {
+                t.s_W = take(want * m.nv);
+                t.w_rows_lds = want;
+            }
+        }
         t.s_total = so;
         {   // the sequential regions strictly increase; the row data sits inside the dead
             // span (overlay) or between s_rp and s_xs
@@ -735,9 +751,6 @@ int mi_sim_create(const mi_model_desc* md, const mi_sim_params* prm, int32_t N, 
         }
         t.max_rows = m.max_rows;
         t.g_row_stride = (size_t)m.max_rows * WNV;
-        // CT path: the rest of the dead span holds the first W rows (P9 -> P10 hand-over)
-        t.s_W = ro;
-        t.w_rows_lds = overlay ? std::min(64, (span1 - ro) / m.nv) : 0;
         // P8 self-collision scratch (segments + broad-phase survivors) in the same free span
         t.ngeoms = md->num_geoms;
         t.s_seg = -1; t.s_surv = -1;
@@ -767,9 +780,23 @@ int mi_sim_create(const mi_model_desc* md, const mi_sim_params* prm, int32_t N, 
     const int D = m.D > 0 ? m.D : 1, S = m.S > 0 ? m.S : 1;
     void* p = nullptr;
 #define AL(field, T, cnt) if ((rc = dev_alloc(s, &p, sizeof(T) * (size_t)(cnt)))) return cleanup(rc); st.field = (T*)p
-    AL(root_pos, float, 3 * N); AL(root_quat, float, 4 * N); AL(root_vel, float, 6 * N);
-    AL(q, float, (size_t)D * N); AL(qd, float, (size_t)D * N); AL(eff, float, (size_t)D * N);
-    AL(sens, float, (size_t)6 * S * N); AL(reset_count, uint32_t, N); AL(nan_flag, int32_t, N);
+    if (s->wave) {
+        // one record per env: pos 3, quat 4, vel 6, q D, qd D, eff D, sensors 6S, padded to
+        // whole 128-B lines (the wave touches only its own lines, each access coalesced)
+        const int rec = (13 + 3 * D + 6 * S + 31) & ~31;
+        float* r = nullptr;
+        if ((rc = dev_alloc(s, &p, sizeof(float) * (size_t)rec * N))) return cleanup(rc);
+        r = (float*)p;
+        st.fs = 1; st.es = rec;
+        st.root_pos = r; st.root_quat = r + 3; st.root_vel = r + 7; st.q = r + 13;
+        st.qd = r + 13 + D; st.eff = r + 13 + 2 * D; st.sens = r + 13 + 3 * D;
+    } else {
+        st.fs = N; st.es = 1;
+        AL(root_pos, float, 3 * N); AL(root_quat, float, 4 * N); AL(root_vel, float, 6 * N);
+        AL(q, float, (size_t)D * N); AL(qd, float, (size_t)D * N); AL(eff, float, (size_t)D * N);
+        AL(sens, float, (size_t)6 * S * N);
+    }
+    AL(reset_count, uint32_t, N); AL(nan_flag, int32_t, N);
     AL(nan_total, unsigned long long, 1);
     if (s->wave) {
         if ((rc = dev_alloc(s, &p, sizeof(float) * (size_t)N * s->wt.g_row_stride))) return cleanup(rc);
@@ -823,9 +850,9 @@ int mi_get_root_state(mi_sim* s, float* pos, float* quat, float* vel, void* stre
     NEED(s);
     HIP_TRY(hipSetDevice(s->device));
     const dim3 g = grid_for(s, s->N), b(s->block);
-    if (pos) hipLaunchKernelGGL(k_soa_to_rows, g, b, 0, STREAM(stream), s->ds.root_pos, s->N, 3, pos);
-    if (quat) hipLaunchKernelGGL(k_soa_to_rows, g, b, 0, STREAM(stream), s->ds.root_quat, s->N, 4, quat);
-    if (vel) hipLaunchKernelGGL(k_soa_to_rows, g, b, 0, STREAM(stream), s->ds.root_vel, s->N, 6, vel);
+    if (pos) hipLaunchKernelGGL(k_soa_to_rows, g, b, 0, STREAM(stream), s->ds.root_pos, s->N, 3, s->ds.fs, s->ds.es, pos);
+    if (quat) hipLaunchKernelGGL(k_soa_to_rows, g, b, 0, STREAM(stream), s->ds.root_quat, s->N, 4, s->ds.fs, s->ds.es, quat);
+    if (vel) hipLaunchKernelGGL(k_soa_to_rows, g, b, 0, STREAM(stream), s->ds.root_vel, s->N, 6, s->ds.fs, s->ds.es, vel);
     LAUNCH_CHECK();
     return MI_OK;
 }
@@ -834,8 +861,8 @@ int mi_get_dof_state(mi_sim* s, float* q, float* qd, void* stream) {
     NEED(s);
     HIP_TRY(hipSetDevice(s->device));
     const dim3 g = grid_for(s, s->N), b(s->block);
-    if (q) hipLaunchKernelGGL(k_soa_to_rows, g, b, 0, STREAM(stream), s->ds.q, s->N, s->dm.D, q);
-    if (qd) hipLaunchKernelGGL(k_soa_to_rows, g, b, 0, STREAM(stream), s->ds.qd, s->N, s->dm.D, qd);
+    if (q) hipLaunchKernelGGL(k_soa_to_rows, g, b, 0, STREAM(stream), s->ds.q, s->N, s->dm.D, s->ds.fs, s->ds.es, q);
+    if (qd) hipLaunchKernelGGL(k_soa_to_rows, g, b, 0, STREAM(stream), s->ds.qd, s->N, s->dm.D, s->ds.fs, s->ds.es, qd);
     LAUNCH_CHECK();
     return MI_OK;
 }
@@ -845,7 +872,7 @@ int mi_get_sensor_wrench(mi_sim* s, float* out, void* stream) {
     HIP_TRY(hipSetDevice(s->device));
     if (s->dm.S == 0) return MI_OK;
     hipLaunchKernelGGL(k_soa_to_rows, grid_for(s, s->N), dim3(s->block), 0, STREAM(stream),
-                       s->ds.sens, s->N, 6 * s->dm.S, out);
+                       s->ds.sens, s->N, 6 * s->dm.S, s->ds.fs, s->ds.es, out);
     LAUNCH_CHECK();
     return MI_OK;
 }
@@ -856,7 +883,7 @@ int mi_set_dof_efforts(mi_sim* s, const float* eff, const int32_t* idx, int32_t 
     HIP_TRY(hipSetDevice(s->device));
     if (n == 0) return MI_OK;
     hipLaunchKernelGGL(k_rows_to_soa<int32_t>, grid_for(s, n), dim3(s->block), 0, STREAM(stream),
-                       eff, n, s->dm.D, idx, s->N, s->ds.eff);
+                       eff, n, s->dm.D, idx, s->N, s->ds.fs, s->ds.es, s->ds.eff);
     LAUNCH_CHECK();
     return MI_OK;
 }
@@ -868,8 +895,8 @@ int mi_set_dof_state(mi_sim* s, const float* q, const float* qd, const int64_t* 
     HIP_TRY(hipSetDevice(s->device));
     if (n == 0) return MI_OK;
     const dim3 g = grid_for(s, n), b(s->block);
-    if (q) hipLaunchKernelGGL(k_rows_to_soa<int64_t>, g, b, 0, STREAM(stream), q, n, s->dm.D, idx, s->N, s->ds.q);
-    if (qd) hipLaunchKernelGGL(k_rows_to_soa<int64_t>, g, b, 0, STREAM(stream), qd, n, s->dm.D, idx, s->N, s->ds.qd);
+    if (q) hipLaunchKernelGGL(k_rows_to_soa<int64_t>, g, b, 0, STREAM(stream), q, n, s->dm.D, idx, s->N, s->ds.fs, s->ds.es, s->ds.q);
+    if (qd) hipLaunchKernelGGL(k_rows_to_soa<int64_t>, g, b, 0, STREAM(stream), qd, n, s->dm.D, idx, s->N, s->ds.fs, s->ds.es, s->ds.qd);
     LAUNCH_CHECK();
     return MI_OK;
 }
@@ -881,9 +908,9 @@ int mi_set_root_state(mi_sim* s, const float* pos, const float* quat, const floa
     HIP_TRY(hipSetDevice(s->device));
     if (n == 0) return MI_OK;
     const dim3 g = grid_for(s, n), b(s->block);
-    if (pos) hipLaunchKernelGGL(k_rows_to_soa<int64_t>, g, b, 0, STREAM(stream), pos, n, 3, idx, s->N, s->ds.root_pos);
-    if (quat) hipLaunchKernelGGL(k_rows_to_soa<int64_t>, g, b, 0, STREAM(stream), quat, n, 4, idx, s->N, s->ds.root_quat);
-    if (vel) hipLaunchKernelGGL(k_rows_to_soa<int64_t>, g, b, 0, STREAM(stream), vel, n, 6, idx, s->N, s->ds.root_vel);
+    if (pos) hipLaunchKernelGGL(k_rows_to_soa<int64_t>, g, b, 0, STREAM(stream), pos, n, 3, idx, s->N, s->ds.fs, s->ds.es, s->ds.root_pos);
+    if (quat) hipLaunchKernelGGL(k_rows_to_soa<int64_t>, g, b, 0, STREAM(stream), quat, n, 4, idx, s->N, s->ds.fs, s->ds.es, s->ds.root_quat);
+    if (vel) hipLaunchKernelGGL(k_rows_to_soa<int64_t>, g, b, 0, STREAM(stream), vel, n, 6, idx, s->N, s->ds.fs, s->ds.es, s->ds.root_vel);
     LAUNCH_CHECK();
     return MI_OK;
 }

@@ -90,10 +90,10 @@ MI_D void task_reset_env(const DevModel& m, const DevState& st, const DevTask& t
     if (tp.kind == MI_TASK_CARTPOLE) {
         float u[4];
         uniform4(st.seed, gid, cnt, 0, 0, u);
-        st.q[i] = 1.0f * (1.0f - 2.0f * u[0]);
-        st.q[N + i] = 0.39269908169872414f * (1.0f - 2.0f * u[1]);
-        st.qd[i] = 0.5f * (1.0f - 2.0f * u[2]);
-        st.qd[N + i] = 0.7853981633974483f * (1.0f - 2.0f * u[3]);
+        st.q[sx(st, 0, i)] = 1.0f * (1.0f - 2.0f * u[0]);
+        st.q[sx(st, 1, i)] = 0.39269908169872414f * (1.0f - 2.0f * u[1]);
+        st.qd[sx(st, 0, i)] = 0.5f * (1.0f - 2.0f * u[2]);
+        st.qd[sx(st, 1, i)] = 0.7853981633974483f * (1.0f - 2.0f * u[3]);
     } else {
         const float pn = tp.dof_pos_noise, vn = tp.dof_vel_noise;
         const float pw = (float)((double)pn - (double)(-pn));
@@ -104,23 +104,23 @@ MI_D void task_reset_env(const DevModel& m, const DevState& st, const DevTask& t
             float v = tp.init_dof[j] + (pw * u[j & 3] + (-pn));
             const float lo = m.lower[j + 1], hi = m.upper[j + 1];
             if (lo < hi) { v = v < hi ? v : hi; v = v > lo ? v : lo; }
-            st.q[(size_t)j * N + i] = v;
+            st.q[sx(st, j, i)] = v;
         }
         for (int j = 0; j < D; ++j) {
             const int s = D + j;
             if (j == 0 || (s & 3) == 0) uniform4(st.seed, gid, cnt, (uint32_t)(s >> 2), 0, u);
-            st.qd[(size_t)j * N + i] = vw * u[s & 3] + (-vn);
+            st.qd[sx(st, j, i)] = vw * u[s & 3] + (-vn);
         }
         float rp[3];
 #pragma unroll
         for (int k = 0; k < 3; ++k) {
             rp[k] = st.origins[(size_t)k * N + i] + tp.init_root_pos[k];
-            st.root_pos[(size_t)k * N + i] = rp[k];
+            st.root_pos[sx(st, k, i)] = rp[k];
         }
 #pragma unroll
-        for (int k = 0; k < 4; ++k) st.root_quat[(size_t)k * N + i] = tp.init_root_quat[k];
+        for (int k = 0; k < 4; ++k) st.root_quat[sx(st, k, i)] = tp.init_root_quat[k];
 #pragma unroll
-        for (int k = 0; k < 6; ++k) st.root_vel[(size_t)k * N + i] = 0.0f;
+        for (int k = 0; k < 6; ++k) st.root_vel[sx(st, k, i)] = 0.0f;
         float tx = tp.target[0] - rp[0], ty = tp.target[1] - rp[1];
         float pot = -sqrtf(tx * tx + ty * ty + 0.0f * 0.0f) / tp.task_dt;
         if (prev_potentials) prev_potentials[i] = pot;
@@ -145,14 +145,14 @@ MI_D void task_pre_env(const DevModel& m, const DevState& st, const DevTask& tp,
         float a = actions[(size_t)A * i];
         if (clamp_actions) a = clampf(a, -tp.clip_actions, tp.clip_actions);
         if (actions_out) actions_out[(size_t)A * i] = a;
-        st.eff[i] = tp.max_push_effort * a;
-        st.eff[N + i] = 0.0f;
+        st.eff[sx(st, 0, i)] = tp.max_push_effort * a;
+        st.eff[sx(st, 1, i)] = 0.0f;
     } else {
         for (int j = 0; j < A; ++j) {
             float a = actions[(size_t)A * i + j];
             if (clamp_actions) a = clampf(a, -tp.clip_actions, tp.clip_actions);
             if (actions_out) actions_out[(size_t)A * i + j] = a;
-            st.eff[(size_t)j * N + i] = a * tp.gears[j] * tp.power_scale;
+            st.eff[sx(st, j, i)] = a * tp.gears[j] * tp.power_scale;
         }
     }
 }
@@ -168,11 +168,11 @@ MI_D void loco_obs_env(const DevModel& m, const DevState& st, const DevTask& tp,
     const int N = st.N, D = m.D, S = m.S;
     float rp[3], rq[4], rv[6];
 #pragma unroll
-    for (int k = 0; k < 3; ++k) rp[k] = st.root_pos[(size_t)k * N + i];
+    for (int k = 0; k < 3; ++k) rp[k] = st.root_pos[sx(st, k, i)];
 #pragma unroll
-    for (int k = 0; k < 4; ++k) rq[k] = st.root_quat[(size_t)k * N + i];
+    for (int k = 0; k < 4; ++k) rq[k] = st.root_quat[sx(st, k, i)];
 #pragma unroll
-    for (int k = 0; k < 6; ++k) rv[k] = st.root_vel[(size_t)k * N + i];
+    for (int k = 0; k < 6; ++k) rv[k] = st.root_vel[sx(st, k, i)];
     float tt[3] = {tp.target[0] - rp[0], tp.target[1] - rp[1], tp.target[2] - rp[2]};
     tt[2] = 0.0f;
     const float prev_p = potentials[i];
@@ -209,12 +209,12 @@ MI_D void loco_obs_env(const DevModel& m, const DevState& st, const DevTask& tp,
     orow[10] = up[2];
     orow[11] = heading_proj;
     for (int j = 0; j < D; ++j) {
-        orow[12 + j] = ref_unscale(st.q[(size_t)j * N + i], m.lower[j + 1], m.upper[j + 1]);
-        orow[12 + D + j] = st.qd[(size_t)j * N + i] * tp.dof_vel_scale;
+        orow[12 + j] = ref_unscale(st.q[sx(st, j, i)], m.lower[j + 1], m.upper[j + 1]);
+        orow[12 + D + j] = st.qd[sx(st, j, i)] * tp.dof_vel_scale;
         orow[12 + 2 * D + 6 * S + j] = clampf(act[j], -act_clip, act_clip);
     }
     for (int k = 0; k < 6 * S; ++k)
-        orow[12 + 2 * D + k] = st.sens[(size_t)k * N + i] * tp.contact_force_scale;
+        orow[12 + 2 * D + k] = st.sens[sx(st, k, i)] * tp.contact_force_scale;
     potentials[i] = new_p;
     prev_potentials[i] = prev_p;
 }
@@ -268,10 +268,10 @@ MI_D int64_t nan_guard(const DevState& st, int i, int64_t done) {
 // cartpole.py:80-99
 MI_D void cartpole_obs_env(const DevState& st, int i, float* orow) {
     const int N = st.N;
-    orow[0] = st.q[i];
-    orow[1] = st.qd[i];
-    orow[2] = st.q[N + i];
-    orow[3] = st.qd[N + i];
+    orow[0] = st.q[sx(st, 0, i)];
+    orow[1] = st.qd[sx(st, 0, i)];
+    orow[2] = st.q[sx(st, 1, i)];
+    orow[3] = st.qd[sx(st, 1, i)];
 }
 // cartpole.py:143-153
 MI_D float cartpole_reward(const DevTask& tp, const float* o) {

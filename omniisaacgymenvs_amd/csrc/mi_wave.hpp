@@ -57,6 +57,10 @@ __device__ unsigned long long g_phase[MI_STAMP_SLOTS][32];
     do {                                                                                  \
         if (threadIdx.x == 0) g_phase[blockIdx.x % MI_STAMP_SLOTS][31] += 1ull;           \
     } while (0)
+#define STAT(id, v)                                                                       \
+    do {                                                                                  \
+        if (threadIdx.x == 0) g_phase[blockIdx.x % MI_STAMP_SLOTS][id] += (unsigned long long)(v); \
+    } while (0)
 #define STAMP_RESET()                                                                     \
     do {                                                                                  \
         __builtin_amdgcn_sched_barrier(0);                                                \
@@ -64,6 +68,7 @@ __device__ unsigned long long g_phase[MI_STAMP_SLOTS][32];
         __builtin_amdgcn_sched_barrier(0);                                                \
     } while (0)
 #else
+#define STAT(id, v) do { } while (0)
 #define STAMP_RESET() do { } while (0)
 #define STAMP_BEGIN() do { } while (0)
 #define STAMP(id) do { } while (0)
@@ -522,9 +527,12 @@ MI_D void wave_link_forward(const MC& mc, int nr, const WaveTabs& t, float* sm, 
 
 // One articulated substep of env i, executed by the whole 64-lane workgroup.
 // sm: this env's LDS region; gW: this env's global slab of W rows [max_rows][WNV].
+// load_state: read the env's state record from HBM (first substep of a launch; later ones
+// continue from LDS); store_state: write the state and sensor wrenches back (last substep).
 template <class TP>
 MI_D void wave_artic_substep(const DevModel& m, const WaveTabs& t, const DevState& st,
-                             const SimP& p, int i, float* sm, float* gW, bool load_state) {
+                             const SimP& p, int i, float* sm, float* gW, bool load_state,
+                             bool store_state) {
     const int lane = threadIdx.x;
     const int N = st.N, L = m.L, D = m.D, nv = m.nv, nr = m.nr;
     const float dt = p.dt;
@@ -539,11 +547,11 @@ MI_D void wave_artic_substep(const DevModel& m, const WaveTabs& t, const DevStat
     // ---- load state into LDS (later substeps of a launch start from the state the previous
     // substep's P11 left in LDS)
     if (load_state) {
-        if (lane < 3) sm[t.s_rp + lane] = st.root_pos[(size_t)lane * N + i];
-        if (lane < 4) sm[t.s_rp + 4 + lane] = st.root_quat[(size_t)lane * N + i];
-        if (lane < nr) us[lane] = st.root_vel[(size_t)lane * N + i];
-        else if (lane < nv) us[lane] = st.qd[(size_t)(lane - nr) * N + i];
-        if (lane < D) sm[t.s_q + lane] = st.q[(size_t)lane * N + i];
+        if (lane < 3) sm[t.s_rp + lane] = st.root_pos[sx(st, lane, i)];
+        if (lane < 4) sm[t.s_rp + 4 + lane] = st.root_quat[sx(st, lane, i)];
+        if (lane < nr) us[lane] = st.root_vel[sx(st, lane, i)];
+        else if (lane < nv) us[lane] = st.qd[sx(st, lane - nr, i)];
+        if (lane < D) sm[t.s_q + lane] = st.q[sx(st, lane, i)];
     }
     if (nr && lane < 6) {
         float s[6] = {0, 0, 0, 0, 0, 0};
@@ -603,7 +611,7 @@ MI_D void wave_artic_substep(const DevModel& m, const WaveTabs& t, const DevStat
         if (k >= nr) {
             const float damp = mc.lf(MC_DAMP, l);
             diag += mc.lf(MC_ARM, l) + dt * damp;
-            r += st.eff[(size_t)(k - nr) * N + i] - damp * us[k];
+            r += st.eff[sx(st, k - nr, i)] - damp * us[k];
         }
         Mx[k * nv + k] = diag;
         rhs[k] = r;
@@ -1033,6 +1041,12 @@ MI_D void wave_artic_substep(const DevModel& m, const WaveTabs& t, const DevStat
     __syncthreads();
 
     STAMP(10);  // P9 row filing + trailing barrier
+    STAT(15, nrows);
+    STAT(16, nrows > t.w_rows_lds);
+    STAT(17, nrows > 64);
+    STAT(18, total > 64);
+    STAT(19, nrows > t.j_rows_lds);
+    STAT(20, ncon);
     // ---- P10: projected Gauss-Seidel. Lane k (mod 32) owns dof k; the wave's lower half
     // holds J / W of rows 0..63 in registers, the upper half rows 64..127. Rows are swept in
     // order; only the half owning the current row is active and u is copied across halves
@@ -1223,10 +1237,8 @@ MI_D void wave_artic_substep(const DevModel& m, const WaveTabs& t, const DevStat
         m3_tvec(R, T, Tl);
 #pragma unroll
         for (int q = 0; q < 3; ++q) {
-            st.sens[(size_t)(6 * si + q) * N + i] = Fl[q];
-            st.sens[(size_t)(6 * si + 3 + q) * N + i] = Tl[q];
-            sm[t.s_rb + 6 * si + q] = Fl[q];         // LDS copy for the post-step (rb is
-            sm[t.s_rb + 6 * si + 3 + q] = Tl[q];     // dead after the PGS)
+            sm[t.s_rb + 6 * si + q] = Fl[q];         // LDS copy for the post-step and the
+            sm[t.s_rb + 6 * si + 3 + q] = Tl[q];     // write-back (rb is dead after the PGS)
         }
     }
     // ---- P11b: integrate; non-finite -> nan flag
@@ -1234,11 +1246,14 @@ MI_D void wave_artic_substep(const DevModel& m, const WaveTabs& t, const DevStat
     if (lane < D) {
         const float v = us[nr + lane];
         const float qn = sm[t.s_q + lane] + dt * v;
-        st.qd[(size_t)lane * N + i] = v;
-        st.q[(size_t)lane * N + i] = qn;
+        if (store_state) {
+            st.qd[sx(st, lane, i)] = v;
+            st.q[sx(st, lane, i)] = qn;
+        }
         sm[t.s_q + lane] = qn;                       // final state stays in LDS (post-step)
         finite = isfinite(v) && isfinite(qn);
     }
+    if (store_state && lane < 6 * m.S) st.sens[sx(st, lane, i)] = sm[t.s_rb + lane];
     if (nr && lane == 0) {
         float u6[6], rp[3], rq[4];
 #pragma unroll
@@ -1278,11 +1293,18 @@ MI_D void wave_artic_substep(const DevModel& m, const WaveTabs& t, const DevStat
 #pragma unroll
         for (int k = 0; k < 6; ++k) us[k] = u6[k];
 #pragma unroll
-        for (int k = 0; k < 3; ++k) { st.root_pos[(size_t)k * N + i] = rp[k]; finite &= isfinite(rp[k]); }
+        for (int k = 0; k < 3; ++k) finite &= isfinite(rp[k]);
 #pragma unroll
-        for (int k = 0; k < 4; ++k) { st.root_quat[(size_t)k * N + i] = rq[k]; finite &= isfinite(rq[k]); }
+        for (int k = 0; k < 4; ++k) finite &= isfinite(rq[k]);
 #pragma unroll
-        for (int k = 0; k < 6; ++k) { st.root_vel[(size_t)k * N + i] = u6[k]; finite &= isfinite(u6[k]); }
+        for (int k = 0; k < 6; ++k) finite &= isfinite(u6[k]);
+    }
+    // root write-back from LDS, one field per lane (LDS operations of the wave complete in
+    // order: lane 0's writes above are visible)
+    if (nr && store_state) {
+        if (lane < 3) st.root_pos[sx(st, lane, i)] = sm[t.s_rp + lane];
+        else if (lane < 7) st.root_quat[sx(st, lane - 3, i)] = sm[t.s_rp + 4 + lane - 3];
+        else if (lane < 13) st.root_vel[sx(st, lane - 7, i)] = us[lane - 7];
     }
     if (__any(!finite) && lane == 0) st.nan_flag[i] = 1;
     __syncthreads();
@@ -1316,17 +1338,17 @@ MI_D void wave_task_pre(const DevModel& m, const WaveTabs& t, const DevState& st
             float v = tp.init_dof[j] + (pw * u[j & 3] + (-pn));
             const float lo = m.lower[j + 1], hi = m.upper[j + 1];
             if (lo < hi) { v = v < hi ? v : hi; v = v > lo ? v : lo; }
-            st.q[(size_t)j * N + i] = v;
+            st.q[sx(st, j, i)] = v;
             const int s = D + j;
             uniform4(st.seed, gid, cnt, (uint32_t)(s >> 2), 0, u);
-            st.qd[(size_t)j * N + i] = vw * u[s & 3] + (-vn);
+            st.qd[sx(st, j, i)] = vw * u[s & 3] + (-vn);
         }
         if (lane < 3) {
             const float rp = st.origins[(size_t)lane * N + i] + tp.init_root_pos[lane];
-            st.root_pos[(size_t)lane * N + i] = rp;
+            st.root_pos[sx(st, lane, i)] = rp;
         }
-        if (lane < 4) st.root_quat[(size_t)lane * N + i] = tp.init_root_quat[lane];
-        if (lane < 6) st.root_vel[(size_t)lane * N + i] = 0.0f;
+        if (lane < 4) st.root_quat[sx(st, lane, i)] = tp.init_root_quat[lane];
+        if (lane < 6) st.root_vel[sx(st, lane, i)] = 0.0f;
         if (lane == 0) {
             float rp[3];
 #pragma unroll
@@ -1344,7 +1366,7 @@ MI_D void wave_task_pre(const DevModel& m, const WaveTabs& t, const DevState& st
         const int j = lane;
         float a = clampf(actions[(size_t)A * i + j], -tp.clip_actions, tp.clip_actions);
         if (actions_out) actions_out[(size_t)A * i + j] = a;
-        st.eff[(size_t)j * N + i] = a * tp.gears[j] * tp.power_scale;
+        st.eff[sx(st, j, i)] = a * tp.gears[j] * tp.power_scale;
     }
 }
 

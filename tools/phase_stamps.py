@@ -51,6 +51,10 @@ def main():
     for k, v in per.items():
         print(f"{k:26s} {v:9.0f}  {100.0 * v / tot:5.1f}%")
     print(f"{'total (1 env-substep)':26s} {tot:9.0f}")
+    stats = {"mean rows": buf[15] / cnt, "frac rows > LDS W rows": buf[16] / cnt,
+             "frac rows > 64": buf[17] / cnt, "frac solve vectors > 64": buf[18] / cnt,
+             "frac rows > LDS J rows": buf[19] / cnt, "mean contacts": buf[20] / cnt}
+    print(json.dumps({"row_stats_per_env_substep": {k: round(v, 4) for k, v in stats.items()}}))
 
 
 if __name__ == "__main__":
