@@ -1,0 +1,58 @@
+/*
+ * mi_rl.h — C ABI of libmi_rl.so: the fused elementwise ops of the PPO learner that drives
+ * the hot path (the caller of VecEnvRLGames.step).
+ *
+ * The reference trains with rl-games 1.5.2 (setup.py:17; not vendored under /root/reference,
+ * absent from this image). Its call sites are scripts/rlgames_train.py:67-84 (Runner over the
+ * 'rlgpu' env) and the hyper-parameters in cfg/train/{Humanoid,Ant,Cartpole}PPO.yaml. The two
+ * per-sample loops of its a2c_continuous agent that are not GEMMs are fused here:
+ *   mi_rl_gae          — rl_games common/a2c_common.py discount_values (GAE(gamma, tau)
+ *                        over the horizon, returns = advantages + values)
+ *   mi_rl_sample_gauss — rl_games algos_torch/models.py ModelA2CContinuousLogStd forward in
+ *                        eval mode: action ~ Normal(mu, exp(logstd)) and its neg-log-prob
+ * The MLP GEMMs stay in hipBLASLt (torch.nn.Linear).
+ *
+ * Conventions: as mi_sim.h — 0 on success or a negative MI_E_* code (mi_rl_last_error());
+ * device pointers; `stream` is a hipStream_t passed as void*; stream-ordered, non-blocking.
+ */
+#ifndef MI_RL_H
+#define MI_RL_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define MI_RL_ABI_VERSION 1
+
+int32_t mi_rl_abi_version(void);
+const char* mi_rl_last_error(void);
+
+/* GAE over a rollout stored time-major [H][N] (rl_games experience buffer layout).
+ * dones[t][n] = episode-end flag BEFORE step t (rl_games stores self.dones before env.step);
+ * last_values / last_dones: bootstrap value and done flags after the last step.
+ *   delta_t = r_t + gamma * v_{t+1} * (1 - d_{t+1}) - v_t
+ *   A_t     = delta_t + gamma * tau * (1 - d_{t+1}) * A_{t+1}
+ * Writes advantages [H][N] and returns = advantages + values [H][N] (either may be NULL). */
+int32_t mi_rl_gae(const float* rewards, const float* values, const float* dones,
+                  const float* last_values, const float* last_dones, int32_t horizon,
+                  int32_t num_envs, float gamma, float tau, float* advantages, float* returns,
+                  void* stream);
+
+/* actions[n][j] = mu[n][j] + exp(logstd[n * logstd_stride + j]) * z, z ~ N(0, 1) from the
+ * counter-based Philox4x32-10 stream keyed (seed, counter, row n, j) — Box-Muller on pairs of
+ * uniforms; neglogp[n] = 0.5 sum_j ((a - mu) / sigma)^2 + 0.5 log(2 pi) A + sum_j logstd,
+ * exactly rl_games' ModelA2CContinuousLogStd.neglogp on the sampled action.
+ * logstd_stride = 0 broadcasts one [A] row (fixed_sigma), = A for per-row sigmas.
+ * counter = *counter_base + counter_offset when counter_base (a device int64) is given, so a
+ * captured HIP graph draws fresh noise on every replay once the base is advanced on device. */
+int32_t mi_rl_sample_gauss(const float* mu, const float* logstd, int32_t logstd_stride,
+                           int32_t num_rows, int32_t num_actions, uint64_t seed,
+                           const int64_t* counter_base, uint64_t counter_offset, float* actions,
+                           float* neglogp, void* stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* MI_RL_H */

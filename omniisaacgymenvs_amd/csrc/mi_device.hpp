@@ -1,8 +1,9 @@
 // mi_device.hpp — device-side building blocks of libmi_sim.so (gfx950).
 //
-// Layout (DESIGN.md §Data layout):
-//   * physics state is struct-of-arrays [field][N] in HBM: lane i of a wave touches element
-//     i of every field, so every state access is a coalesced 256-B wave transaction;
+// Layout:
+//   * physics state (DevState): per-env records for the wavefront-per-env kernels (a wave
+//     reads / writes its env's fields in whole 128-B lines), field-major SoA [field][N] for
+//     the one-lane-per-env kernels (lane i touches element i of every field: coalesced);
 //   * the per-env solver workspace is [env/64][slot][64] — a wave's workspace is one
 //     contiguous slab and every slot access is one coalesced 256-B line;
 //   * the model (link tree, inertias, geoms) is shared by all envs and read through

@@ -1,0 +1,468 @@
+"""PPO agent with the semantics of rl-games 1.5.2 ``a2c_continuous`` (setup.py:17; the library
+is neither vendored nor installable here), driving the hot path through the IVecEnv contract
+(``RLGPUEnv``, utils/rlgames/rlgames_utils.py:94-118) the way scripts/rlgames_train.py:67-84
+does. Hyper-parameters come from cfg/train/<Task>PPO.yaml ``params.config``.
+
+What is restated from rl-games (per epoch):
+  play_steps    horizon_length env steps under the eval-mode policy; the experience buffer
+                holds obs, dones-before-step, actions, neglogp, values (un-normalised), mus,
+                sigmas and shaped rewards (reward_shaper.scale_value); per-env episode return /
+                length meters (games_to_track = 100).
+  GAE           discount_values(gamma, tau); returns = advantages + values.
+  prepare       swap_and_flatten01 (actor-major batch), value normalisation of values and
+                returns (value RunningMeanStd in train mode, values first), advantage
+                normalisation over the batch.
+  train         mini_epochs x (batch / minibatch_size) contiguous minibatches (no shuffling),
+                clipped surrogate + clipped value loss (x 0.5 critic_coef) + bound loss
+                (soft bound 1.1) - entropy_coef x entropy; Adam(eps 1e-8), fp16 autocast +
+                GradScaler when mixed_precision, grad-norm clip; the mu/sigma of each minibatch
+                written back for the next mini-epoch's KL; the legacy adaptive LR schedule
+                after every minibatch (KL > 2 thr: lr / 1.5; KL < thr / 2: lr x 1.5; clamped to
+                [1e-6, 1e-2]); obs statistics updated during the first mini-epoch only.
+
+MI355X-first execution:
+  * GAE and action sampling are single HIP launches (libmi_rl.so, include/mi_rl.h);
+  * the whole rollout — horizon x (policy GEMMs, sampling, mi_env_step, buffer writes, meter
+    sums) — is captured once into a HIP graph and replayed every epoch, so a rollout costs one
+    graph launch instead of ~30 launches per env step; episode meters are accumulated on
+    device as per-step (count, sum) pairs and folded into the host meters with one copy per
+    epoch (no nonzero() host syncs in the loop);
+  * on CPU (BASELINE config 0) the same code runs eagerly with the torch statements of
+    those ops.
+"""
+from __future__ import annotations
+
+import math
+import os
+import time
+from typing import Dict, Optional
+
+import numpy as np
+import torch
+import torch.nn as nn
+
+from . import ops
+from .models import ModelA2CContinuousLogStd
+
+
+def _f(x) -> float:
+    return float(x)
+
+
+class AverageMeter:
+    """rl_games torch_ext.AverageMeter: mean over the last max_size values, updated with
+    batches (size, mean)."""
+
+    def __init__(self, max_size: int = 100) -> None:
+        self.max_size = max_size
+        self.current_size = 0
+        self.mean = 0.0
+
+    def update_moments(self, size: int, mean: float) -> None:
+        if size <= 0:
+            return
+        size = int(np.clip(size, 0, self.max_size))
+        old_size = min(self.max_size - size, self.current_size)
+        size_sum = old_size + size
+        self.current_size = size_sum
+        self.mean = (self.mean * old_size + mean * size) / size_sum
+
+    def clear(self) -> None:
+        self.current_size = 0
+        self.mean = 0.0
+
+    def get_mean(self) -> float:
+        return self.mean
+
+
+class AdaptiveScheduler:
+    def __init__(self, kl_threshold: float = 0.008, min_lr: float = 1e-6, max_lr: float = 1e-2) -> None:
+        self.kl_threshold, self.min_lr, self.max_lr = kl_threshold, min_lr, max_lr
+
+    def update(self, lr: float, kl: float) -> float:
+        if kl > 2.0 * self.kl_threshold:
+            lr = max(lr / 1.5, self.min_lr)
+        if kl < 0.5 * self.kl_threshold:
+            lr = min(lr * 1.5, self.max_lr)
+        return lr
+
+
+def policy_kl(p0_mu, p0_sigma, p1_mu, p1_sigma):
+    """rl_games torch_ext.policy_kl, reduced (mean over rows of the per-row sum)."""
+    c1 = torch.log(p1_sigma / p0_sigma + 1e-5)
+    c2 = (p0_sigma ** 2 + (p1_mu - p0_mu) ** 2) / (2.0 * (p1_sigma ** 2 + 1e-5))
+    return (c1 + c2 - 0.5).sum(dim=-1).mean()
+
+
+def swap_and_flatten01(x: torch.Tensor) -> torch.Tensor:
+    """[H, N, ...] -> [N * H, ...] (actor-major), rl_games a2c_common.swap_and_flatten01."""
+    s = x.shape
+    return x.transpose(0, 1).reshape(s[0] * s[1], *s[2:])
+
+
+class A2CAgent:
+    """rl_games a2c_continuous.A2CAgent over an IVecEnv."""
+
+    def __init__(self, env, params: Dict, run_dir: Optional[str] = None) -> None:
+        cfg = params["config"]
+        self.env = env
+        self.cfg = cfg
+        self.params = params
+        self.device = torch.device(cfg.get("device", "cuda:0"))
+        info = env.get_env_info()
+        self.num_obs = int(np.prod(info["observation_space"].shape))
+        self.num_actions = int(np.prod(info["action_space"].shape))
+        self.actions_low = torch.as_tensor(np.asarray(info["action_space"].low, np.float32), device=self.device)
+        self.actions_high = torch.as_tensor(np.asarray(info["action_space"].high, np.float32), device=self.device)
+        self.num_actors = int(cfg["num_actors"])
+        self.horizon = int(cfg["horizon_length"])
+        self.batch_size = self.horizon * self.num_actors
+        self.minibatch_size = int(cfg["minibatch_size"])
+        if self.batch_size % self.minibatch_size != 0:
+            raise ValueError(f"minibatch_size {self.minibatch_size} must divide horizon x actors = "
+                             f"{self.batch_size} (docs/troubleshoot.md:44)")
+        self.num_minibatches = self.batch_size // self.minibatch_size
+        self.mini_epochs = int(cfg["mini_epochs"])
+        self.gamma, self.tau = _f(cfg["gamma"]), _f(cfg["tau"])
+        self.e_clip = _f(cfg["e_clip"])
+        self.clip_value = bool(cfg.get("clip_value", False))
+        self.critic_coef = _f(cfg["critic_coef"])
+        self.entropy_coef = _f(cfg.get("entropy_coef", 0.0))
+        self.bounds_loss_coef = cfg.get("bounds_loss_coef", None)
+        self.grad_norm = _f(cfg.get("grad_norm", 1.0))
+        self.truncate_grads = bool(cfg.get("truncate_grads", False))
+        self.normalize_advantage = bool(cfg.get("normalize_advantage", True))
+        self.normalize_value = bool(cfg.get("normalize_value", False))
+        self.normalize_input = bool(cfg.get("normalize_input", False))
+        self.value_bootstrap = bool(cfg.get("value_bootstrap", False))
+        self.reward_scale = _f(cfg.get("reward_shaper", {}).get("scale_value", 1.0))
+        self.last_lr = _f(cfg["learning_rate"])
+        self.lr_schedule = cfg.get("lr_schedule", None)
+        self.scheduler = AdaptiveScheduler(_f(cfg.get("kl_threshold", 0.008))) if self.lr_schedule == "adaptive" else None
+        self.max_epochs = int(cfg.get("max_epochs", 1000))
+        self.save_best_after = int(cfg.get("save_best_after", 100))
+        self.save_frequency = int(cfg.get("save_frequency", 0))
+        self.score_to_win = _f(cfg.get("score_to_win", math.inf))
+        self.mixed_precision = bool(cfg.get("mixed_precision", False)) and self.device.type == "cuda"
+        self.name = cfg.get("name", "run")
+        self.run_dir = run_dir or os.path.join("runs", str(self.name))
+        self.seed = int(params.get("seed", 42))
+
+        torch.manual_seed(self.seed)
+        self.model = ModelA2CContinuousLogStd(self.num_obs, self.num_actions, params["network"],
+                                              self.normalize_input, self.normalize_value).to(self.device)
+        self.optimizer = torch.optim.Adam(self.model.parameters(), lr=self.last_lr, eps=1e-08,
+                                          weight_decay=float(cfg.get("weight_decay", 0.0)))
+        self.scaler = torch.amp.GradScaler("cuda", enabled=self.mixed_precision)
+        self.sample_gen = torch.Generator(device="cpu").manual_seed(self.seed)
+        self.sample_seed = (self.seed * 0x9E3779B97F4A7C15 + 1) & ((1 << 64) - 1)
+
+        H, N, O, A = self.horizon, self.num_actors, self.num_obs, self.num_actions
+        dev, f32 = self.device, torch.float32
+        self.buf = {
+            "obses": torch.zeros((H, N, O), device=dev, dtype=f32),
+            "dones": torch.zeros((H, N), device=dev, dtype=f32),
+            "actions": torch.zeros((H, N, A), device=dev, dtype=f32),
+            "neglogpacs": torch.zeros((H, N), device=dev, dtype=f32),
+            "values": torch.zeros((H, N), device=dev, dtype=f32),
+            "mus": torch.zeros((H, N, A), device=dev, dtype=f32),
+            "sigmas": torch.zeros((H, N, A), device=dev, dtype=f32),
+            "rewards": torch.zeros((H, N), device=dev, dtype=f32),
+        }
+        self.obs = torch.zeros((N, O), device=dev, dtype=f32)      # static rollout input
+        self.dones = torch.zeros((N,), device=dev, dtype=f32)
+        self.last_values = torch.zeros((N,), device=dev, dtype=f32)
+        self.current_rewards = torch.zeros((N,), device=dev, dtype=f32)
+        self.current_lengths = torch.zeros((N,), device=dev, dtype=f32)
+        self.episode_sums = torch.zeros((H, 3), device=dev, dtype=torch.float64)  # count, rew, len
+        self.rng_counter = torch.zeros((1,), device=dev, dtype=torch.int64)
+        self.game_rewards = AverageMeter(int(cfg.get("games_to_track", 100)))
+        self.game_lengths = AverageMeter(int(cfg.get("games_to_track", 100)))
+        self.use_graph = self.device.type == "cuda" and bool(cfg.get("graph_rollout", True))
+        self.graph: Optional[torch.cuda.CUDAGraph] = None
+        self.epoch_num = 0
+        self.frame = 0
+        self.last_mean_rewards = -100500.0
+        self.stats: Dict[str, float] = {}
+
+    # ------------------------------------------------------------------ env plumbing
+    def _obs_tensor(self, obs) -> torch.Tensor:
+        o = obs["obs"] if isinstance(obs, dict) else obs
+        return o.to(self.device, dtype=torch.float32)
+
+    def env_reset(self) -> None:
+        self.obs.copy_(self._obs_tensor(self.env.reset()))
+
+    def preprocess_actions(self, actions: torch.Tensor) -> torch.Tensor:
+        """clip_actions: clamp to [-1, 1] then rescale to the action space."""
+        a = torch.clamp(actions, -1.0, 1.0)
+        return self.actions_low + (a + 1.0) * 0.5 * (self.actions_high - self.actions_low)
+
+    # ------------------------------------------------------------------ rollout
+    def _policy_step(self, obs: torch.Tensor, n: int):
+        """Eval-mode policy on raw obs: actions, neglogp, un-normalised values, mu, sigma."""
+        mu, logstd, value = self.model.policy(obs)
+        mu = mu.float()
+        logstd = logstd.float()
+        if self.device.type == "cuda":
+            act, nlp = ops.sample_gauss(mu, self.model.a2c_network.sigma.detach().float()
+                                        if self.model.a2c_network.fixed_sigma else logstd,
+                                        self.sample_seed, self.rng_counter, n)
+        else:
+            act, nlp = ops.sample_gauss(mu, logstd, 0, generator=self.sample_gen)
+        values = self.model.unnorm_value(value.float()).squeeze(-1)
+        return act, nlp, values, mu, torch.exp(logstd)
+
+    def _rollout_body(self) -> None:
+        """horizon env steps; everything stays on the device (graph-capturable)."""
+        b = self.buf
+        for n in range(self.horizon):
+            act, nlp, values, mu, sigma = self._policy_step(self.obs, n)
+            b["obses"][n].copy_(self.obs)
+            b["dones"][n].copy_(self.dones)
+            b["actions"][n].copy_(act)
+            b["neglogpacs"][n].copy_(nlp)
+            b["values"][n].copy_(values)
+            b["mus"][n].copy_(mu)
+            b["sigmas"][n].copy_(sigma)
+            obs, rewards, dones, infos = self.env.step(self.preprocess_actions(act))
+            rewards = rewards.to(self.device, dtype=torch.float32).view(-1)
+            shaped = rewards * self.reward_scale
+            if self.value_bootstrap and isinstance(infos, dict) and "time_outs" in infos:
+                shaped = shaped + self.gamma * values * infos["time_outs"].to(self.device).float()
+            b["rewards"][n].copy_(shaped)
+            self.obs.copy_(self._obs_tensor(obs))
+            self.dones.copy_(dones.to(self.device).view(-1).float())
+            self.current_rewards.add_(rewards)
+            self.current_lengths.add_(1.0)
+            d = self.dones
+            self.episode_sums[n, 0] = d.double().sum()
+            self.episode_sums[n, 1] = (self.current_rewards.double() * d.double()).sum()
+            self.episode_sums[n, 2] = (self.current_lengths.double() * d.double()).sum()
+            self.current_rewards.mul_(1.0 - d)
+            self.current_lengths.mul_(1.0 - d)
+        # bootstrap value of the state after the last step
+        _, _, value = self.model.policy(self.obs)
+        self.last_values.copy_(self.model.unnorm_value(value.float()).squeeze(-1))
+        self.rng_counter.add_(self.horizon)
+
+    def play_steps(self) -> float:
+        """Run the rollout (graph replay on GPU after the first epoch); returns seconds."""
+        self.model.eval()
+        t0 = time.perf_counter()
+        with torch.no_grad():
+            if self.use_graph and self.graph is None and self.epoch_num >= 2:
+                self._capture()
+            if self.graph is not None:
+                self.graph.replay()
+            else:
+                self._rollout_body()
+        ep = self.episode_sums.cpu().numpy()           # the rollout's one host sync
+        for cnt, rsum, lsum in ep:
+            if cnt > 0:
+                self.game_rewards.update_moments(int(cnt), rsum / cnt)
+                self.game_lengths.update_moments(int(cnt), lsum / cnt)
+        return time.perf_counter() - t0
+
+    def _capture(self) -> None:
+        torch.cuda.synchronize(self.device)
+        g = torch.cuda.CUDAGraph()
+        try:
+            with torch.cuda.graph(g):
+                self._rollout_body()
+        except Exception as e:  # noqa: BLE001 - fall back to eager launches, loudly
+            print(f"[rlg] rollout graph capture failed ({e}); running the rollout eagerly")
+            self.use_graph = False
+            torch.cuda.synchronize(self.device)
+            return
+        self.graph = g   # capture records the launches without running them
+
+    # ------------------------------------------------------------------ training
+    def prepare_dataset(self) -> Dict[str, torch.Tensor]:
+        b = self.buf
+        adv, ret = ops.gae(b["rewards"], b["values"], b["dones"], self.last_values, self.dones,
+                           self.gamma, self.tau)
+        values = swap_and_flatten01(b["values"]).unsqueeze(1)
+        returns = swap_and_flatten01(ret).unsqueeze(1)
+        advantages = (returns - values).squeeze(1)
+        if self.normalize_value:
+            vms = self.model.value_mean_std
+            vms.train()
+            values = vms(values)
+            returns = vms(returns)
+            vms.eval()
+        if self.normalize_advantage:
+            advantages = (advantages - advantages.mean()) / (advantages.std() + 1e-8)
+        return {
+            "old_values": values, "old_logp_actions": swap_and_flatten01(b["neglogpacs"]),
+            "advantages": advantages, "returns": returns,
+            "actions": swap_and_flatten01(b["actions"]), "obs": swap_and_flatten01(b["obses"]),
+            "mu": swap_and_flatten01(b["mus"]).clone(), "sigma": swap_and_flatten01(b["sigmas"]).clone(),
+        }
+
+    def calc_gradients(self, mb: Dict[str, torch.Tensor]):
+        with torch.autocast(device_type=self.device.type, dtype=torch.float16, enabled=self.mixed_precision):
+            res = self.model.forward_train(mb["obs"], mb["actions"])
+            nlp, values, entropy, mu, sigma = (res["prev_neglogp"], res["values"], res["entropy"],
+                                               res["mus"], res["sigmas"])
+            ratio = torch.exp(mb["old_logp_actions"] - nlp)
+            surr1 = mb["advantages"] * ratio
+            surr2 = mb["advantages"] * torch.clamp(ratio, 1.0 - self.e_clip, 1.0 + self.e_clip)
+            a_loss = torch.max(-surr1, -surr2)
+            if self.clip_value:
+                vpc = mb["old_values"] + (values - mb["old_values"]).clamp(-self.e_clip, self.e_clip)
+                c_loss = torch.max((values - mb["returns"]) ** 2, (vpc - mb["returns"]) ** 2)
+            else:
+                c_loss = (mb["returns"] - values) ** 2
+            if self.bounds_loss_coef is not None:
+                soft_bound = 1.1
+                hi = torch.clamp_min(mu - soft_bound, 0.0) ** 2
+                lo = torch.clamp_max(mu + soft_bound, 0.0) ** 2
+                b_loss = (lo + hi).sum(dim=-1)
+            else:
+                b_loss = torch.zeros_like(a_loss)
+            a_loss, c_loss, entropy, b_loss = a_loss.mean(), c_loss.mean(), entropy.mean(), b_loss.mean()
+            loss = (a_loss + 0.5 * c_loss * self.critic_coef - entropy * self.entropy_coef
+                    + b_loss * float(self.bounds_loss_coef or 0.0))
+        for p in self.model.parameters():
+            p.grad = None
+        self.scaler.scale(loss).backward()
+        if self.truncate_grads:
+            self.scaler.unscale_(self.optimizer)
+            nn.utils.clip_grad_norm_(self.model.parameters(), self.grad_norm)
+        self.scaler.step(self.optimizer)
+        self.scaler.update()
+        with torch.no_grad():
+            kl = policy_kl(mu.detach().float(), sigma.detach().float(), mb["mu"], mb["sigma"])
+        return a_loss.detach(), c_loss.detach(), entropy.detach(), kl, mu.detach().float(), sigma.detach().float(), b_loss.detach()
+
+    def update_lr(self, lr: float) -> None:
+        for g in self.optimizer.param_groups:
+            g["lr"] = lr
+
+    def train_epoch(self) -> Dict[str, float]:
+        self.epoch_num += 1
+        play_time = self.play_steps()
+        t0 = time.perf_counter()
+        self.model.train()
+        data = self.prepare_dataset()
+        kls, a_l, c_l, b_l, ents = [], [], [], [], []
+        for mini_ep in range(self.mini_epochs):
+            ep_kls = []
+            for i in range(self.num_minibatches):
+                s, e = i * self.minibatch_size, (i + 1) * self.minibatch_size
+                mb = {k: v[s:e] for k, v in data.items()}
+                a_loss, c_loss, ent, kl, cmu, csigma, b_loss = self.calc_gradients(mb)
+                data["mu"][s:e] = cmu
+                data["sigma"][s:e] = csigma
+                ep_kls.append(kl); a_l.append(a_loss); c_l.append(c_loss); ents.append(ent); b_l.append(b_loss)
+                if self.scheduler is not None:
+                    self.last_lr = self.scheduler.update(self.last_lr, kl.item())
+                    self.update_lr(self.last_lr)
+            kls.append(torch.stack(ep_kls).mean())
+            if self.normalize_input:
+                self.model.running_mean_std.eval()   # statistics from the first mini-epoch only
+        if self.device.type == "cuda":
+            torch.cuda.synchronize(self.device)
+        update_time = time.perf_counter() - t0
+        self.frame += self.batch_size
+        st = {
+            "epoch": self.epoch_num, "frames": self.frame, "play_time": play_time,
+            "update_time": update_time,
+            "fps_step_inference": self.batch_size / play_time,
+            "fps_total": self.batch_size / (play_time + update_time),
+            "a_loss": torch.stack(a_l).mean().item(), "c_loss": torch.stack(c_l).mean().item(),
+            "b_loss": torch.stack(b_l).mean().item(), "entropy": torch.stack(ents).mean().item(),
+            "kl": torch.stack(kls).mean().item(), "lr": self.last_lr,
+            "mean_rewards": self.game_rewards.get_mean(), "mean_lengths": self.game_lengths.get_mean(),
+            "games": self.game_rewards.current_size,
+        }
+        self.stats = st
+        return st
+
+    def train(self, max_epochs: Optional[int] = None, log=print) -> Dict[str, float]:
+        max_epochs = self.max_epochs if max_epochs is None else int(max_epochs)
+        self.env_reset()
+        st: Dict[str, float] = {}
+        while self.epoch_num < max_epochs:
+            st = self.train_epoch()
+            if log is not None:
+                log(f"fps step and policy inference: {st['fps_step_inference']:.0f} fps total: "
+                    f"{st['fps_total']:.0f} epoch: {st['epoch']}/{max_epochs} "
+                    f"mean reward: {st['mean_rewards']:.3f} mean length: {st['mean_lengths']:.1f}")
+            mean_rewards = st["mean_rewards"]
+            if self.save_frequency > 0 and self.epoch_num % self.save_frequency == 0:
+                self.save(os.path.join(self.run_dir, "nn", f"last_{self.name}_ep_{self.epoch_num}"))
+            if (self.game_rewards.current_size > 0 and mean_rewards > self.last_mean_rewards
+                    and self.epoch_num >= self.save_best_after):
+                self.last_mean_rewards = mean_rewards
+                self.save(os.path.join(self.run_dir, "nn", str(self.name)))
+                if mean_rewards > self.score_to_win:
+                    break
+        return st
+
+    # ------------------------------------------------------------------ checkpoints
+    def get_full_state_weights(self) -> Dict:
+        return {"model": self.model.state_dict(), "epoch": self.epoch_num, "frame": self.frame,
+                "optimizer": self.optimizer.state_dict(), "last_mean_rewards": self.last_mean_rewards,
+                "scaler": self.scaler.state_dict(), "last_lr": self.last_lr}
+
+    def save(self, fn: str) -> str:
+        os.makedirs(os.path.dirname(fn) or ".", exist_ok=True)
+        path = fn if fn.endswith(".pth") else fn + ".pth"
+        torch.save(self.get_full_state_weights(), path)
+        return path
+
+    def restore(self, fn: str) -> None:
+        ck = torch.load(fn, map_location=self.device, weights_only=True)
+        self.model.load_state_dict(ck["model"])
+        self.epoch_num = int(ck.get("epoch", 0))
+        self.frame = int(ck.get("frame", 0))
+        self.last_mean_rewards = float(ck.get("last_mean_rewards", -100500.0))
+        self.last_lr = float(ck.get("last_lr", self.last_lr))
+        if "optimizer" in ck:
+            self.optimizer.load_state_dict(ck["optimizer"])
+        if "scaler" in ck:
+            self.scaler.load_state_dict(ck["scaler"])
+        self.graph = None
+
+
+class A2CPlayer:
+    """rl_games PpoPlayerContinuous: deterministic policy (mu) rollouts of a checkpoint."""
+
+    def __init__(self, env, params: Dict) -> None:
+        self.agent = A2CAgent(env, params)
+        self.env = env
+
+    def restore(self, fn: str) -> None:
+        self.agent.restore(fn)
+
+    @torch.no_grad()
+    def run(self, games: int = 10, max_steps: int = 108000, log=print) -> Dict[str, float]:
+        ag = self.agent
+        ag.model.eval()
+        ag.env_reset()
+        cr = torch.zeros_like(ag.current_rewards)
+        cl = torch.zeros_like(ag.current_lengths)
+        done_games, rew_sum, len_sum = 0, 0.0, 0.0
+        for _ in range(max_steps):
+            mu, _, _ = ag.model.policy(ag.obs)
+            obs, r, d, _ = self.env.step(ag.preprocess_actions(mu.float()))
+            ag.obs.copy_(ag._obs_tensor(obs))
+            d = d.to(ag.device).view(-1).float()
+            cr += r.to(ag.device).view(-1)
+            cl += 1.0
+            n = int(d.sum().item())
+            if n:
+                rew_sum += float((cr * d).sum().item())
+                len_sum += float((cl * d).sum().item())
+                done_games += n
+                cr *= 1.0 - d
+                cl *= 1.0 - d
+            if done_games >= games:
+                break
+        res = {"games": done_games, "mean_reward": rew_sum / max(1, done_games),
+               "mean_length": len_sum / max(1, done_games)}
+        if log is not None:
+            log(f"av reward: {res['mean_reward']:.3f} av steps: {res['mean_length']:.1f}")
+        return res

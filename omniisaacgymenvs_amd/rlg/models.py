@@ -1,0 +1,142 @@
+"""Actor-critic network of the reference's PPO configs (cfg/train/*PPO.yaml ``network``:
+``actor_critic``, ``separate: False``, ``mlp.units``, ``activation: elu``, ``space.continuous``
+with ``fixed_sigma: True``; ``model: continuous_a2c_logstd``), restating rl-games 1.5.2
+``algos_torch/network_builder.py`` (A2CBuilder) and ``algos_torch/models.py``
+(ModelA2CContinuousLogStd) and ``algos_torch/running_mean_std.py``.
+
+Statistics buffers are updated IN PLACE so a captured HIP graph of the rollout (which reads
+them by address) always sees the current values.
+"""
+from __future__ import annotations
+
+from typing import Dict, Sequence
+
+import torch
+import torch.nn as nn
+
+from .ops import neglogp_torch
+
+_ACT = {"elu": nn.ELU, "relu": nn.ReLU, "tanh": nn.Tanh, "selu": nn.SELU, "None": nn.Identity,
+        None: nn.Identity}
+
+
+class RunningMeanStd(nn.Module):
+    """Running mean / variance of a batch stream (parallel-variance merge), f64 buffers;
+    forward normalises (clamped to ±5) or un-normalises. Statistics update only in
+    training mode."""
+
+    def __init__(self, insize, epsilon: float = 1e-05, norm_only: bool = False) -> None:
+        super().__init__()
+        self.epsilon = epsilon
+        self.norm_only = norm_only
+        shape = (insize,) if isinstance(insize, int) else tuple(insize)
+        self.register_buffer("running_mean", torch.zeros(shape, dtype=torch.float64))
+        self.register_buffer("running_var", torch.ones(shape, dtype=torch.float64))
+        self.register_buffer("count", torch.ones((), dtype=torch.float64))
+
+    @torch.no_grad()
+    def _update(self, x: torch.Tensor) -> None:
+        batch_mean = x.mean(0).double()
+        batch_var = x.var(0).double()          # unbiased, as torch.var's default
+        batch_count = float(x.shape[0])
+        delta = batch_mean - self.running_mean
+        tot = self.count + batch_count
+        new_mean = self.running_mean + delta * batch_count / tot
+        m2 = (self.running_var * self.count + batch_var * batch_count
+              + delta ** 2 * self.count * batch_count / tot)
+        self.running_mean.copy_(new_mean)
+        self.running_var.copy_(m2 / tot)
+        self.count.copy_(tot)
+
+    def forward(self, x: torch.Tensor, unnorm: bool = False) -> torch.Tensor:
+        if self.training and not unnorm:
+            self._update(x)
+        mean = self.running_mean.float()
+        var = self.running_var.float()
+        if unnorm:
+            y = torch.clamp(x, min=-5.0, max=5.0)
+            return torch.sqrt(var + self.epsilon) * y + mean
+        if self.norm_only:
+            return x / torch.sqrt(var + self.epsilon)
+        y = (x - mean) / torch.sqrt(var + self.epsilon)
+        return torch.clamp(y, min=-5.0, max=5.0)
+
+
+class ActorCriticMLP(nn.Module):
+    """A2CBuilder.Network with separate=False, continuous space, fixed sigma: a shared MLP
+    trunk, linear mu and value heads, sigma a free [A] parameter (log-std). Linear weights keep
+    torch's default init, every Linear bias starts at 0, sigma at ``sigma_init`` (the
+    builder's initialisation)."""
+
+    def __init__(self, num_obs: int, num_actions: int, units: Sequence[int] = (400, 200, 100),
+                 activation: str = "elu", sigma_init: float = 0.0, fixed_sigma: bool = True) -> None:
+        super().__init__()
+        layers = []
+        d = num_obs
+        for u in units:
+            layers += [nn.Linear(d, u), _ACT[activation]()]
+            d = u
+        self.actor_mlp = nn.Sequential(*layers)
+        self.value = nn.Linear(d, 1)
+        self.mu = nn.Linear(d, num_actions)
+        self.fixed_sigma = fixed_sigma
+        if fixed_sigma:
+            self.sigma = nn.Parameter(torch.zeros(num_actions, dtype=torch.float32), requires_grad=True)
+        else:
+            self.sigma = nn.Linear(d, num_actions)
+        for m in self.modules():
+            if isinstance(m, nn.Linear):
+                nn.init.zeros_(m.bias)
+        with torch.no_grad():
+            if fixed_sigma:
+                self.sigma.fill_(sigma_init)
+            else:
+                self.sigma.weight.fill_(sigma_init)
+
+    def forward(self, obs: torch.Tensor):
+        out = self.actor_mlp(obs)
+        value = self.value(out)
+        mu = self.mu(out)
+        logstd = mu * 0.0 + self.sigma if self.fixed_sigma else self.sigma(out)
+        return mu, logstd, value
+
+
+class ModelA2CContinuousLogStd(nn.Module):
+    """Observation / value normalisation around the network; the train-mode forward returns
+    what the PPO loss needs (rl_games ModelA2CContinuousLogStd.Network.forward, is_train)."""
+
+    def __init__(self, num_obs: int, num_actions: int, network_cfg: Dict, normalize_input: bool,
+                 normalize_value: bool) -> None:
+        super().__init__()
+        mlp = network_cfg.get("mlp", {})
+        space = network_cfg.get("space", {}).get("continuous", {})
+        sigma_init = float(space.get("sigma_init", {}).get("val", 0.0))
+        self.a2c_network = ActorCriticMLP(num_obs, num_actions, tuple(mlp.get("units", (400, 200, 100))),
+                                          mlp.get("activation", "elu"), sigma_init,
+                                          bool(space.get("fixed_sigma", True)))
+        self.normalize_input = normalize_input
+        self.normalize_value = normalize_value
+        if normalize_input:
+            self.running_mean_std = RunningMeanStd(num_obs)
+        if normalize_value:
+            self.value_mean_std = RunningMeanStd(1)
+
+    def norm_obs(self, obs: torch.Tensor) -> torch.Tensor:
+        with torch.no_grad():
+            return self.running_mean_std(obs) if self.normalize_input else obs
+
+    def unnorm_value(self, value: torch.Tensor) -> torch.Tensor:
+        with torch.no_grad():
+            return self.value_mean_std(value, unnorm=True) if self.normalize_value else value
+
+    def policy(self, obs: torch.Tensor):
+        """(mu, logstd, normalised value) of raw observations."""
+        return self.a2c_network(self.norm_obs(obs))
+
+    def forward_train(self, obs: torch.Tensor, prev_actions: torch.Tensor):
+        mu, logstd, value = self.policy(obs)
+        sigma = torch.exp(logstd)
+        entropy = (0.5 + 0.5 * torch.log(torch.tensor(2.0 * torch.pi, device=mu.device)) + logstd).sum(dim=-1)
+        prev_neglogp = neglogp_torch(prev_actions, mu, sigma, logstd)
+        return {"prev_neglogp": prev_neglogp, "values": value, "entropy": entropy, "mus": mu,
+                "sigmas": sigma}

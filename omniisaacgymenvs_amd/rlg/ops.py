@@ -1,0 +1,148 @@
+"""Fused per-sample ops of the PPO learner: ctypes binding of libmi_rl.so (include/mi_rl.h)
+plus the plain-torch statements of the same ops.
+
+On a GPU device the learner calls the HIP kernels and nothing else: :func:`kernels` raises
+when libmi_rl.so is missing (no silent fallback). The torch statements are the fp32
+references the GPU numerics tests compare against, and the implementation of BASELINE
+config 0 (Cartpole, 16 envs, CPU torch), where no GPU exists.
+
+Semantics follow rl-games 1.5.2 (setup.py:17; not vendored, absent from this image):
+``common/a2c_common.py`` ``discount_values`` and ``algos_torch/models.py``
+``ModelA2CContinuousLogStd`` (sample + ``neglogp``).
+"""
+from __future__ import annotations
+
+import ctypes as C
+import math
+import os
+from typing import Optional, Tuple
+
+import torch
+
+_HERE = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+LIB_PATH = os.environ.get("MI_RL_LIB", os.path.join(_HERE, "libmi_rl.so"))
+_LIB: Optional[C.CDLL] = None
+LOG_SQRT_2PI = 0.5 * math.log(2.0 * math.pi)
+
+
+class RLKernelsUnavailable(RuntimeError):
+    pass
+
+
+def load_library() -> C.CDLL:
+    """Load libmi_rl.so and declare every prototype of include/mi_rl.h (no GPU needed)."""
+    global _LIB
+    if _LIB is None:
+        if not os.path.exists(LIB_PATH):
+            raise RLKernelsUnavailable(f"{LIB_PATH} not built (python -c 'import __graft_entry__ as g; g.build()')")
+        lib = C.CDLL(LIB_PATH)
+        vp, f, i32, u64 = C.c_void_p, C.c_float, C.c_int32, C.c_uint64
+        lib.mi_rl_abi_version.restype = i32
+        lib.mi_rl_abi_version.argtypes = []
+        lib.mi_rl_last_error.restype = C.c_char_p
+        lib.mi_rl_last_error.argtypes = []
+        lib.mi_rl_gae.restype = i32
+        lib.mi_rl_gae.argtypes = [vp, vp, vp, vp, vp, i32, i32, f, f, vp, vp, vp]
+        lib.mi_rl_sample_gauss.restype = i32
+        lib.mi_rl_sample_gauss.argtypes = [vp, vp, i32, i32, i32, u64, vp, u64, vp, vp, vp]
+        _LIB = lib
+    return _LIB
+
+
+def kernels() -> C.CDLL:
+    lib = load_library()
+    if not torch.cuda.is_available():
+        raise RLKernelsUnavailable("libmi_rl.so needs a GPU")
+    return lib
+
+
+def _check(rc: int, what: str) -> None:
+    if rc != 0:
+        raise RuntimeError(f"{what} failed ({rc}): {load_library().mi_rl_last_error().decode()}")
+
+
+def _stream(t: torch.Tensor) -> int:
+    return torch.cuda.current_stream(t.device).cuda_stream
+
+
+def _ptr(t: Optional[torch.Tensor]) -> Optional[int]:
+    return None if t is None else t.data_ptr()
+
+
+# ------------------------------------------------------------------------------ GAE
+def gae_torch(rewards, values, dones, last_values, last_dones, gamma: float, tau: float):
+    """rl_games discount_values on [H, N] tensors (dones[t] = done flag before step t).
+    Returns (advantages, returns)."""
+    H = rewards.shape[0]
+    adv = torch.zeros_like(rewards)
+    lastgaelam = torch.zeros_like(rewards[0])
+    for t in reversed(range(H)):
+        if t == H - 1:
+            nnt = 1.0 - last_dones
+            nv = last_values
+        else:
+            nnt = 1.0 - dones[t + 1]
+            nv = values[t + 1]
+        delta = rewards[t] + gamma * nv * nnt - values[t]
+        lastgaelam = delta + gamma * tau * nnt * lastgaelam
+        adv[t] = lastgaelam
+    return adv, adv + values
+
+
+def gae(rewards, values, dones, last_values, last_dones, gamma: float, tau: float,
+        advantages: Optional[torch.Tensor] = None, returns: Optional[torch.Tensor] = None
+        ) -> Tuple[torch.Tensor, torch.Tensor]:
+    """GAE over a time-major [H, N] rollout (f32, contiguous). GPU: mi_rl_gae (one launch);
+    CPU: gae_torch."""
+    if rewards.device.type != "cuda":
+        return gae_torch(rewards, values, dones, last_values, last_dones, gamma, tau)
+    H, N = rewards.shape
+    for name, t in (("rewards", rewards), ("values", values), ("dones", dones)):
+        if t.shape != (H, N) or t.dtype != torch.float32 or not t.is_contiguous():
+            raise ValueError(f"gae: {name} must be contiguous f32 [{H}, {N}], got {tuple(t.shape)} {t.dtype}")
+    for name, t in (("last_values", last_values), ("last_dones", last_dones)):
+        if t.numel() != N or t.dtype != torch.float32 or not t.is_contiguous():
+            raise ValueError(f"gae: {name} must be contiguous f32 [{N}]")
+    adv = torch.empty_like(rewards) if advantages is None else advantages
+    ret = torch.empty_like(rewards) if returns is None else returns
+    _check(kernels().mi_rl_gae(rewards.data_ptr(), values.data_ptr(), dones.data_ptr(),
+                               last_values.data_ptr(), last_dones.data_ptr(), H, N, float(gamma),
+                               float(tau), adv.data_ptr(), ret.data_ptr(), _stream(rewards)),
+           "mi_rl_gae")
+    return adv, ret
+
+
+# ------------------------------------------------------------------------------ sampling
+def neglogp_torch(x, mean, std, logstd):
+    """rl_games ModelA2CContinuousLogStd.neglogp."""
+    return (0.5 * (((x - mean) / std) ** 2).sum(dim=-1) + LOG_SQRT_2PI * x.size()[-1]
+            + logstd.sum(dim=-1))
+
+
+def sample_gauss(mu: torch.Tensor, logstd: torch.Tensor, seed: int,
+                 counter_base: Optional[torch.Tensor] = None, counter_offset: int = 0,
+                 generator: Optional[torch.Generator] = None):
+    """action ~ Normal(mu, exp(logstd)) and its neg-log-prob. GPU: mi_rl_sample_gauss (Philox
+    keyed on (seed, counter, row, j); counter = counter_base[0] + counter_offset); CPU:
+    torch.normal with ``generator``. logstd is [A] (fixed sigma) or [R, A]."""
+    R, A = mu.shape
+    if mu.device.type != "cuda":
+        sigma = torch.exp(logstd)
+        a = torch.normal(mu, sigma.expand_as(mu), generator=generator)
+        return a, neglogp_torch(a, mu, sigma.expand_as(mu), logstd.expand_as(mu))
+    if mu.dtype != torch.float32 or logstd.dtype != torch.float32:
+        raise ValueError("sample_gauss: f32 mu / logstd expected")
+    mu = mu.contiguous()
+    ls = logstd.contiguous()
+    stride = 0 if ls.dim() == 1 else A
+    if ls.numel() != (A if stride == 0 else R * A):
+        raise ValueError(f"sample_gauss: logstd shape {tuple(ls.shape)} vs mu {tuple(mu.shape)}")
+    if counter_base is not None and (counter_base.dtype != torch.int64 or counter_base.device != mu.device):
+        raise ValueError("sample_gauss: counter_base must be an int64 tensor on the mu device")
+    act = torch.empty_like(mu)
+    nlp = torch.empty((R,), device=mu.device, dtype=torch.float32)
+    _check(kernels().mi_rl_sample_gauss(mu.data_ptr(), ls.data_ptr(), stride, R, A,
+                                        int(seed) & ((1 << 64) - 1), _ptr(counter_base),
+                                        int(counter_offset), act.data_ptr(), nlp.data_ptr(),
+                                        _stream(mu)), "mi_rl_sample_gauss")
+    return act, nlp

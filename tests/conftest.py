@@ -20,6 +20,7 @@ def _built():
     g.build_oracle()
     if os.path.exists("/opt/rocm/bin/hipcc"):
         g.build_hip()
+        g.build_rl()
     yield
 
 
