@@ -8,7 +8,8 @@ HBM (Philox) before the timed region.
 
 N=1: `python bench.py` (Humanoid, 4096 envs). N>1: launched by torch.distributed.run, one
 rank per GPU; each rank owns 4096 envs of a global grid (weak scaling) and every
---gather-every steps the rollout slab (obs, rew, done) is gathered to rank 0 over RCCL.
+--gather-every steps the rollout slab (obs, rew, done), which the fused launch writes in
+place, is all-gathered over RCCL asynchronously while the next horizon steps.
 
 Prints ONE JSON line (rank 0). `roofline` is for the dominant kernel (k_env_step), timed
 with HIP events on the stream it is launched on; `cpu_baseline` times the CPU oracle (the
@@ -150,16 +151,24 @@ def main():
     rollout = RolloutGather(args.gather_every, n_local, O, device, world) if world > 1 else None
 
     def one_step(k):
-        obs, rew, done, _ = env.step(actions[k % pool])
-        if rollout is not None:
-            h = k % args.gather_every
+        if rollout is None:
+            return env.step(actions[k % pool])[0]
+        # the launch writes obs/rew/done straight into the rollout slab row (no copies); a full
+        # horizon is all-gathered asynchronously over RCCL while the next one steps
+        h = k % args.gather_every
+        if env.fused:
+            obs = env.step(actions[k % pool], out=rollout.slot(h))[0]
+        else:
+            obs, rew, done, _ = env.step(actions[k % pool])
             rollout.record(h, obs["obs"], rew, done)
-            if h == args.gather_every - 1:
-                rollout.gather()
+        if h == args.gather_every - 1:
+            rollout.gather(async_op=True)
         return obs
 
     for k in range(args.warmup):
         one_step(k)
+    if rollout is not None:
+        rollout.wait()
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
@@ -171,6 +180,8 @@ def main():
     t0 = time.perf_counter()
     for k in range(args.steps):
         one_step(args.warmup + k)
+    if rollout is not None:
+        rollout.wait()   # every collective issued inside the window completes inside it
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
@@ -208,7 +219,7 @@ def main():
                        "task": args.task, "num_envs_per_gpu": n_local, "global_envs": world * n_local,
                        "substeps": task.control_frequency_inv, "path": "fused" if env.fused else "modular",
                        "lds_bytes_per_env": view.sim_kernel_path()[2],
-                       "parallelism": f"env-shard x{world}" + (f" + RCCL all_gather every {args.gather_every}" if world > 1 else "")},
+                       "parallelism": f"env-shard x{world}" + (f" + async RCCL all_gather of the rollout slab every {args.gather_every} steps" if world > 1 else "")},
             "roofline": roof,
             "nan_resets": nan,
         }

@@ -213,6 +213,35 @@ int mi_env_step(mi_sim* sim, const float* actions /*[N,A]*/, int32_t substeps,
 /* rew_out / reset_out: the fresh copies VecEnvRLGames._process_data returns
  * (vec_env_rlgames.py:41-46), written by the same launch instead of two clone kernels. */
 
+/* --- observation / action noise DR (utils/domain_randomization/randomize.py:176-306) ------
+ * The `domain_randomization.randomization_params.{observations,actions}` block of a task YAML.
+ * Noise math and per-env schedule state: include/mi_dr.h. */
+enum { MI_DR_OP_ADDITIVE = 0, MI_DR_OP_SCALING = 1 };
+enum { MI_DR_DIST_GAUSSIAN = 0, MI_DR_DIST_UNIFORM = 1, MI_DR_DIST_LOGUNIFORM = 2 };
+typedef struct mi_dr_noise {
+    int32_t enabled;            /* 0: schedule absent                                  */
+    int32_t operation;          /* MI_DR_OP_*          (randomize.py:277-282,298-303)  */
+    int32_t distribution;       /* MI_DR_DIST_*        (randomize.py:270-275,290-296)  */
+    int32_t frequency_interval; /* on_interval only    (randomize.py:228,252)          */
+    float params[2];            /* distribution_parameters: (mean, std) | (lo, hi)     */
+} mi_dr_noise;
+typedef struct mi_dr_params {
+    mi_dr_noise obs_on_reset, obs_on_interval, act_on_reset, act_on_interval;
+} mi_dr_params;
+/* Randomizer._set_up_{observations,actions}_randomization (randomize.py:176-210): configures
+ * the schedules and zeroes the per-env state (counters, correlated-noise epochs). NULL or all
+ * disabled turns DR off. Once on, mi_env_step applies the action noise after its clamp and the
+ * observation noise before _process_data's clamp, in the same launch (vec_env_rlgames.py:59-71),
+ * and requires actions_out (task.actions) for locomotion tasks. */
+int mi_task_set_dr(mi_sim* sim, const mi_dr_params* dr /*host|NULL*/);
+/* apply_actions_randomization / apply_observations_randomization (randomize.py:212-260) for the
+ * method-by-method step: in place on [N,A] actions / [N,O] obs, with the step's reset_buf. */
+int mi_dr_apply_actions(mi_sim* sim, float* actions /*[N,A]*/, const int64_t* reset_buf, void* stream);
+int mi_dr_apply_observations(mi_sim* sim, float* obs /*[N,O]*/, const int64_t* reset_buf,
+                             void* stream);
+/* Per-env DR schedule state -> host [N,6] uint32: obs (counter, epoch, draws), act (same). */
+int mi_get_dr_state(mi_sim* sim, uint32_t* out /*[N,6] host*/);
+
 /* --- utilities --------------------------------------------------------------------- */
 /* U(lo,hi) Philox4x32-10 actions for the random-policy driver (scripts/random_policy.py:57),
  * keyed on (seed, env_id_offset + env, step). */

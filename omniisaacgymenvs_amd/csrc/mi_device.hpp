@@ -12,6 +12,7 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 #include "../../include/mi_sim.h"
+#include "../../include/mi_dr.h"
 
 #define MI_D __device__ __forceinline__
 #define MI_MAXA 32     // max actions / joint DOFs handled by the task kernels
@@ -76,6 +77,7 @@ struct DevState {
     uint32_t* reset_count;// [N]
     int32_t* nan_flag;    // [N]
     unsigned long long* nan_total;
+    uint32_t* dr_state;   // [6][N] obs counter, epoch, draws; act counter, epoch, draws (or null)
     float* ws;            // workspace [N/64][slots][64]
 };
 
@@ -92,6 +94,8 @@ struct DevTask {
     float task_dt, target[3], init_root_pos[3], init_root_quat[4];
     float dof_pos_noise, dof_vel_noise, reset_dist, max_push_effort;
     float gears[MI_MAXA], ratio[MI_MAXA], init_dof[MI_MAXA];
+    int dr_obs, dr_act;                       // observation / action noise DR on
+    mi_dr_noise obs_r, obs_i, act_r, act_i;   // schedules (include/mi_sim.h, mi_dr.h)
 };
 
 // ---------------------------------------------------------------------------------------

@@ -206,9 +206,14 @@ __global__ void k_env_step(DevModel m, DevState st, SimP p, DevTask tp, const fl
     float* R = (obs_task ? obs_task : obs_out) + (size_t)O * i;
     if (tp.kind == MI_TASK_CARTPOLE)
         cartpole_post(st, tp, i, R, rew, reset_buf, progress_buf);
+    else if (tp.dr_act)   // task.actions = the noisy actions pre_physics_step received
+        loco_post(m, st, tp, i, actions_out + (size_t)tp.A * i, INFINITY, R, rew, reset_buf,
+                  progress_buf, pot, prev);
     else
         loco_post(m, st, tp, i, actions + (size_t)tp.A * i, tp.clip_actions, R, rew, reset_buf,
                   progress_buf, pot, prev);
+    // 4. observation noise DR on task.obs_buf with the new reset_buf (vec_env_rlgames.py:70-71)
+    if (tp.dr_obs) dr_row(st, tp, 0, i, R, O, reset_buf[i] != 0);
     const float co = tp.clip_obs;
     float* OUT = obs_out + (size_t)O * i;
     if (obs_task) {
@@ -318,7 +323,8 @@ __global__ __launch_bounds__(64) void k_env_step_wave(const KParams* __restrict_
     const int lane = threadIdx.x;
     // 1. clamp + pre_physics_step (scalar task math on lane 0); model constants into LDS
     STAMP_BEGIN();
-    wave_task_pre(m, t, st, tp, i, actions, reset_buf, progress_buf, pot, prev, actions_out);
+    const float a_lane =
+        wave_task_pre(m, t, st, tp, i, actions, reset_buf, progress_buf, pot, prev, actions_out);
     stage_model_constants(t, smem);
     STAMP(13);
     // 2. controlFrequencyInv x World.step, wave-cooperative
@@ -329,9 +335,17 @@ __global__ __launch_bounds__(64) void k_env_step_wave(const KParams* __restrict_
     }
     // 3. post_physics_step + obs clamp, wave-cooperative from the LDS-resident state
     STAMP_RESET();
-    wave_loco_post(m, t, st, tp, i, smem, actions, obs_out, obs_task, rew, reset_buf, progress_buf,
+    wave_loco_post(m, t, st, tp, i, smem, a_lane, obs_out, obs_task, rew, reset_buf, progress_buf,
                    pot, prev, rew_out, reset_out);
     STAMP(14);
+}
+
+// Randomizer.apply_{observations,actions}_randomization (randomize.py:212-260), modular path
+__global__ void k_dr_apply(DevState st, DevTask tp, int which, float* buf, int C,
+                           const int64_t* reset_buf) {
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= st.N) return;
+    dr_row(st, tp, which, i, buf + (size_t)C * i, C, reset_buf[i] != 0);
 }
 
 __global__ void k_reset_idx(DevModel m, DevState st, DevTask tp, const int64_t* ids, int n,
@@ -796,7 +810,7 @@ int mi_sim_create(const mi_model_desc* md, const mi_sim_params* prm, int32_t N, 
         AL(q, float, (size_t)D * N); AL(qd, float, (size_t)D * N); AL(eff, float, (size_t)D * N);
         AL(sens, float, (size_t)6 * S * N);
     }
-    AL(reset_count, uint32_t, N); AL(nan_flag, int32_t, N);
+    AL(reset_count, uint32_t, N); AL(nan_flag, int32_t, N); AL(dr_state, uint32_t, (size_t)6 * N);
     AL(nan_total, unsigned long long, 1);
     if (s->wave) {
         if ((rc = dev_alloc(s, &p, sizeof(float) * (size_t)N * s->wt.g_row_stride))) return cleanup(rc);
@@ -1048,6 +1062,8 @@ int mi_env_step(mi_sim* s, const float* actions, int32_t substeps, float* obs_ou
                 void* stream) {
     NEED(s); NEED_TASK(s); NEED(actions); NEED(obs_out); NEED(rew); NEED(reset_buf); NEED(progress_buf);
     if (s->tp.kind != MI_TASK_CARTPOLE) { NEED(potentials); NEED(prev_potentials); }
+    if (s->tp.dr_act && s->tp.kind != MI_TASK_CARTPOLE && !actions_out)
+        return fail(MI_E_NULL, "mi_env_step: action DR needs actions_out (task.actions)");
     if (substeps < 0 || substeps > 64) return fail(MI_E_ARG, "substeps %d out of range", substeps);
     HIP_TRY(hipSetDevice(s->device));
     if (s->wave && s->tp.kind != MI_TASK_CARTPOLE)
@@ -1062,6 +1078,63 @@ int mi_env_step(mi_sim* s, const float* actions, int32_t substeps, float* obs_ou
                            s->ds, s->sp, s->tp, actions, substeps, obs_out, obs_task, rew, reset_buf,
                            progress_buf, potentials, prev_potentials, actions_out, rew_out, reset_out);
     LAUNCH_CHECK();
+    return MI_OK;
+}
+
+int mi_task_set_dr(mi_sim* s, const mi_dr_params* dr) {
+    NEED(s); NEED_TASK(s);
+    mi_dr_params z{};
+    const mi_dr_params& d = dr ? *dr : z;
+    const mi_dr_noise* all[4] = {&d.obs_on_reset, &d.obs_on_interval, &d.act_on_reset, &d.act_on_interval};
+    for (int k = 0; k < 4; ++k) {
+        const mi_dr_noise& n = *all[k];
+        if (!n.enabled) continue;
+        if (n.operation < MI_DR_OP_ADDITIVE || n.operation > MI_DR_OP_SCALING)
+            return fail(MI_E_ARG, "DR: bad operation %d", n.operation);
+        if (n.distribution < MI_DR_DIST_GAUSSIAN || n.distribution > MI_DR_DIST_LOGUNIFORM)
+            return fail(MI_E_ARG, "DR: bad distribution %d", n.distribution);
+        if (n.distribution == MI_DR_DIST_LOGUNIFORM && !(n.params[0] > 0.0f && n.params[1] > 0.0f))
+            return fail(MI_E_ARG, "DR: loguniform needs positive bounds");
+        if ((k & 1) && n.frequency_interval < 1)
+            return fail(MI_E_ARG, "DR: on_interval frequency_interval %d < 1", n.frequency_interval);
+    }
+    DevTask& t = s->tp;
+    t.obs_r = d.obs_on_reset; t.obs_i = d.obs_on_interval;
+    t.act_r = d.act_on_reset; t.act_i = d.act_on_interval;
+    t.dr_obs = d.obs_on_reset.enabled || d.obs_on_interval.enabled;
+    t.dr_act = d.act_on_reset.enabled || d.act_on_interval.enabled;
+    HIP_TRY(hipSetDevice(s->device));
+    HIP_TRY(hipMemset(s->ds.dr_state, 0, sizeof(uint32_t) * 6 * (size_t)s->N));
+    return sync_kparams(s);
+}
+
+int mi_dr_apply_actions(mi_sim* s, float* actions, const int64_t* reset_buf, void* stream) {
+    NEED(s); NEED_TASK(s); NEED(actions); NEED(reset_buf);
+    if (!s->tp.dr_act) return MI_OK;
+    HIP_TRY(hipSetDevice(s->device));
+    hipLaunchKernelGGL(k_dr_apply, grid_for(s, s->N), dim3(s->block), 0, STREAM(stream), s->ds, s->tp,
+                       1, actions, s->tp.A, reset_buf);
+    LAUNCH_CHECK();
+    return MI_OK;
+}
+
+int mi_dr_apply_observations(mi_sim* s, float* obs, const int64_t* reset_buf, void* stream) {
+    NEED(s); NEED_TASK(s); NEED(obs); NEED(reset_buf);
+    if (!s->tp.dr_obs) return MI_OK;
+    HIP_TRY(hipSetDevice(s->device));
+    hipLaunchKernelGGL(k_dr_apply, grid_for(s, s->N), dim3(s->block), 0, STREAM(stream), s->ds, s->tp,
+                       0, obs, s->tp.O, reset_buf);
+    LAUNCH_CHECK();
+    return MI_OK;
+}
+
+int mi_get_dr_state(mi_sim* s, uint32_t* out) {
+    NEED(s); NEED(out);
+    HIP_TRY(hipSetDevice(s->device));
+    std::vector<uint32_t> f((size_t)6 * s->N);
+    HIP_TRY(hipMemcpy(f.data(), s->ds.dr_state, f.size() * 4, hipMemcpyDeviceToHost));
+    for (int i = 0; i < s->N; ++i)
+        for (int k = 0; k < 6; ++k) out[(size_t)6 * i + k] = f[(size_t)k * s->N + i];
     return MI_OK;
 }
 

@@ -79,6 +79,54 @@ MI_D float ref_unscale(float x, float l, float u) {
 MI_D float clampf(float x, float lo, float hi) { return x < lo ? lo : (x > hi ? hi : x); }
 
 // ---------------------------------------------------------------------------------------
+// observation / action noise DR (randomize.py:212-306); noise math in include/mi_dr.h.
+// which: 0 observations, 1 actions. State [6][N] field-major: coalesced across lanes = envs.
+// ---------------------------------------------------------------------------------------
+MI_D mi_dr_env dr_begin(const DevState& st, const DevTask& tp, int which, int i, bool reset) {
+    const mi_dr_noise& r = which ? tp.act_r : tp.obs_r;
+    const mi_dr_noise& v = which ? tp.act_i : tp.obs_i;
+    const uint32_t* s = st.dr_state + (size_t)(3 * which) * st.N;
+    return mi_dr_begin(s[i], s[st.N + i], s[2 * (size_t)st.N + i], reset ? 1 : 0, r.enabled,
+                       v.enabled, v.frequency_interval);
+}
+MI_D void dr_store(const DevState& st, int which, int i, const mi_dr_env& e) {
+    uint32_t* s = st.dr_state + (size_t)(3 * which) * st.N;
+    s[i] = e.counter;
+    s[st.N + i] = e.epoch;
+    s[2 * (size_t)st.N + i] = e.draws;
+}
+// column k of env i's row after both schedules (correlated noise recomputed from the epoch)
+MI_D float dr_col(const DevState& st, const DevTask& tp, int which, const mi_dr_env& e, int i,
+                  int k, float x) {
+    const mi_dr_noise& r = which ? tp.act_r : tp.obs_r;
+    const mi_dr_noise& v = which ? tp.act_i : tp.obs_i;
+    const uint64_t gid = (uint64_t)(st.off + i);
+    float u[4];
+    if (r.enabled) {
+        float c = 0.0f;                      // epoch 0: the reference's zero-initialised buffer
+        if (e.epoch) {
+            uniform4(st.seed, gid, e.epoch, (uint32_t)(k >> 1),
+                     which ? MI_DR_STREAM_ACT_RESET : MI_DR_STREAM_OBS_RESET, u);
+            c = mi_dr_value(r.distribution, r.params[0], r.params[1], u, k);
+        }
+        x = mi_dr_op(r.operation, x, c);
+    }
+    if (v.enabled && e.fire) {
+        uniform4(st.seed, gid, e.draws, (uint32_t)(k >> 1),
+                 which ? MI_DR_STREAM_ACT_INTERVAL : MI_DR_STREAM_OBS_INTERVAL, u);
+        x = mi_dr_op(v.operation, x, mi_dr_value(v.distribution, v.params[0], v.params[1], u, k));
+    }
+    return x;
+}
+// one env's whole row (one-lane-per-env kernels)
+MI_D void dr_row(const DevState& st, const DevTask& tp, int which, int i, float* x, int C,
+                 bool reset) {
+    const mi_dr_env e = dr_begin(st, tp, which, i, reset);
+    for (int k = 0; k < C; ++k) x[k] = dr_col(st, tp, which, e, i, k, x[k]);
+    dr_store(st, which, i, e);
+}
+
+// ---------------------------------------------------------------------------------------
 // reset_idx for one env (mask-driven on the device: no nonzero()/host sync)
 // ---------------------------------------------------------------------------------------
 MI_D void task_reset_env(const DevModel& m, const DevState& st, const DevTask& tp, int i,
@@ -130,12 +178,16 @@ MI_D void task_reset_env(const DevModel& m, const DevState& st, const DevTask& t
 }
 
 // pre_physics_step for one env: reset if flagged, clamp actions, efforts = a*gear*power
+// fused: VecEnvRLGames.step's clamp + action noise DR (vec_env_rlgames.py:57-60) first
 MI_D void task_pre_env(const DevModel& m, const DevState& st, const DevTask& tp, int i,
                        const float* actions, int64_t* reset_buf, int64_t* progress_buf,
                        float* potentials, float* prev_potentials, float* actions_out,
-                       bool clamp_actions) {
+                       bool fused) {
 #pragma clang fp contract(off)
     const int N = st.N, A = tp.A;
+    const bool clamp_actions = fused, dr = fused && tp.dr_act;
+    mi_dr_env e{};
+    if (dr) e = dr_begin(st, tp, 1, i, reset_buf[i] != 0);
     if (reset_buf[i] != 0) {
         task_reset_env(m, st, tp, i, potentials, prev_potentials);
         reset_buf[i] = 0;
@@ -144,6 +196,7 @@ MI_D void task_pre_env(const DevModel& m, const DevState& st, const DevTask& tp,
     if (tp.kind == MI_TASK_CARTPOLE) {
         float a = actions[(size_t)A * i];
         if (clamp_actions) a = clampf(a, -tp.clip_actions, tp.clip_actions);
+        if (dr) a = dr_col(st, tp, 1, e, i, 0, a);
         if (actions_out) actions_out[(size_t)A * i] = a;
         st.eff[sx(st, 0, i)] = tp.max_push_effort * a;
         st.eff[sx(st, 1, i)] = 0.0f;
@@ -151,10 +204,12 @@ MI_D void task_pre_env(const DevModel& m, const DevState& st, const DevTask& tp,
         for (int j = 0; j < A; ++j) {
             float a = actions[(size_t)A * i + j];
             if (clamp_actions) a = clampf(a, -tp.clip_actions, tp.clip_actions);
+            if (dr) a = dr_col(st, tp, 1, e, i, j, a);
             if (actions_out) actions_out[(size_t)A * i + j] = a;
             st.eff[sx(st, j, i)] = a * tp.gears[j] * tp.power_scale;
         }
     }
+    if (dr) dr_store(st, 1, i, e);
 }
 
 // ---------------------------------------------------------------------------------------

@@ -1318,14 +1318,19 @@ MI_D void wave_artic_substep(const DevModel& m, const WaveTabs& t, const DevStat
 // work is spread over lanes (lane j = DOF j) and reads the LDS-resident physics state.
 // ---------------------------------------------------------------------------------------
 
-// pre_physics_step (locomotion.py:103-145): mask-driven reset_idx, clamp, efforts
-MI_D void wave_task_pre(const DevModel& m, const WaveTabs& t, const DevState& st,
-                        const DevTask& tp, int i, const float* actions, int64_t* reset_buf,
-                        int64_t* progress_buf, float* potentials, float* prev_potentials,
-                        float* actions_out) {
+// VecEnvRLGames.step's clamp + action noise DR (vec_env_rlgames.py:57-60), then
+// pre_physics_step (locomotion.py:103-145): mask-driven reset_idx, efforts. Returns lane j's
+// action as pre_physics_step received it (task.actions[i, j]; 0 on lanes >= A).
+MI_D float wave_task_pre(const DevModel& m, const WaveTabs& t, const DevState& st,
+                         const DevTask& tp, int i, const float* actions, int64_t* reset_buf,
+                         int64_t* progress_buf, float* potentials, float* prev_potentials,
+                         float* actions_out) {
 #pragma clang fp contract(off)
     const int lane = threadIdx.x, N = st.N, D = m.D, A = tp.A;
-    if (reset_buf[i] != 0) {                     // wave-uniform
+    const bool flagged = reset_buf[i] != 0;      // wave-uniform
+    mi_dr_env dre{};
+    if (tp.dr_act) dre = dr_begin(st, tp, 1, i, flagged);
+    if (flagged) {
         const uint64_t gid = (uint64_t)(st.off + i);
         const uint32_t cnt = st.reset_count[i];
         const float pn = tp.dof_pos_noise, vn = tp.dof_vel_noise;
@@ -1362,19 +1367,24 @@ MI_D void wave_task_pre(const DevModel& m, const WaveTabs& t, const DevState& st
             progress_buf[i] = 0;
         }
     }
+    float a = 0.0f;
     if (lane < A) {
         const int j = lane;
-        float a = clampf(actions[(size_t)A * i + j], -tp.clip_actions, tp.clip_actions);
+        a = clampf(actions[(size_t)A * i + j], -tp.clip_actions, tp.clip_actions);
+        if (tp.dr_act) a = dr_col(st, tp, 1, dre, i, j, a);
         if (actions_out) actions_out[(size_t)A * i + j] = a;
         st.eff[sx(st, j, i)] = a * tp.gears[j] * tp.power_scale;
     }
+    if (tp.dr_act && lane == 0) dr_store(st, 1, i, dre);
+    return a;
 }
 
-// post_physics_step (rl_task.py:231-251 -> locomotion.py:80-101,173-183) + _process_data's obs
-// clamp, from the final physics state the last substep left in LDS. Writes the unclamped row
-// to obs_task (when given) and the clamped row to obs_out.
+// post_physics_step (rl_task.py:231-251 -> locomotion.py:80-101,173-183), observation noise
+// DR (vec_env_rlgames.py:70-71) and _process_data's obs clamp, from the final physics state the
+// last substep left in LDS. Writes the unclamped (noisy) row to obs_task (when given) and the
+// clamped row to obs_out. a_lane: lane j's task.actions entry (wave_task_pre).
 MI_D void wave_loco_post(const DevModel& m, const WaveTabs& t, const DevState& st,
-                         const DevTask& tp, int i, float* sm, const float* actions,
+                         const DevTask& tp, int i, float* sm, float a_lane,
                          float* obs_out, float* obs_task, float* rew, int64_t* reset_buf,
                          int64_t* progress_buf, float* potentials, float* prev_potentials,
                          float* rew_out, int64_t* reset_out) {
@@ -1384,7 +1394,24 @@ MI_D void wave_loco_post(const DevModel& m, const WaveTabs& t, const DevState& s
     const float* us = sm + t.s_us;
     float* out = obs_out + (size_t)O * i;
     float* raw = obs_task ? obs_task + (size_t)O * i : nullptr;
+    // is_done's decision first (wave-uniform: obs0 = root z, progress, reset_buf, NaN flag) —
+    // the observation noise schedule keys on the reset_buf it produces
+    // (read by lane 0, which wrote them earlier in this launch, and broadcast)
+    int64_t progress = 0, flagged = 0;
+    int nan_env = 0;
+    if (lane == 0) {
+        progress = progress_buf[i] + 1;                      // rl_task.py:242
+        flagged = reset_buf[i];
+        nan_env = st.nan_flag[i];
+    }
+    progress = __shfl(progress, 0);
+    flagged = __shfl(flagged, 0);
+    nan_env = __shfl(nan_env, 0);
+    const int64_t done = nan_env ? 1 : loco_done(tp, sm[t.s_rp + 2], flagged, progress);
+    mi_dr_env dre{};
+    if (tp.dr_obs) dre = dr_begin(st, tp, 0, i, done != 0);
     auto put = [&](int k, float v) {
+        if (tp.dr_obs) v = dr_col(st, tp, 0, dre, i, k, v);
         if (raw) raw[k] = v;
         out[k] = clampf(v, -co, co);
     };
@@ -1394,7 +1421,7 @@ MI_D void wave_loco_post(const DevModel& m, const WaveTabs& t, const DevState& s
         const int j = lane;
         const float pos = ref_unscale(sm[t.s_q + j], m.lower[j + 1], m.upper[j + 1]);
         const float vel = us[m.nr + j] * tp.dof_vel_scale;
-        const float a = clampf(actions[(size_t)tp.A * i + j], -tp.clip_actions, tp.clip_actions);
+        const float a = a_lane;
         put(12 + j, pos);
         put(12 + D + j, vel);
         put(12 + 2 * D + 6 * S + j, a);
@@ -1471,9 +1498,12 @@ MI_D void wave_loco_post(const DevModel& m, const WaveTabs& t, const DevState& s
                       tp.actions_cost * act_cost - tp.energy_cost * elec - limit_cost;
         if (rp[2] < tp.termination_height) total = tp.death_cost;
         rew[i] = total;
-        // is_done + NaN guard; progress_buf += 1 (rl_task.py:242)
-        const int64_t progress = progress_buf[i] + 1;
-        const int64_t done = nan_guard(st, i, loco_done(tp, rp[2], reset_buf[i], progress));
+        // is_done + NaN guard (decided above); progress_buf += 1
+        if (nan_env) {
+            st.nan_flag[i] = 0;
+            atomicAdd(st.nan_total, 1ull);
+        }
+        if (tp.dr_obs) dr_store(st, 0, i, dre);
         reset_buf[i] = done;
         progress_buf[i] = progress;
         if (rew_out) rew_out[i] = total;          // _process_data's returned copies

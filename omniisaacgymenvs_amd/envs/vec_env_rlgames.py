@@ -85,19 +85,24 @@ class VecEnvRLGames:
         self._resets = self._resets.to(t.rl_device).clone()
         self._extras = self._extras.copy()
 
-    def step(self, actions):
+    def step(self, actions, out=None):
+        """vec_env_rlgames.py:56-78. ``out`` (build extension, fused path only): (obs, rew, resets)
+        buffers for the returned copies, e.g. a rollout slab row; by default fresh tensors."""
         t = self._task
+        if out is not None and (not self._fused or str(t.rl_device) != str(t.device)):
+            raise ValueError("step(out=...) needs the fused path with rl_device == sim device")
         if self._fused:
-            # one launch = clamp + pre_physics_step + N substeps + post_physics_step + obs clamp
+            # one launch = clamp + action DR + pre_physics_step + N substeps + post_physics_step +
+            # observation DR + obs clamp
             ev = self.kernel_events
             if ev is not None:
                 k = self._ev_i % len(ev[0])
                 ev[0][k].record()
-                obs, rew, resets = t.fused_step(actions)
+                obs, rew, resets = t.fused_step(actions, out)
                 ev[1][k].record()
                 self._ev_i += 1
             else:
-                obs, rew, resets = t.fused_step(actions)
+                obs, rew, resets = t.fused_step(actions, out)
             self.sim_frame_count += t.control_frequency_inv
             # fresh tensors written by the launch itself (= _process_data's clones)
             rl = str(t.rl_device)
@@ -108,11 +113,16 @@ class VecEnvRLGames:
             self._states = torch.clamp(t.get_states(), -t.clip_obs, t.clip_obs).to(t.rl_device).clone()
             return {"obs": self._obs, "states": self._states}, self._rew, self._resets, self._extras
         actions = torch.clamp(actions, -t.clip_actions, t.clip_actions).to(t.device).clone()
+        if t.randomize_actions:
+            actions = t._dr_randomizer.apply_actions_randomization(actions=actions, reset_buf=t.reset_buf)
         t.pre_physics_step(actions)
         for _ in range(t.control_frequency_inv):
             self._world.step(render=self._render)
             self.sim_frame_count += 1
         self._obs, self._rew, self._resets, self._extras = t.post_physics_step()
+        if t.randomize_observations:
+            self._obs = t._dr_randomizer.apply_observations_randomization(observations=self._obs,
+                                                                          reset_buf=t.reset_buf)
         self._states = t.get_states()
         self._process_data()
         return {"obs": self._obs, "states": self._states}, self._rew, self._resets, self._extras

@@ -65,6 +65,20 @@ class MiTaskParams(C.Structure):
     ]
 
 
+MI_DR_OP_ADDITIVE, MI_DR_OP_SCALING = 0, 1
+MI_DR_DIST_GAUSSIAN, MI_DR_DIST_UNIFORM, MI_DR_DIST_LOGUNIFORM = 0, 1, 2
+
+
+class MiDrNoise(C.Structure):
+    _fields_ = [("enabled", C.c_int32), ("operation", C.c_int32), ("distribution", C.c_int32),
+                ("frequency_interval", C.c_int32), ("params", C.c_float * 2)]
+
+
+class MiDrParams(C.Structure):
+    _fields_ = [("obs_on_reset", MiDrNoise), ("obs_on_interval", MiDrNoise),
+                ("act_on_reset", MiDrNoise), ("act_on_interval", MiDrNoise)]
+
+
 def fptr(a: Optional[np.ndarray]):
     return None if a is None else a.ctypes.data_as(_f32p)
 
@@ -101,6 +115,10 @@ _SIGS = {
     "mi_task_metrics": (C.c_int, [C.c_void_p] + [C.c_void_p] * 6),
     "mi_task_is_done": (C.c_int, [C.c_void_p] + [C.c_void_p] * 4),
     "mi_env_step": (C.c_int, [C.c_void_p, C.c_void_p, C.c_int32] + [C.c_void_p] * 11),
+    "mi_task_set_dr": (C.c_int, [C.c_void_p, C.POINTER(MiDrParams)]),
+    "mi_dr_apply_actions": (C.c_int, [C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p]),
+    "mi_dr_apply_observations": (C.c_int, [C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p]),
+    "mi_get_dr_state": (C.c_int, [C.c_void_p, C.c_void_p]),
     "mi_fill_uniform": (C.c_int, [C.c_void_p, C.c_void_p, C.c_int32, C.c_uint64, C.c_uint64,
                                   C.c_float, C.c_float, C.c_void_p]),
     "mi_get_reset_count": (C.c_int, [C.c_void_p, C.c_void_p]),

@@ -13,6 +13,7 @@ import numpy as np
 import torch
 
 from ...robots.articulations import GridCloner
+from ...utils.domain_randomization.randomize import Randomizer
 from ...utils.spaces import Box
 
 
@@ -21,6 +22,7 @@ class RLTask:
         self._name = name
         self.test = self._cfg.get("test", False)
         self._device = self._cfg["sim_device"]
+        self._dr_randomizer = Randomizer(self._sim_config)
         print("Task Device:", self._device)
 
         self.randomize_actions = False
@@ -146,11 +148,33 @@ class RLTask:
 
     def supports_fused_step(self) -> bool:
         """True when this task runs the build's own task methods unmodified, so
-        VecEnvRLGames.step may replace pre -> N x World.step -> post by ONE mi_env_step."""
+        VecEnvRLGames.step may replace pre -> N x World.step -> post by ONE mi_env_step
+        (observation / action noise DR included: the launch applies it)."""
         native = getattr(self, "_native_task_class", None)
-        if native is None or self.randomize_actions or self.randomize_observations:
+        if native is None:
             return False
         return all(getattr(type(self), m, None) is getattr(native, m, None) for m in self._FUSABLE)
+
+    def _set_up_dr(self) -> None:
+        """Observation / action noise DR from the task YAML (randomize.py:126-174). The
+        reference's locomotion and cartpole tasks never call it; here a `domain_randomization`
+        block with randomize: True in their YAML turns it on (after mi_task_configure)."""
+        if self._dr_randomizer.randomize:
+            self._dr_randomizer.set_up_domain_randomization(self)
+
+    def _step_outputs(self, out=None):
+        """(obs, rew, reset) buffers a fused launch writes its returned copies into: fresh
+        tensors (_process_data's clones), or caller-provided views such as a rollout slab row
+        (utils/distributed.py RolloutGather.slot) — checked here, since the kernel trusts them."""
+        if out is None:
+            return (torch.empty_like(self.obs_buf), torch.empty_like(self.rew_buf),
+                    torch.empty_like(self.reset_buf))
+        obs, rew, reset = out
+        for t, ref in ((obs, self.obs_buf), (rew, self.rew_buf), (reset, self.reset_buf)):
+            if t.shape != ref.shape or t.dtype != ref.dtype or t.device != ref.device or not t.is_contiguous():
+                raise ValueError(f"step output buffer {tuple(t.shape)} {t.dtype} {t.device} does not "
+                                 f"match {tuple(ref.shape)} {ref.dtype} {ref.device} (contiguous)")
+        return obs, rew, reset
 
     def close(self) -> None:
         view = getattr(self, "_robots", None)

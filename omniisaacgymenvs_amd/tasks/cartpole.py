@@ -81,6 +81,7 @@ class CartpoleTask(RLTask):
         self._cart_dof_idx = self._cartpoles.get_dof_index("cartJoint")
         self._pole_dof_idx = self._cartpoles.get_dof_index("poleJoint")
         N.check(N.lib().mi_task_configure(self._h(), C.byref(self.task_params())), "mi_task_configure")
+        self._set_up_dr()
         indices = torch.arange(self._cartpoles.count, dtype=torch.int64, device=self._device)
         self.reset_idx(indices)
 
@@ -92,11 +93,9 @@ class CartpoleTask(RLTask):
         N.check(N.lib().mi_task_is_done(self._h(), self.obs_buf.data_ptr(), self.reset_buf.data_ptr(),
                                         self.progress_buf.data_ptr(), self._stream()), "mi_task_is_done")
 
-    def fused_step(self, actions: torch.Tensor):
+    def fused_step(self, actions: torch.Tensor, out=None):
         a = actions.to(self._device, dtype=torch.float32).contiguous()
-        obs_out = torch.empty_like(self.obs_buf)
-        rew_out = torch.empty_like(self.rew_buf)
-        reset_out = torch.empty_like(self.reset_buf)
+        obs_out, rew_out, reset_out = self._step_outputs(out)
         N.check(N.lib().mi_env_step(self._h(), a.data_ptr(), int(self.control_frequency_inv),
                                     obs_out.data_ptr(), self.obs_buf.data_ptr(), self.rew_buf.data_ptr(),
                                     self.reset_buf.data_ptr(), self.progress_buf.data_ptr(), None, None,

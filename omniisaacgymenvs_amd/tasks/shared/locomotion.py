@@ -145,6 +145,7 @@ class LocomotionTask(RLTask):
         self.actions = torch.zeros((self.num_envs, self.num_actions), device=self._device)
 
         N.check(N.lib().mi_task_configure(self._h(), C.byref(self.task_params())), "mi_task_configure")
+        self._set_up_dr()
         indices = torch.arange(self._robots.count, dtype=torch.int64, device=self._device)
         self.reset_idx(indices)
 
@@ -159,13 +160,11 @@ class LocomotionTask(RLTask):
                                         self.progress_buf.data_ptr(), self._stream()), "mi_task_is_done")
 
     # ------------------------------------------------------------------ fused path
-    def fused_step(self, actions: torch.Tensor):
+    def fused_step(self, actions: torch.Tensor, out=None):
         """VecEnvRLGames.step in one launch; returns fresh (obs clamped, rew, resets) tensors,
         the copies _process_data hands back (vec_env_rlgames.py:41-46)."""
         a = actions.to(self._device, dtype=torch.float32).contiguous()
-        obs_out = torch.empty_like(self.obs_buf)
-        rew_out = torch.empty_like(self.rew_buf)
-        reset_out = torch.empty_like(self.reset_buf)
+        obs_out, rew_out, reset_out = self._step_outputs(out)
         N.check(N.lib().mi_env_step(self._h(), a.data_ptr(), int(self.control_frequency_inv),
                                     obs_out.data_ptr(), self.obs_buf.data_ptr(), self.rew_buf.data_ptr(),
                                     self.reset_buf.data_ptr(), self.progress_buf.data_ptr(),

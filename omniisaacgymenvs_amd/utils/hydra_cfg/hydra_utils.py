@@ -171,6 +171,7 @@ def compose(overrides: Optional[Sequence[str]] = None, cfg_dir: str = CFG_DIR) -
     rest = []
     for ov in overrides:
         k, _, v = ov.partition("=")
+        k = k.lstrip("+")          # Hydra's "+key=value" (append a key absent from the YAML)
         if k in ("task", "train"):
             groups[k] = v
         else:

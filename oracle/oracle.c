@@ -15,6 +15,7 @@
  */
 #include "oracle.h"
 #include "../include/mi_geom.h"   /* contact geometry, shared as source with the device */
+#include "../include/mi_dr.h"     /* obs / action noise DR, shared as source with the device */
 #include <math.h>
 #include <stdlib.h>
 #include <string.h>
@@ -210,6 +211,9 @@ struct orc_sim {
     int32_t* nan_flag;
     int64_t nan_total;
     float* margin; /* per env: ws_t.margin over the last physics call */
+    mi_dr_params dr;   /* observation / action noise DR (randomize.py:176-306) */
+    int dr_obs, dr_act;
+    uint32_t* dr_state; /* [N][6]: obs counter, epoch, draws; act counter, epoch, draws */
 };
 
 static int g_threads = 1;
@@ -301,7 +305,8 @@ void orc_sim_destroy(orc_sim* s) {
                     m->lower, m->upper, m->damping, m->armature, m->geom_link, m->geom_type,
                     m->geom_p0, m->geom_p1, m->geom_radius, m->sensor_link, m->sensor_pos,
                     m->pairs, m->pt_geom, m->pt_end, s->origins, s->root_pos, s->root_quat,
-                    s->root_vel, s->q, s->qd, s->eff, s->sens, s->reset_count, s->nan_flag, s->margin};
+                    s->root_vel, s->q, s->qd, s->eff, s->sens, s->reset_count, s->nan_flag, s->margin,
+                    s->dr_state};
     for (size_t i = 0; i < sizeof ptrs / sizeof ptrs[0]; ++i) free(ptrs[i]);
     free(s);
 }
@@ -897,7 +902,7 @@ void orc_task_configure(orc_sim* s, const mi_task_params* tp) {
 static float clampf(float x, float lo, float hi) { return x < lo ? lo : (x > hi ? hi : x); }
 
 /* pre_physics_step for env i: reset if flagged, clamp actions, compute efforts */
-static void task_pre_env(orc_sim* s, int i, const float* actions, int64_t* reset_buf,
+static void task_pre_env(orc_sim* s, int i, const float* arow /* env i's actions */, int64_t* reset_buf,
                          int64_t* progress_buf, float* potentials, float* prev_potentials,
                          float* actions_out, int clamp_actions) {
     const mi_task_params* tp = &s->tp;
@@ -905,14 +910,14 @@ static void task_pre_env(orc_sim* s, int i, const float* actions, int64_t* reset
     if (reset_buf[i] != 0) task_reset_env(s, i, reset_buf, progress_buf, potentials, prev_potentials);
     float* eff = s->eff + (size_t)D * i;
     if (tp->task_kind == MI_TASK_CARTPOLE) {
-        float a = actions[(size_t)A * i];
+        float a = arow[0];
         if (clamp_actions) a = clampf(a, -tp->clip_actions, tp->clip_actions);
         if (actions_out) actions_out[(size_t)A * i] = a;
         eff[0] = tp->max_push_effort * a;
         eff[1] = 0.0f;
     } else {
         for (int j = 0; j < A; ++j) {
-            float a = actions[(size_t)A * i + j];
+            float a = arow[j];
             if (clamp_actions) a = clampf(a, -tp->clip_actions, tp->clip_actions);
             if (actions_out) actions_out[(size_t)A * i + j] = a;
             eff[j] = a * s->gears[j] * tp->power_scale;
@@ -923,8 +928,8 @@ static void task_pre_env(orc_sim* s, int i, const float* actions, int64_t* reset
 void orc_task_pre_step(orc_sim* s, const float* actions, int64_t* reset_buf, int64_t* progress_buf,
                        float* potentials, float* prev_potentials, float* actions_out) {
     for (int i = 0; i < s->N; ++i)
-        task_pre_env(s, i, actions, reset_buf, progress_buf, potentials, prev_potentials,
-                     actions_out, 0);
+        task_pre_env(s, i, actions + (size_t)s->tp.num_actions * i, reset_buf, progress_buf,
+                     potentials, prev_potentials, actions_out, 0);
 }
 
 void orc_task_reset_idx(orc_sim* s, const int64_t* env_ids, int n, int64_t* reset_buf,
@@ -1079,7 +1084,63 @@ void orc_task_post_step(orc_sim* s, const float* actions, float* obs, float* rew
         task_post_env(s, i, actions, obs, rew, reset_buf, progress_buf, potentials, prev_potentials);
 }
 
-/* VecEnvRLGames.step fused: clamp -> pre -> substeps -> post -> clamp obs */
+/* ---- observation / action noise DR (randomize.py:212-306; math in include/mi_dr.h) ---- */
+void orc_task_set_dr(orc_sim* s, const mi_dr_params* dr) {
+    memset(&s->dr, 0, sizeof(s->dr));
+    if (dr) s->dr = *dr;
+    s->dr_obs = s->dr.obs_on_reset.enabled || s->dr.obs_on_interval.enabled;
+    s->dr_act = s->dr.act_on_reset.enabled || s->dr.act_on_interval.enabled;
+    free(s->dr_state);
+    s->dr_state = (uint32_t*)calloc((size_t)s->N * 6, 4);
+}
+
+/* apply_{observations,actions}_randomization for ONE env row x[0..C) (randomize.py:212-260) */
+static void dr_apply_row(orc_sim* s, int which /* 0 obs, 1 act */, int i, float* x, int C,
+                         int reset) {
+    const mi_dr_noise* r = which ? &s->dr.act_on_reset : &s->dr.obs_on_reset;
+    const mi_dr_noise* v = which ? &s->dr.act_on_interval : &s->dr.obs_on_interval;
+    const uint32_t sr = which ? MI_DR_STREAM_ACT_RESET : MI_DR_STREAM_OBS_RESET;
+    const uint32_t sv = which ? MI_DR_STREAM_ACT_INTERVAL : MI_DR_STREAM_OBS_INTERVAL;
+    uint32_t* st = s->dr_state + (size_t)6 * i + 3 * which;
+    const uint64_t gid = (uint64_t)(s->off + i);
+    mi_dr_env e = mi_dr_begin(st[0], st[1], st[2], reset, r->enabled, v->enabled,
+                              v->frequency_interval);
+    for (int k = 0; k < C; ++k) {
+        float u[4];
+        if (r->enabled) {                       /* correlated: buf (+|*)= corr[epoch] */
+            float c = 0.0f;                     /* epoch 0: the zero-initialised buffer */
+            if (e.epoch) {
+                for (int q = 0; q < 4; ++q) u[q] = orc_uniform(s->seed, gid, e.epoch, (uint32_t)(4 * (k >> 1) + q), sr);
+                c = mi_dr_value(r->distribution, r->params[0], r->params[1], u, k);
+            }
+            x[k] = mi_dr_op(r->operation, x[k], c);
+        }
+        if (v->enabled && e.fire) {             /* uncorrelated, on the fired envs only */
+            for (int q = 0; q < 4; ++q) u[q] = orc_uniform(s->seed, gid, e.draws, (uint32_t)(4 * (k >> 1) + q), sv);
+            x[k] = mi_dr_op(v->operation, x[k], mi_dr_value(v->distribution, v->params[0], v->params[1], u, k));
+        }
+    }
+    st[0] = e.counter; st[1] = e.epoch; st[2] = e.draws;
+}
+
+void orc_dr_apply_actions(orc_sim* s, float* actions, const int64_t* reset_buf) {
+    if (!s->dr_act) return;
+    int A = s->tp.num_actions;
+    for (int i = 0; i < s->N; ++i) dr_apply_row(s, 1, i, actions + (size_t)A * i, A, reset_buf[i] != 0);
+}
+
+void orc_dr_apply_observations(orc_sim* s, float* obs, const int64_t* reset_buf) {
+    if (!s->dr_obs) return;
+    int O = s->tp.num_obs;
+    for (int i = 0; i < s->N; ++i) dr_apply_row(s, 0, i, obs + (size_t)O * i, O, reset_buf[i] != 0);
+}
+
+void orc_get_dr_state(const orc_sim* s, uint32_t* out) {
+    if (s->dr_state) memcpy(out, s->dr_state, (size_t)s->N * 6 * 4);
+    else memset(out, 0, (size_t)s->N * 6 * 4);
+}
+
+/* VecEnvRLGames.step fused: clamp -> [action DR] -> pre -> substeps -> post -> [obs DR] -> clamp obs */
 void orc_env_step(orc_sim* s, const float* actions, int substeps, float* obs_out, float* obs_task,
                   float* rew, int64_t* reset_buf, int64_t* progress_buf, float* potentials,
                   float* prev_potentials, float* actions_out) {
@@ -1092,9 +1153,11 @@ void orc_env_step(orc_sim* s, const float* actions, int substeps, float* obs_out
 #pragma omp for schedule(static)
         for (int i = 0; i < s->N; ++i) {
             /* task.actions is per-env; use a private row so envs stay independent */
-            task_pre_env(s, i, actions, reset_buf, progress_buf, potentials, prev_potentials,
-                         NULL, 1);
             for (int j = 0; j < A; ++j) act[j] = clampf(actions[(size_t)A * i + j], -tp->clip_actions, tp->clip_actions);
+            /* vec_env_rlgames.py:59-60: action noise on the clamped actions, before pre_physics_step
+             * (with the reset_buf that step's reset_idx is about to clear) */
+            if (s->dr_act) dr_apply_row(s, 1, i, act, A, reset_buf[i] != 0);
+            task_pre_env(s, i, act, reset_buf, progress_buf, potentials, prev_potentials, NULL, 0);
             if (actions_out) memcpy(actions_out + (size_t)A * i, act, A * 4);
             env_physics(s, w, i, substeps);
             /* post on a one-env view */
@@ -1116,6 +1179,9 @@ void orc_env_step(orc_sim* s, const float* actions, int substeps, float* obs_out
 #pragma omp atomic
                 s->nan_total++;
             }
+            /* vec_env_rlgames.py:70-71: obs noise on task.obs_buf with the new reset_buf, then
+             * _process_data's clamp */
+            if (s->dr_obs) dr_apply_row(s, 0, i, ob, O, reset_buf[i] != 0);
             for (int k = 0; k < O; ++k) {
                 if (obs_task) obs_task[(size_t)O * i + k] = ob[k];
                 obs_out[(size_t)O * i + k] = clampf(ob[k], -tp->clip_obs, tp->clip_obs);

@@ -62,6 +62,12 @@ void orc_env_step(orc_sim* s, const float* actions, int substeps, float* obs_out
 void orc_task_reset_idx(orc_sim* s, const int64_t* env_ids, int n, int64_t* reset_buf,
                         int64_t* progress_buf, float* potentials, float* prev_potentials);
 
+/* observation / action noise DR (randomize.py:176-306, include/mi_dr.h) */
+void orc_task_set_dr(orc_sim* s, const mi_dr_params* dr /*NULL = off*/);
+void orc_dr_apply_actions(orc_sim* s, float* actions, const int64_t* reset_buf);
+void orc_dr_apply_observations(orc_sim* s, float* obs, const int64_t* reset_buf);
+void orc_get_dr_state(const orc_sim* s, uint32_t* out /*[N,6]*/);
+
 /* stateless task math on caller-provided state (KAT + device task-kernel parity) */
 void orc_loco_post_math(const mi_task_params* tp, int N, int D, int S, const float* root_pos,
                         const float* root_quat, const float* root_vel, const float* q,

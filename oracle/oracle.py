@@ -61,6 +61,10 @@ def lib() -> C.CDLL:
                                           _f, _f]),
             "orc_cartpole_post_math": (None, [C.POINTER(N.MiTaskParams), C.c_int, _f, _f, _f, _f,
                                               _i64, _i64]),
+            "orc_task_set_dr": (None, [C.c_void_p, C.POINTER(N.MiDrParams)]),
+            "orc_dr_apply_actions": (None, [C.c_void_p, _f, _i64]),
+            "orc_dr_apply_observations": (None, [C.c_void_p, _f, _i64]),
+            "orc_get_dr_state": (None, [C.c_void_p, _u32]),
             "orc_dynamics_terms": (None, [C.c_void_p, C.c_int, _f, _f]),
             "orc_aba": (None, [C.c_void_p, C.c_int, _f, _f]),
             "orc_energy": (C.c_double, [C.c_void_p, C.c_int]),
@@ -169,6 +173,21 @@ class OracleSim:
     def configure(self, tp, keep=None):
         self._tp_keep = keep
         lib().orc_task_configure(self.h, C.byref(tp))
+
+    def set_dr(self, dr):
+        """dr: N.MiDrParams or None (off)."""
+        lib().orc_task_set_dr(self.h, C.byref(dr) if dr is not None else None)
+
+    def dr_apply_actions(self, actions, reset):
+        lib().orc_dr_apply_actions(self.h, fp(actions), ip(reset))
+
+    def dr_apply_observations(self, obs, reset):
+        lib().orc_dr_apply_observations(self.h, fp(obs), ip(reset))
+
+    def dr_state(self):
+        out = np.zeros((self.N, 6), np.uint32)
+        lib().orc_get_dr_state(self.h, out.ctypes.data_as(_u32))
+        return out
 
     def env_step(self, actions, substeps, bufs):
         A = np.ascontiguousarray(actions, np.float32)

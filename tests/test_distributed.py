@@ -70,3 +70,57 @@ def test_two_rank_shard_and_gather_equals_single_process():
     ref = _rollout(0, world * N_PER_RANK, world * N_PER_RANK)
     assert got.shape == ref.shape
     np.testing.assert_array_equal(got, ref)
+
+
+def _async_worker(rank, world, port, q):
+    """Three horizons through the double-buffered slabs with async gathers: every gathered
+    horizon must hold each rank's rows exactly, even while the next horizon is being written."""
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    n, O, Hh = 5, 3, 4
+    g = RolloutGather(Hh, n, O, "cpu", world)
+    got = []
+    for hz in range(3):
+        for h in range(Hh):
+            obs, rew, done = g.slot(h)
+            base = 1000 * hz + 100 * rank + 10 * h
+            obs.copy_(torch.arange(n * O, dtype=torch.float32).view(n, O) + base)
+            rew.fill_(base + 0.5)
+            done.fill_(hz + rank)
+        out = g.gather(async_op=True)
+        if hz > 0:
+            got.append(prev_view())
+        prev = out
+
+        def prev_view(o=prev):
+            g.wait()
+            return (o.obs.clone(), o.rew.clone(), o.done.clone())
+    got.append(prev_view())
+    if rank == 0:
+        q.put([tuple(t.numpy() for t in x) for x in got])
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def test_async_double_buffered_gather_two_ranks():
+    world = 2
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = 30500 + os.getpid() % 1000
+    procs = [ctx.Process(target=_async_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    got = q.get(timeout=120)
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    n, O, Hh = 5, 3, 4
+    assert len(got) == 3
+    for hz, (obs, rew, done) in enumerate(got):
+        assert obs.shape == (world, Hh, n, O)
+        for r in range(world):
+            for h in range(Hh):
+                base = 1000 * hz + 100 * r + 10 * h
+                np.testing.assert_array_equal(obs[r, h], np.arange(n * O, dtype=np.float32).reshape(n, O) + base)
+                np.testing.assert_array_equal(rew[r, h], np.full(n, base + 0.5, np.float32))
+                np.testing.assert_array_equal(done[r, h], np.full(n, hz + r, np.int64))
