@@ -43,6 +43,8 @@ def parse():
     ap.add_argument("--cpu-seconds", type=float, default=10.0, help="CPU baseline sample budget")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--modular", action="store_true", help="method-by-method path, not fused")
+    ap.add_argument("--fuse-envs", type=int, default=262144,
+                    help="envs of the obs/reward-fuse HBM roofline side measurement (0: skip)")
     return ap.parse_args()
 
 
@@ -223,6 +225,12 @@ def main():
             "roofline": roof,
             "nan_resets": nan,
         }
+        if world == 1 and args.fuse_envs > 0 and args.task != "Cartpole":
+            # north_star: achieved HBM GB/s of the obs/reward fuse (RLTask.post_physics_step as ONE
+            # streaming kernel, the method-by-method path) where its working set streams from HBM
+            sys.path.insert(0, os.path.join(ROOT, "tools"))
+            from fuse_roofline import measure
+            out["obs_reward_fuse"] = measure(args.task, args.fuse_envs, 30)
         if world == 1 and not args.no_cpu_baseline:
             out["cpu_baseline"] = cpu_baseline(args.task, env, args.cpu_seconds)
         print(json.dumps(out), flush=True)

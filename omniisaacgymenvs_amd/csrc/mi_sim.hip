@@ -160,6 +160,100 @@ __global__ void k_post_step(DevModel m, DevState st, DevTask tp, const float* ac
                   progress_buf, pot, prev);
 }
 
+// RLTask.post_physics_step for the locomotion tasks on the per-env record layout (fs = 1,
+// es = record floats): 64 envs per 64-lane workgroup, HBM-streaming. The block's records and
+// action rows are contiguous in HBM: loaded with coalesced float4 reads into padded LDS rows;
+// each lane then runs the same per-env task math as k_post_step (loco_obs_env / loco_reward /
+// loco_done) on an LDS view of its env, into an LDS obs tile that leaves as coalesced float4
+// stores (the [N, O] obs rows of 64 consecutive envs are one contiguous span).
+// RLTask.post_physics_step for the locomotion tasks on the per-env record layout (fs = 1,
+// es = record floats): TE envs per 64-lane workgroup, HBM-streaming. The block's records and
+// action rows are contiguous in HBM: loaded with coalesced float4 reads into padded LDS rows;
+// lanes < TE then run the same per-env task math as k_post_step (loco_obs_env / loco_reward /
+// loco_done) on an LDS view of their env. STAGE: the obs rows go through an LDS tile and leave
+// as coalesced float4 stores (the [N, O] rows of TE consecutive envs are one contiguous span);
+// otherwise each lane stores its own row.
+MI_D void tile_load(const float* __restrict__ src, int count, float* dst, int row, int pad) {
+    // count floats (a multiple of row) from src into dst rows of `pad` floats
+    const int lane = threadIdx.x;
+    if ((((uintptr_t)src) & 15) == 0 && (row & 3) == 0) {
+        const float4* s4 = (const float4*)src;
+        for (int k = lane; k < count / 4; k += 64) {
+            const float4 v = s4[k];
+            const int f = 4 * k, e = f / row, c = f - e * row;
+            float* d = dst + e * pad + c;
+            d[0] = v.x; d[1] = v.y; d[2] = v.z; d[3] = v.w;
+        }
+    } else {
+        for (int k = lane; k < count; k += 64) {
+            const int e = k / row;
+            dst[e * pad + (k - e * row)] = src[k];
+        }
+    }
+}
+
+template <int TE, bool STAGE>
+__global__ __launch_bounds__(64) void k_loco_post_tiled(DevModel m, DevState st, DevTask tp,
+                                                        const float* __restrict__ actions,
+                                                        float* obs, float* rew, int64_t* reset_buf,
+                                                        int64_t* progress_buf, float* pot,
+                                                        float* prev) {
+    extern __shared__ __attribute__((aligned(16))) float sm[];
+    const int lane = threadIdx.x, e0 = blockIdx.x * TE;
+    const int n = min(TE, st.N - e0);
+    const int O = tp.O, A = tp.A, P = st.es + 1, AP = A + 1;
+    float* srec = sm;
+    float* sact = sm + TE * P;
+    float* sobs = sact + TE * AP;
+    tile_load(st.root_pos + (size_t)e0 * st.es, n * st.es, srec, st.es, P);
+    tile_load(actions + (size_t)e0 * A, n * A, sact, A, AP);
+    __syncthreads();
+    if (lane < n) {
+        DevState v = st;                    // this lane's env, viewed in LDS
+        v.fs = 1; v.es = P;
+        v.root_pos = srec; v.root_quat = srec + (st.root_quat - st.root_pos);
+        v.root_vel = srec + (st.root_vel - st.root_pos);
+        v.q = srec + (st.q - st.root_pos); v.qd = srec + (st.qd - st.root_pos);
+        v.sens = srec + (st.sens - st.root_pos);
+        const int i = e0 + lane;
+        float* R = STAGE ? sobs + (size_t)lane * O : obs + (size_t)i * O;
+        const int64_t progress = progress_buf[i] + 1;                   // rl_task.py:242
+        loco_obs_env(m, v, tp, lane, sact + lane * AP, INFINITY, R, pot + e0, prev + e0);
+        const float* ca = R + 12 + 2 * m.D + 6 * m.S;
+        rew[i] = loco_reward(tp, m.D, R, ca, pot[i], prev[i]);        // calculate_metrics
+        reset_buf[i] = nan_guard(st, i, loco_done(tp, R[0], reset_buf[i], progress));  // is_done
+        progress_buf[i] = progress;
+    }
+    if (!STAGE) return;
+    __syncthreads();
+    float* dst = obs + (size_t)e0 * O;
+    const int cnt = n * O;
+    if ((((uintptr_t)dst) & 15) == 0 && (cnt & 3) == 0) {
+        for (int k = lane; k < cnt / 4; k += 64)
+            ((float4*)dst)[k] = make_float4(sobs[4 * k], sobs[4 * k + 1], sobs[4 * k + 2], sobs[4 * k + 3]);
+    } else {
+        for (int k = lane; k < cnt; k += 64) dst[k] = sobs[k];
+    }
+}
+
+static size_t post_tile_lds(int te, bool stage, int es, int A, int O) {
+    return sizeof(float) * (size_t)(te * (es + 1) + te * (A + 1) + (stage ? te * O : 0));
+}
+
+// variant of the tiled post-step (MI_POST_TILE=64s|64d|32s|32d, default below)
+static int post_tile_variant() {
+    static int v = -1;
+    if (v < 0) {
+        const char* e = getenv("MI_POST_TILE");
+        v = 2;   // 32s
+        if (e && !strcmp(e, "64s")) v = 0;
+        if (e && !strcmp(e, "64d")) v = 1;
+        if (e && !strcmp(e, "32s")) v = 2;
+        if (e && !strcmp(e, "32d")) v = 3;
+    }
+    return v;
+}
+
 // the three task methods as separate kernels, for tasks that override some of them
 __global__ void k_observations(DevModel m, DevState st, DevTask tp, const float* actions,
                                float* obs, float* pot, float* prev) {
@@ -1017,9 +1111,25 @@ int mi_task_post_step(mi_sim* s, const float* actions, float* obs, float* rew, i
     NEED(s); NEED_TASK(s); NEED(obs); NEED(rew); NEED(reset_buf); NEED(progress_buf);
     if (s->tp.kind != MI_TASK_CARTPOLE) { NEED(actions); NEED(potentials); NEED(prev_potentials); }
     HIP_TRY(hipSetDevice(s->device));
-    hipLaunchKernelGGL(k_post_step, grid_for(s, s->N), dim3(s->block), 0, STREAM(stream), s->dm,
-                       s->ds, s->tp, actions, obs, rew, reset_buf, progress_buf, potentials,
-                       prev_potentials);
+    const int var = post_tile_variant();
+    const int te = var < 2 ? 64 : 32;
+    const bool stage = (var & 1) == 0;
+    const size_t tile = post_tile_lds(te, stage, s->ds.es, s->tp.A, s->tp.O);
+    if (s->tp.kind != MI_TASK_CARTPOLE && s->ds.fs == 1 && tile <= 64 * 1024) {
+        const dim3 g((s->N + te - 1) / te);
+#define POST_TILED(TE, ST) hipLaunchKernelGGL((k_loco_post_tiled<TE, ST>), g, dim3(64), tile, STREAM(stream), \
+            s->dm, s->ds, s->tp, actions, obs, rew, reset_buf, progress_buf, potentials, prev_potentials)
+        switch (var) {
+            case 0: POST_TILED(64, true); break;
+            case 1: POST_TILED(64, false); break;
+            case 2: POST_TILED(32, true); break;
+            default: POST_TILED(32, false); break;
+        }
+#undef POST_TILED
+    } else
+        hipLaunchKernelGGL(k_post_step, grid_for(s, s->N), dim3(s->block), 0, STREAM(stream), s->dm,
+                           s->ds, s->tp, actions, obs, rew, reset_buf, progress_buf, potentials,
+                           prev_potentials);
     LAUNCH_CHECK();
     return MI_OK;
 }

@@ -47,6 +47,18 @@ def main():
                            check=True)
             shutil.copy(os.path.join(ROOT, "profiles", f"traffic_{task}.json"),
                         os.path.join(dst, f"traffic_{task.lower()}.json"))
+    # obs/reward fuse (k_loco_post_tiled) at 1M Humanoid envs: stats, traffic, roofline sweep
+    for f in glob.glob(os.path.join(OUT, "prof_fuse", "**", "*kernel_stats.csv"), recursive=True):
+        shutil.copy(f, os.path.join(dst, "kernel_stats_fuse_humanoid.csv"))
+    if os.path.isdir(os.path.join(OUT, "pmcf_fuse")):
+        subprocess.run([sys.executable, os.path.join(ROOT, "tools", "pmc_traffic.py"), "Humanoid",
+                        os.path.join(OUT, "pmcf_fuse"), os.path.join(OUT, "pmcw_fuse"), "--kernel",
+                        "k_loco_post_tiled", "--out", os.path.join(dst, "traffic_fuse_humanoid.json")],
+                       check=True)
+    for t in ("humanoid", "ant"):
+        p = os.path.join(OUT, f"fuse_roofline_{t}.json")
+        if os.path.exists(p):
+            shutil.copy(p, os.path.join(dst, f"fuse_roofline_{t}.json"))
     sq = {}
     for d in ("sq1", "sq2"):
         if os.path.isdir(os.path.join(OUT, d)):
