@@ -1053,6 +1053,75 @@ MI_D void wave_artic_substep(const DevModel& m, const WaveTabs& t, const DevStat
     // between the two sub-sweeps. Row metadata and lambdas live in lane registers (row r in
     // lane r % 64, bank r / 64) and are read with readlane.
 #ifndef MI_DIAG_NO_PGS
+    // Delassus-space (lambda-space) sweeps on the compiled-topology path when every row's J and
+    // W sit in LDS (the common case): lane r holds row r's v_r = J_r . u and its Delassus row
+    // A[r][s] = J_r . W_s, so a row update is readlanes + the projection + one FMA per lane,
+    // with no cross-lane reduction on the dependent chain; u = u* + sum_r W_r lambda_r after the
+    // sweeps. Same row order, projection and lambda carry as the u-space sweeps below (equal in
+    // exact arithmetic; float rounding differs).
+    bool lam_done = false;
+    if constexpr (TP::kCT) {
+        if (nrows <= TP::kLamRows && nrows <= t.j_rows_lds && nrows <= t.w_rows_lds) {   // wave-uniform
+            constexpr int NV = TP::nv;
+            constexpr int RMAX = TP::kLamRows;                      // rows of this path
+            const float* sJ = sm + t.s_J;
+            const float* sW = sm + t.s_W;
+            float b = 0.0f, ia = 1.0f, kd = 0.0f, lam = 0.0f;
+            if (lane < nrows) {
+                b = sm[t.s_rb + lane];
+                ia = 1.0f / sm[t.s_ad + lane];
+                kd = sm[t.s_rk + lane];
+            }
+            const int rl = lane < nrows ? lane : 0;
+            float Jr[NV];
+            sfor<0, NV>([&](auto C) { Jr[C] = sJ[rl * NV + C]; });
+            float v = 0.0f;
+            sfor<0, NV>([&](auto C) { v += Jr[C] * us[C]; });
+            float Ar[RMAX];
+#pragma unroll
+            for (int s2 = 0; s2 < RMAX; ++s2) {
+                float a = 0.0f;
+                if (s2 < nrows) sfor<0, NV>([&](auto C) { a += Jr[C] * sW[s2 * NV + C]; });
+                Ar[s2] = a;
+            }
+            const float mu = p.friction;
+            for (int it = 0; it < p.iters; ++it) {
+                // opaque per sweep: keeps the loop-invariant readlanes inside the sweep
+                asm volatile("" : "+v"(b), "+v"(ia), "+v"(kd));
+                int nrow_it = nrows;
+                asm volatile("" : "+s"(nrow_it));
+                float lamn = 0.0f;
+#pragma unroll
+                for (int rr = 0; rr < RMAX; ++rr) {
+                    if (rr >= nrow_it) break;
+                    __builtin_amdgcn_sched_barrier(0);
+                    const float vr = readlane(v, rr);
+                    const float br = readlane(b, rr), iar = readlane(ia, rr);
+                    const float l0 = readlane(lam, rr);
+                    const int kind = (int)readlane(kd, rr);
+                    float ln = l0 + (br - vr) * iar;
+                    const bool fric = kind == 1 || kind == 2;
+                    const float lim = mu * lamn;
+                    ln = fmaxf(ln, fric ? -lim : 0.0f);     // normal / limit: lambda >= 0
+                    ln = fric ? fminf(ln, lim) : ln;         // friction: |lambda| <= mu lambda_n
+                    lamn = kind == 0 ? ln : lamn;
+                    v += Ar[rr] * (ln - l0);
+                    if (lane_here(lane) == rr) lam = ln;
+                }
+            }
+            float u = lane < NV ? us[lane] : 0.0f;
+            const int kc = lane < NV ? lane : 0;
+#pragma unroll
+            for (int rr = 0; rr < RMAX; ++rr) {
+                if (rr >= nrows) break;
+                u += sW[rr * NV + kc] * readlane(lam, rr);
+            }
+            if (lane < NV) us[lane] = u;
+            if (lane < nrows) sm[t.s_ad + lane] = lam;           // reuse: lambda of row lane
+            lam_done = true;
+        }
+    }
+    if (!lam_done)
     {
         const int half = lane >> 5, kl = lane & 31;
         // J_r[kl] is rebuilt per row from this lane's DOF subspace and the row's force
