@@ -780,7 +780,8 @@ int mi_sim_create(const mi_model_desc* md, const mi_sim_params* prm, int32_t N, 
                 pad4();
                 t.mc_geo = (int)mcb.size();
                 mcb.insert(mcb.end(), geo.begin(), geo.begin() + 8 * md->num_geoms);
-                t.mc_pairs = put_ints(prs);
+                // the pair table stays global (cache-resident, read once per substep by the
+                // broad phase): its LDS room goes to W rows
             }
             pad4();
             t.mc_len = (int)mcb.size();
@@ -835,14 +836,24 @@ int mi_sim_create(const mi_model_desc* md, const mi_sim_params* prm, int32_t N, 
         // span; when that holds fewer rows than a one-bank PGS can use and the LDS budget of
         // the wave path (8 envs / CU, 20 KB each) has room, a dedicated region instead, so
         // the global slab is only the fallback of rare row-heavy substeps.
+        // Otherwise, a second segment at the end takes whatever rows the budget still holds
+        // (rows [w_rows_a, w_rows_lds) at s_W2).
         t.s_W = ro;
         t.w_rows_lds = overlay ? std::min(64, (span1 - ro) / m.nv) : 0;
+        t.w_rows_a = t.w_rows_lds;
+        t.s_W2 = 0;
         {
             const int want = std::min(64, m.max_rows);
             const int lds_budget_floats = (160 * 1024 / 8) / (int)sizeof(float);
             if (ct && t.w_rows_lds < want && so + al4(want * m.nv) <= lds_budget_floats) {
                 t.s_W = take(want * m.nv);
-                t.w_rows_lds = want;
+                t.w_rows_lds = t.w_rows_a = want;
+            } else if (ct && self_on && t.w_rows_lds < want) {   // (w_row<kSelf> on device)
+                const int extra = std::min(want - t.w_rows_lds, (lds_budget_floats - so - 3) / m.nv);
+                if (extra > 0) {
+                    t.s_W2 = take(extra * m.nv);
+                    t.w_rows_lds += extra;
+                }
             }
         }
         t.s_total = so;

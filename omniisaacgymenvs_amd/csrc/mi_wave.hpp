@@ -98,6 +98,7 @@ struct WaveTabs {
     // W rows [0, w_rows_lds) are handed from P9 to P10 through LDS at s_W (stride nv, in the
     // span that is dead by then); rows beyond go through the global slab
     int s_W, w_rows_lds;
+    int s_W2, w_rows_a;   // rows [w_rows_a, w_rows_lds) in a second segment at s_W2
     // J rows [0, j_rows_lds) kept in LDS at s_J (stride nv) for the PGS sweeps
     int s_J, j_rows_lds;
     // per-model constant block (see McLayout): global copy, staged into LDS at s_mc once per
@@ -191,6 +192,14 @@ MI_D float wave_sum(float v) {
     for (int o = 32; o >= 1; o >>= 1) v += __shfl_xor(v, o, 64);
     return v;
 }
+// LDS W row r. Two segments (WaveTabs::s_W2) only on self-collision topologies (the host
+// creates the second segment only for them); otherwise one.
+template <bool SEG2>
+MI_D float* w_row(const WaveTabs& t, float* sm, int r, int nv) {
+    if constexpr (!SEG2) return sm + t.s_W + r * nv;
+    return sm + (r < t.w_rows_a ? t.s_W + r * nv : t.s_W2 + (r - t.w_rows_a) * nv);
+}
+
 MI_D float readlane(float v, int l) {
     return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), l));
 }
@@ -722,8 +731,16 @@ MI_D void wave_artic_substep(const DevModel& m, const WaveTabs& t, const DevStat
         // world segments of every geom, once (lanes over geoms)
         float* seg = sm + t.s_seg;
         float* bnd = seg + 8 * t.ngeoms;   // bounding sphere: centre (3), half-length + radius
-        const float* geo = sm + t.s_mc + t.mc_geo;                        // LDS copies
-        const int* prs = reinterpret_cast<const int*>(sm + t.s_mc + t.mc_pairs);
+        const float* geo = sm + t.s_mc + t.mc_geo;                        // LDS copy
+        // geom pairs from the global table (cache-resident), the first 256 prefetched ahead of
+        // the segment pass
+        const int2* gpr = reinterpret_cast<const int2*>(t.g_pairs);
+        int2 gpf[4];
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+            const int pi = 64 * q + lane;
+            gpf[q] = pi < t.npairs ? gpr[pi] : make_int2(0, 0);
+        }
         for (int g = lane; g < t.ngeoms; g += 64) {
             const float* A = geo + 8 * g;
             const int l = (int)A[0];
@@ -755,8 +772,10 @@ MI_D void wave_artic_substep(const DevModel& m, const WaveTabs& t, const DevStat
         for (int pb = 0; pb < t.npairs; pb += 64) {
             const int pi = pb + lane;
             bool keep = false;
+            int2 gp = make_int2(0, 0);
             if (pi < t.npairs) {
-                const int2 gp = *reinterpret_cast<const int2*>(prs + 2 * pi);
+                const int q = pb >> 6;
+                gp = q == 0 ? gpf[0] : q == 1 ? gpf[1] : q == 2 ? gpf[2] : q == 3 ? gpf[3] : gpr[pi];
                 const float4 A = *reinterpret_cast<const float4*>(bnd + 4 * gp.x);
                 const float4 B = *reinterpret_cast<const float4*>(bnd + 4 * gp.y);
                 const float cx = A.x - B.x, cy = A.y - B.y, cz = A.z - B.z;
@@ -764,7 +783,7 @@ MI_D void wave_artic_substep(const DevModel& m, const WaveTabs& t, const DevStat
                 keep = cx * cx + cy * cy + cz * cz < reach * reach;
             }
             const unsigned long long mask = __ballot(keep);
-            if (keep) surv[nsv + __popcll(mask & ((1ull << lane) - 1ull))] = pi;
+            if (keep) surv[nsv + __popcll(mask & ((1ull << lane) - 1ull))] = gp.x | (gp.y << 16);
             nsv += __popcll(mask);
         }
         nsv = __builtin_amdgcn_readfirstlane(nsv);
@@ -777,9 +796,9 @@ MI_D void wave_artic_substep(const DevModel& m, const WaveTabs& t, const DevStat
             float pc[3], n[3], bn = 0.0f;
             int la = 0, lb = 0;
             if (sidx < nsv) {
-                const int pi = surv[sidx];
-                const float* A = seg + 8 * prs[2 * pi];
-                const float* B = seg + 8 * prs[2 * pi + 1];
+                const int pk = surv[sidx];                 // geom pair, packed (a | b << 16)
+                const float* A = seg + 8 * (pk & 0xffff);
+                const float* B = seg + 8 * (pk >> 16);
                 la = (int)A[7]; lb = (int)B[7];
                 const float gap = mi_pair_contact(A, A + 3, A[6], B, B + 3, B[6], pc, n);
                 act = gap < p.contact_offset;
@@ -938,7 +957,7 @@ MI_D void wave_artic_substep(const DevModel& m, const WaveTabs& t, const DevStat
                     if (c < nv) jl[c] = c == kd ? sc : 0.0f;
             }
             if (nrows <= t.w_rows_lds) {   // uniform: every row of this substep fits in LDS
-                float* wl = sm + t.s_W + slot * nv;
+                float* wl = w_row<TP::kSelf>(t, sm, slot, nv);
 #pragma unroll
                 for (int c = 0; c < NR; ++c)
                     if (c < nv) wl[c] = res[c] * sc;
@@ -1047,6 +1066,13 @@ MI_D void wave_artic_substep(const DevModel& m, const WaveTabs& t, const DevStat
     STAT(18, total > 64);
     STAT(19, nrows > t.j_rows_lds);
     STAT(20, ncon);
+    STAT(21, nrows > 16);
+    STAT(22, nrows > 24);
+    STAT(23, nrows > 32);
+    STAT(24, nrows > 40);
+    STAT(25, nrows > 48);
+    STAT(26, t.w_rows_lds);
+    STAT(27, t.j_rows_lds);
     // ---- P10: projected Gauss-Seidel. Lane k (mod 32) owns dof k; the wave's lower half
     // holds J / W of rows 0..63 in registers, the upper half rows 64..127. Rows are swept in
     // order; only the half owning the current row is active and u is copied across halves
@@ -1065,7 +1091,6 @@ MI_D void wave_artic_substep(const DevModel& m, const WaveTabs& t, const DevStat
             constexpr int NV = TP::nv;
             constexpr int RMAX = TP::kLamRows;                      // rows of this path
             const float* sJ = sm + t.s_J;
-            const float* sW = sm + t.s_W;
             float b = 0.0f, ia = 1.0f, kd = 0.0f, lam = 0.0f;
             if (lane < nrows) {
                 b = sm[t.s_rb + lane];
@@ -1081,7 +1106,10 @@ MI_D void wave_artic_substep(const DevModel& m, const WaveTabs& t, const DevStat
 #pragma unroll
             for (int s2 = 0; s2 < RMAX; ++s2) {
                 float a = 0.0f;
-                if (s2 < nrows) sfor<0, NV>([&](auto C) { a += Jr[C] * sW[s2 * NV + C]; });
+                if (s2 < nrows) {
+                    const float* w = w_row<TP::kSelf>(t, sm, s2, NV);
+                    sfor<0, NV>([&](auto C) { a += Jr[C] * w[C]; });
+                }
                 Ar[s2] = a;
             }
             const float mu = p.friction;
@@ -1114,7 +1142,7 @@ MI_D void wave_artic_substep(const DevModel& m, const WaveTabs& t, const DevStat
 #pragma unroll
             for (int rr = 0; rr < RMAX; ++rr) {
                 if (rr >= nrows) break;
-                u += sW[rr * NV + kc] * readlane(lam, rr);
+                u += w_row<TP::kSelf>(t, sm, rr, NV)[kc] * readlane(lam, rr);
             }
             if (lane < NV) us[lane] = u;
             if (lane < nrows) sm[t.s_ad + lane] = lam;           // reuse: lambda of row lane
@@ -1139,13 +1167,15 @@ MI_D void wave_artic_substep(const DevModel& m, const WaveTabs& t, const DevStat
         float Wr[64];
         if (nrows <= t.w_rows_lds) {                  // implies one_bank (w_rows_lds <= 64)
             const float km = kl < nv ? 1.0f : 0.0f;
-            const float* wl = sm + t.s_W + (kl < nv ? kl : 0);
+            const int kc = kl < nv ? kl : 0;
             if constexpr (TP::kCT) {
 #pragma unroll
-                for (int rr = 0; rr < 64; ++rr) Wr[rr] = wl[rr * TP::nv] * km;
+                for (int rr = 0; rr < 64; ++rr)
+                    Wr[rr] = w_row<TP::kSelf>(t, sm, min(rr, t.w_rows_lds - 1), TP::nv)[kc] * km;
             } else {
 #pragma unroll
-                for (int rr = 0; rr < 64; ++rr) Wr[rr] = wl[rr * nv] * km;
+                for (int rr = 0; rr < 64; ++rr)
+                    Wr[rr] = w_row<TP::kSelf>(t, sm, min(rr, t.w_rows_lds - 1), nv)[kc] * km;
             }
         } else {
             const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
