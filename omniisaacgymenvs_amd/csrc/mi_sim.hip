@@ -201,20 +201,81 @@ __global__ __launch_bounds__(64) void k_loco_post_tiled(DevModel m, DevState st,
     extern __shared__ __attribute__((aligned(16))) float sm[];
     const int lane = threadIdx.x, e0 = blockIdx.x * TE;
     const int n = min(TE, st.N - e0);
-    const int O = tp.O, A = tp.A, P = st.es + 1, AP = A + 1;
+    const int O = tp.O, A = tp.A;
+    if (TE == 32 && STAGE) {
+        // compact tile: each record's used fields only (root 13, q, qd, sensors: the efforts
+        // and the line padding are dropped on the way into LDS), actions read in place
+        const int D = m.D, S = m.S;
+        const int k0 = 13 + 2 * D, s0 = 13 + 3 * D, ns = 6 * S, PC = k0 + ns + 1;
+        float* srec = sm;
+        float* sobs = sm + TE * PC;
+        float* sterm = sobs + TE * O;                          // [TE][3] sums
+        {
+            const float4* s4 = (const float4*)(st.root_pos + (size_t)e0 * st.es);
+            for (int k = lane; k < n * st.es / 4; k += 64) {   // es % 4 == 0 (whole lines)
+                const float4 v4 = s4[k];
+                const float vv[4] = {v4.x, v4.y, v4.z, v4.w};
+                const int f0 = 4 * k, e = f0 / st.es, c0 = f0 - e * st.es;
+#pragma unroll
+                for (int q = 0; q < 4; ++q) {
+                    const int c = c0 + q;
+                    if (c < k0) srec[e * PC + c] = vv[q];
+                    else if (c >= s0 && c < s0 + ns) srec[e * PC + k0 + (c - s0)] = vv[q];
+                }
+            }
+        }
+        __syncthreads();
+        DevState v = st;                    // the block's envs, viewed in LDS
+        v.fs = 1; v.es = PC;
+        v.root_pos = srec; v.root_quat = srec + 3; v.root_vel = srec + 7;
+        v.q = srec + 13; v.qd = srec + 13 + D; v.sens = srec + k0;
+        // split by lane halves: lanes 0..31 the root-frame block of env `lane`, lanes 32..63 the
+        // per-DOF / sensor block and the reward's DOF-order sums of env `lane - 32`
+        const int e = lane & 31;
+        float* R = sobs + (size_t)e * O;
+        if (e < n) {
+            if (lane < 32) {
+                loco_obs_root(v, tp, e, R, pot + e0, prev + e0);
+            } else {
+                loco_obs_dof(m, v, tp, e, actions + (size_t)(e0 + e) * A, INFINITY, R);
+                const LocoTerms lt = loco_reward_terms(tp, m.D, R, R + 12 + 2 * m.D + 6 * m.S);
+                sterm[3 * e] = lt.limit_cost; sterm[3 * e + 1] = lt.act_cost; sterm[3 * e + 2] = lt.elec;
+            }
+        }
+        __syncthreads();
+        if (lane < n) {
+            const int i = e0 + lane;
+            const LocoTerms lt{sterm[3 * lane], sterm[3 * lane + 1], sterm[3 * lane + 2]};
+            const int64_t progress = progress_buf[i] + 1;               // rl_task.py:242
+            rew[i] = loco_reward_total(tp, R[0], R[10], R[11], pot[i], prev[i], lt);
+            reset_buf[i] = nan_guard(st, i, loco_done(tp, R[0], reset_buf[i], progress));
+            progress_buf[i] = progress;
+        }
+        __syncthreads();
+        float* dst = obs + (size_t)e0 * O;
+        const int cnt = n * O;
+        if ((((uintptr_t)dst) & 15) == 0 && (cnt & 3) == 0) {
+            for (int k = lane; k < cnt / 4; k += 64)
+                ((float4*)dst)[k] = make_float4(sobs[4 * k], sobs[4 * k + 1], sobs[4 * k + 2], sobs[4 * k + 3]);
+        } else {
+            for (int k = lane; k < cnt; k += 64) dst[k] = sobs[k];
+        }
+        return;
+    }
+    const int P = st.es + 1, AP = A + 1;
     float* srec = sm;
     float* sact = sm + TE * P;
     float* sobs = sact + TE * AP;
     tile_load(st.root_pos + (size_t)e0 * st.es, n * st.es, srec, st.es, P);
     tile_load(actions + (size_t)e0 * A, n * A, sact, A, AP);
     __syncthreads();
+    DevState v = st;                        // the block's envs, viewed in LDS
+    v.fs = 1; v.es = P;
+    v.root_pos = srec; v.root_quat = srec + (st.root_quat - st.root_pos);
+    v.root_vel = srec + (st.root_vel - st.root_pos);
+    v.q = srec + (st.q - st.root_pos); v.qd = srec + (st.qd - st.root_pos);
+    v.sens = srec + (st.sens - st.root_pos);
     if (lane < n) {
-        DevState v = st;                    // this lane's env, viewed in LDS
-        v.fs = 1; v.es = P;
-        v.root_pos = srec; v.root_quat = srec + (st.root_quat - st.root_pos);
-        v.root_vel = srec + (st.root_vel - st.root_pos);
-        v.q = srec + (st.q - st.root_pos); v.qd = srec + (st.qd - st.root_pos);
-        v.sens = srec + (st.sens - st.root_pos);
         const int i = e0 + lane;
         float* R = STAGE ? sobs + (size_t)lane * O : obs + (size_t)i * O;
         const int64_t progress = progress_buf[i] + 1;                   // rl_task.py:242
@@ -236,7 +297,9 @@ __global__ __launch_bounds__(64) void k_loco_post_tiled(DevModel m, DevState st,
     }
 }
 
-static size_t post_tile_lds(int te, bool stage, int es, int A, int O) {
+static size_t post_tile_lds(int te, bool stage, int es, int A, int O, int D, int S) {
+    if (te == 32 && stage)   // compact record tile + obs tile + reward sums
+        return sizeof(float) * (size_t)(te * (13 + 2 * D + 6 * S + 1) + te * O + 3 * te);
     return sizeof(float) * (size_t)(te * (es + 1) + te * (A + 1) + (stage ? te * O : 0));
 }
 
@@ -1125,7 +1188,7 @@ int mi_task_post_step(mi_sim* s, const float* actions, float* obs, float* rew, i
     const int var = post_tile_variant();
     const int te = var < 2 ? 64 : 32;
     const bool stage = (var & 1) == 0;
-    const size_t tile = post_tile_lds(te, stage, s->ds.es, s->tp.A, s->tp.O);
+    const size_t tile = post_tile_lds(te, stage, s->ds.es, s->tp.A, s->tp.O, s->dm.D, s->dm.S);
     if (s->tp.kind != MI_TASK_CARTPOLE && s->ds.fs == 1 && tile <= 64 * 1024) {
         const dim3 g((s->N + te - 1) / te);
 #define POST_TILED(TE, ST) hipLaunchKernelGGL((k_loco_post_tiled<TE, ST>), g, dim3(64), tile, STREAM(stream), \

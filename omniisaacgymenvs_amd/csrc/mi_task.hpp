@@ -216,11 +216,10 @@ MI_D void task_pre_env(const DevModel& m, const DevState& st, const DevTask& tp,
 // get_observations (locomotion.py:80-101,194-254) for one env: writes the UNCLAMPED obs row
 // and updates potentials / prev_potentials.
 // ---------------------------------------------------------------------------------------
-MI_D void loco_obs_env(const DevModel& m, const DevState& st, const DevTask& tp, int i,
-                       const float* act /* row */, float act_clip, float* orow,
-                       float* potentials, float* prev_potentials) {
+// get_observations, root-frame block: obs[0..11] + potentials / prev_potentials
+MI_D void loco_obs_root(const DevState& st, const DevTask& tp, int i, float* orow,
+                        float* potentials, float* prev_potentials) {
 #pragma clang fp contract(off)
-    const int N = st.N, D = m.D, S = m.S;
     float rp[3], rq[4], rv[6];
 #pragma unroll
     for (int k = 0; k < 3; ++k) rp[k] = st.root_pos[sx(st, k, i)];
@@ -263,6 +262,15 @@ MI_D void loco_obs_env(const DevModel& m, const DevState& st, const DevTask& tp,
     orow[9] = ref_normalize_angle(angle_to_target);
     orow[10] = up[2];
     orow[11] = heading_proj;
+    potentials[i] = new_p;
+    prev_potentials[i] = prev_p;
+}
+
+// get_observations, per-DOF / sensor block: obs[12 ..]
+MI_D void loco_obs_dof(const DevModel& m, const DevState& st, const DevTask& tp, int i,
+                       const float* act /* row */, float act_clip, float* orow) {
+#pragma clang fp contract(off)
+    const int D = m.D, S = m.S;
     for (int j = 0; j < D; ++j) {
         orow[12 + j] = ref_unscale(st.q[sx(st, j, i)], m.lower[j + 1], m.upper[j + 1]);
         orow[12 + D + j] = st.qd[sx(st, j, i)] * tp.dof_vel_scale;
@@ -270,37 +278,54 @@ MI_D void loco_obs_env(const DevModel& m, const DevState& st, const DevTask& tp,
     }
     for (int k = 0; k < 6 * S; ++k)
         orow[12 + 2 * D + k] = st.sens[sx(st, k, i)] * tp.contact_force_scale;
-    potentials[i] = new_p;
-    prev_potentials[i] = prev_p;
 }
 
-// calculate_metrics (locomotion.py:271-321 + humanoid.py:120-127 / ant.py:92-95) from the
-// unclamped obs row
-MI_D float loco_reward(const DevTask& tp, int D, const float* orow, const float* act, float pot,
-                       float prev) {
+// ---------------------------------------------------------------------------------------
+// get_observations (locomotion.py:80-101,194-254) for one env: writes the UNCLAMPED obs row
+// and updates potentials / prev_potentials.
+// ---------------------------------------------------------------------------------------
+MI_D void loco_obs_env(const DevModel& m, const DevState& st, const DevTask& tp, int i,
+                       const float* act /* row */, float act_clip, float* orow,
+                       float* potentials, float* prev_potentials) {
+    loco_obs_root(st, tp, i, orow, potentials, prev_potentials);
+    loco_obs_dof(m, st, tp, i, act, act_clip, orow);
+}
+
+// calculate_metrics (locomotion.py:271-321 + humanoid.py:120-127 / ant.py:92-95), split into
+// the per-DOF sums (DOF order) and the total
+struct LocoTerms { float limit_cost, act_cost, elec; };
+MI_D LocoTerms loco_reward_terms(const DevTask& tp, int D, const float* orow, const float* act) {
 #pragma clang fp contract(off)
-    float limit_cost = 0.0f;
+    LocoTerms r{0.0f, 0.0f, 0.0f};
     if (tp.kind == MI_TASK_HUMANOID) {
         for (int j = 0; j < D; ++j) {
             const float a = fabsf(orow[12 + j]);
             const float sc = tp.joints_at_limit_cost * (a - 0.98f) / 0.02f;
-            limit_cost += (a > 0.98f ? 1.0f : 0.0f) * sc * tp.ratio[j];
+            r.limit_cost += (a > 0.98f ? 1.0f : 0.0f) * sc * tp.ratio[j];
         }
     } else {
         int64_t cnt = 0;
         for (int j = 0; j < D; ++j) cnt += orow[12 + j] > 0.99f;
-        limit_cost = (float)cnt;
+        r.limit_cost = (float)cnt;
     }
-    const float o11 = orow[11], o10 = orow[10];
+    for (int j = 0; j < D; ++j) r.act_cost += act[j] * act[j];
+    for (int j = 0; j < D; ++j) r.elec += fabsf(act[j] * orow[12 + D + j]) * tp.ratio[j];
+    return r;
+}
+MI_D float loco_reward_total(const DevTask& tp, float o0, float o10, float o11, float pot,
+                             float prev, const LocoTerms& t) {
+#pragma clang fp contract(off)
     const float heading = o11 > 0.8f ? tp.heading_weight : tp.heading_weight * o11 / 0.8f;
     const float upr = o10 > 0.93f ? 0.0f + tp.up_weight : 0.0f;
-    float act_cost = 0.0f, elec = 0.0f;
-    for (int j = 0; j < D; ++j) act_cost += act[j] * act[j];
-    for (int j = 0; j < D; ++j) elec += fabsf(act[j] * orow[12 + D + j]) * tp.ratio[j];
     float total = (pot - prev) + tp.alive_reward_scale + upr + heading -
-                  tp.actions_cost * act_cost - tp.energy_cost * elec - limit_cost;
-    if (orow[0] < tp.termination_height) total = tp.death_cost;
+                  tp.actions_cost * t.act_cost - tp.energy_cost * t.elec - t.limit_cost;
+    if (o0 < tp.termination_height) total = tp.death_cost;
     return total;
+}
+MI_D float loco_reward(const DevTask& tp, int D, const float* orow, const float* act, float pot,
+                       float prev) {
+    return loco_reward_total(tp, orow[0], orow[10], orow[11], pot, prev,
+                             loco_reward_terms(tp, D, orow, act));
 }
 
 // is_done (locomotion.py:257-268)
