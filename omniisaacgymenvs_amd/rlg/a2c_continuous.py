@@ -151,8 +151,18 @@ class A2CAgent:
         torch.manual_seed(self.seed)
         self.model = ModelA2CContinuousLogStd(self.num_obs, self.num_actions, params["network"],
                                               self.normalize_input, self.normalize_value).to(self.device)
-        self.optimizer = torch.optim.Adam(self.model.parameters(), lr=self.last_lr, eps=1e-08,
-                                          weight_decay=float(cfg.get("weight_decay", 0.0)))
+        wd = float(cfg.get("weight_decay", 0.0))
+        if self.device.type == "cuda":
+            # LR lives on the device and the legacy adaptive schedule updates it there (no
+            # kl.item() per minibatch); fused Adam takes the tensor LR and GradScaler's
+            # found_inf / scale without host syncs, so a minibatch update is graph-capturable
+            self.lr_t = torch.tensor(self.last_lr, device=self.device, dtype=torch.float32)
+            self.optimizer = torch.optim.Adam(self.model.parameters(), lr=self.lr_t, eps=1e-08,
+                                              weight_decay=wd, fused=True, capturable=True)
+        else:
+            self.lr_t = None
+            self.optimizer = torch.optim.Adam(self.model.parameters(), lr=self.last_lr, eps=1e-08,
+                                              weight_decay=wd)
         self.scaler = torch.amp.GradScaler("cuda", enabled=self.mixed_precision)
         self.sample_gen = torch.Generator(device="cpu").manual_seed(self.seed)
         self.sample_seed = (self.seed * 0x9E3779B97F4A7C15 + 1) & ((1 << 64) - 1)
@@ -180,6 +190,12 @@ class A2CAgent:
         self.game_lengths = AverageMeter(int(cfg.get("games_to_track", 100)))
         self.use_graph = self.device.type == "cuda" and bool(cfg.get("graph_rollout", True))
         self.graph: Optional[torch.cuda.CUDAGraph] = None
+        # minibatch updates: one captured graph per (obs-statistics mode, minibatch index)
+        self.graph_update = self.device.type == "cuda" and bool(cfg.get("graph_update", True))
+        self.upd_graphs: Dict = {}
+        self._data: Optional[Dict[str, torch.Tensor]] = None
+        self._mb_out = torch.zeros((self.num_minibatches, 5), device=dev, dtype=f32)
+        self._mb_stats = torch.zeros((self.mini_epochs, self.num_minibatches, 5), device=dev, dtype=f32)
         self.epoch_num = 0
         self.frame = 0
         self.last_mean_rewards = -100500.0
@@ -293,15 +309,56 @@ class A2CAgent:
             vms.eval()
         if self.normalize_advantage:
             advantages = (advantages - advantages.mean()) / (advantages.std() + 1e-8)
-        return {
+        fresh = {
             "old_values": values, "old_logp_actions": swap_and_flatten01(b["neglogpacs"]),
             "advantages": advantages, "returns": returns,
             "actions": swap_and_flatten01(b["actions"]), "obs": swap_and_flatten01(b["obses"]),
-            "mu": swap_and_flatten01(b["mus"]).clone(), "sigma": swap_and_flatten01(b["sigmas"]).clone(),
+            "mu": swap_and_flatten01(b["mus"]), "sigma": swap_and_flatten01(b["sigmas"]),
         }
+        # persistent dataset buffers: the captured minibatch updates read them by address
+        if self._data is None:
+            self._data = {k: torch.empty_like(v).contiguous() for k, v in fresh.items()}
+        for k, v in fresh.items():
+            self._data[k].copy_(v)
+        return self._data
+
+    def _lr_update_device(self, kl: torch.Tensor) -> None:
+        """AdaptiveScheduler.update on the device LR (legacy schedule, every minibatch)."""
+        s, lr = self.scheduler, self.lr_t
+        down = torch.clamp(lr / 1.5, min=s.min_lr)
+        lr1 = torch.where(kl > 2.0 * s.kl_threshold, down, lr)
+        up = torch.clamp(lr1 * 1.5, max=s.max_lr)
+        lr.copy_(torch.where(kl < 0.5 * s.kl_threshold, up, lr1))
+
+    def _minibatch_device(self, i: int) -> None:
+        """One minibatch update on the device, without host syncs (graph-capturable): PPO loss,
+        backward, GradScaler + fused Adam, mu / sigma write-back, adaptive LR, stats row i."""
+        s, e = i * self.minibatch_size, (i + 1) * self.minibatch_size
+        data = self._data
+        mb = {k: v[s:e] for k, v in data.items()}
+        a_loss, c_loss, ent, kl, cmu, csigma, b_loss = self.calc_gradients(mb)
+        data["mu"][s:e].copy_(cmu)
+        data["sigma"][s:e].copy_(csigma)
+        if self.scheduler is not None:
+            self._lr_update_device(kl)
+        self._mb_out[i].copy_(torch.stack([a_loss.float(), c_loss.float(), ent.float(), kl.float(),
+                                           b_loss.float()]))
+
+    def _minibatch_graphed(self, mode: int, i: int) -> None:
+        key = (mode, i)
+        g = self.upd_graphs.get(key)
+        if g is None:
+            torch.cuda.synchronize(self.device)
+            g = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(g):        # records the launches without running them
+                self._minibatch_device(i)
+            self.upd_graphs[key] = g
+        g.replay()
 
     def calc_gradients(self, mb: Dict[str, torch.Tensor]):
-        with torch.autocast(device_type=self.device.type, dtype=torch.float16, enabled=self.mixed_precision):
+        # autocast's weight cast cache off: every cast is a recorded launch (graph replay)
+        with torch.autocast(device_type=self.device.type, dtype=torch.float16, enabled=self.mixed_precision,
+                            cache_enabled=False):
             res = self.model.forward_train(mb["obs"], mb["actions"])
             nlp, values, entropy, mu, sigma = (res["prev_neglogp"], res["values"], res["entropy"],
                                                res["mus"], res["sigmas"])
@@ -337,6 +394,9 @@ class A2CAgent:
         return a_loss.detach(), c_loss.detach(), entropy.detach(), kl, mu.detach().float(), sigma.detach().float(), b_loss.detach()
 
     def update_lr(self, lr: float) -> None:
+        if self.lr_t is not None:      # device LR: one tensor shared by every param group
+            self.lr_t.fill_(lr)
+            lr = self.lr_t
         for g in self.optimizer.param_groups:
             g["lr"] = lr
 
@@ -346,24 +406,43 @@ class A2CAgent:
         t0 = time.perf_counter()
         self.model.train()
         data = self.prepare_dataset()
-        kls, a_l, c_l, b_l, ents = [], [], [], [], []
-        for mini_ep in range(self.mini_epochs):
-            ep_kls = []
-            for i in range(self.num_minibatches):
-                s, e = i * self.minibatch_size, (i + 1) * self.minibatch_size
-                mb = {k: v[s:e] for k, v in data.items()}
-                a_loss, c_loss, ent, kl, cmu, csigma, b_loss = self.calc_gradients(mb)
-                data["mu"][s:e] = cmu
-                data["sigma"][s:e] = csigma
-                ep_kls.append(kl); a_l.append(a_loss); c_l.append(c_loss); ents.append(ent); b_l.append(b_loss)
-                if self.scheduler is not None:
-                    self.last_lr = self.scheduler.update(self.last_lr, kl.item())
-                    self.update_lr(self.last_lr)
-            kls.append(torch.stack(ep_kls).mean())
-            if self.normalize_input:
-                self.model.running_mean_std.eval()   # statistics from the first mini-epoch only
         if self.device.type == "cuda":
-            torch.cuda.synchronize(self.device)
+            # device path: per-minibatch work is sync-free; epochs >= 2 replay captured graphs
+            # (epoch 1 runs eagerly: Adam state, BLAS handles and autocast are initialised)
+            graphed = self.graph_update and self.epoch_num >= 2
+            for mini_ep in range(self.mini_epochs):
+                mode = int(self.normalize_input and mini_ep == 0)   # obs statistics update on
+                for i in range(self.num_minibatches):
+                    if graphed:
+                        self._minibatch_graphed(mode, i)
+                    else:
+                        self._minibatch_device(i)
+                    self._mb_stats[mini_ep, i].copy_(self._mb_out[i])
+                if self.normalize_input:
+                    self.model.running_mean_std.eval()   # statistics from the first mini-epoch only
+            ms = self._mb_stats.mean(dim=(0, 1)).tolist()           # the update's one host sync
+            self.last_lr = float(self.lr_t.item())
+            a_loss_m, c_loss_m, ent_m, kl_m, b_loss_m = ms
+        else:
+            kls, a_l, c_l, b_l, ents = [], [], [], [], []
+            for mini_ep in range(self.mini_epochs):
+                ep_kls = []
+                for i in range(self.num_minibatches):
+                    s, e = i * self.minibatch_size, (i + 1) * self.minibatch_size
+                    mb = {k: v[s:e] for k, v in data.items()}
+                    a_loss, c_loss, ent, kl, cmu, csigma, b_loss = self.calc_gradients(mb)
+                    data["mu"][s:e] = cmu
+                    data["sigma"][s:e] = csigma
+                    ep_kls.append(kl); a_l.append(a_loss); c_l.append(c_loss); ents.append(ent); b_l.append(b_loss)
+                    if self.scheduler is not None:
+                        self.last_lr = self.scheduler.update(self.last_lr, kl.item())
+                        self.update_lr(self.last_lr)
+                kls.append(torch.stack(ep_kls).mean())
+                if self.normalize_input:
+                    self.model.running_mean_std.eval()   # statistics from the first mini-epoch only
+            a_loss_m, c_loss_m = torch.stack(a_l).mean().item(), torch.stack(c_l).mean().item()
+            b_loss_m, ent_m = torch.stack(b_l).mean().item(), torch.stack(ents).mean().item()
+            kl_m = torch.stack(kls).mean().item()
         update_time = time.perf_counter() - t0
         self.frame += self.batch_size
         st = {
@@ -371,9 +450,8 @@ class A2CAgent:
             "update_time": update_time,
             "fps_step_inference": self.batch_size / play_time,
             "fps_total": self.batch_size / (play_time + update_time),
-            "a_loss": torch.stack(a_l).mean().item(), "c_loss": torch.stack(c_l).mean().item(),
-            "b_loss": torch.stack(b_l).mean().item(), "entropy": torch.stack(ents).mean().item(),
-            "kl": torch.stack(kls).mean().item(), "lr": self.last_lr,
+            "a_loss": a_loss_m, "c_loss": c_loss_m, "b_loss": b_loss_m, "entropy": ent_m,
+            "kl": kl_m, "lr": self.last_lr,
             "mean_rewards": self.game_rewards.get_mean(), "mean_lengths": self.game_lengths.get_mean(),
             "games": self.game_rewards.current_size,
         }
@@ -424,7 +502,9 @@ class A2CAgent:
             self.optimizer.load_state_dict(ck["optimizer"])
         if "scaler" in ck:
             self.scaler.load_state_dict(ck["scaler"])
+        self.update_lr(self.last_lr)   # re-binds the device LR tensor to the param groups
         self.graph = None
+        self.upd_graphs = {}           # captured updates referenced the old optimizer state
 
 
 class A2CPlayer:

@@ -16,6 +16,9 @@ import torch.nn as nn
 
 from .ops import neglogp_torch
 
+# 0.5 + 0.5 log(2 pi), evaluated in float32 like rl_games' tensor expression
+_HALF_LOG_2PI_E = float((0.5 + 0.5 * torch.log(torch.tensor(2.0 * torch.pi, dtype=torch.float32))).item())
+
 _ACT = {"elu": nn.ELU, "relu": nn.ReLU, "tanh": nn.Tanh, "selu": nn.SELU, "None": nn.Identity,
         None: nn.Identity}
 
@@ -136,7 +139,8 @@ class ModelA2CContinuousLogStd(nn.Module):
     def forward_train(self, obs: torch.Tensor, prev_actions: torch.Tensor):
         mu, logstd, value = self.policy(obs)
         sigma = torch.exp(logstd)
-        entropy = (0.5 + 0.5 * torch.log(torch.tensor(2.0 * torch.pi, device=mu.device)) + logstd).sum(dim=-1)
+        # host constant, no tensor creation inside the step (graph-capturable)
+        entropy = (_HALF_LOG_2PI_E + logstd).sum(dim=-1)
         prev_neglogp = neglogp_torch(prev_actions, mu, sigma, logstd)
         return {"prev_neglogp": prev_neglogp, "values": value, "entropy": entropy, "mus": mu,
                 "sigmas": sigma}

@@ -23,7 +23,8 @@ def main():
     ap.add_argument("--num-envs", type=int, default=None)
     ap.add_argument("--epochs", type=int, default=6)
     ap.add_argument("--warmup", type=int, default=3)
-    ap.add_argument("--no-graph", action="store_true")
+    ap.add_argument("--no-graph", action="store_true", help="eager rollout and eager updates")
+    ap.add_argument("--no-graph-update", action="store_true", help="eager (sync-free) updates only")
     args = ap.parse_args()
     import torch
 
@@ -35,6 +36,7 @@ def main():
     register_env("rlgpu", lambda **kw: env)
     params = env.task_cfg["train"]["params"]
     params["config"]["graph_rollout"] = not args.no_graph
+    params["config"]["graph_update"] = not (args.no_graph or args.no_graph_update)
     n = env.num_envs
     agent = A2CAgent(RLGPUEnv("rlgpu", n), params, run_dir=os.path.join("/tmp", "bench_train"))
     agent.env_reset()
@@ -56,6 +58,7 @@ def main():
         "task": args.task, "num_envs": n, "horizon": agent.horizon,
         "minibatch": agent.minibatch_size, "mini_epochs": agent.mini_epochs,
         "mixed_precision": agent.mixed_precision, "graph_rollout": agent.graph is not None,
+        "graph_update": len(agent.upd_graphs) > 0,
         "units": params["network"]["mlp"]["units"], "epochs": args.epochs,
         "fps_total": round(frames / wall, 1), "fps_step_inference": round(frames / play, 1),
         "ms_per_epoch": round(1e3 * wall / args.epochs, 3),
