@@ -27,6 +27,11 @@ MI355X-first execution:
     graph launch instead of ~30 launches per env step; episode meters are accumulated on
     device as per-step (count, sum) pairs and folded into the host meters with one copy per
     epoch (no nonzero() host syncs in the loop);
+  * the minibatch update is sync-free — the learning rate is a device tensor the legacy
+    adaptive schedule updates in place (no kl.item() per minibatch), fused capturable Adam takes
+    it and GradScaler's found_inf / scale on the device, the dataset lives in persistent
+    buffers — and is captured once per (obs-statistics mode, minibatch index) into a HIP graph
+    replayed from epoch 2 on; the update's only host sync is the per-epoch stats read;
   * on CPU (BASELINE config 0) the same code runs eagerly with the torch statements of
     those ops.
 """
