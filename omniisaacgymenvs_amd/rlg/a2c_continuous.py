@@ -54,6 +54,31 @@ def _f(x) -> float:
     return float(x)
 
 
+_TUNINGS = os.path.join(os.path.dirname(os.path.abspath(__file__)), "tunableop_mi355x.csv")
+
+
+def _use_shipped_gemm_tunings() -> bool:
+    """Route the learner's GEMMs through TunableOp with the solutions measured on MI355X for
+    these shapes (rollout fp32 + update fp16 GEMMs of the 400-200-100 MLP at 4096 / 32768 rows:
+    rocBLAS / hipBLASLt solution per shape; tuning itself stays off). The file's validator lines
+    pin the torch / HIP / BLAS versions; on a mismatch TunableOp rejects it and the default
+    solutions run. Skipped when the user drives TunableOp through its environment variables."""
+    if os.environ.get("PYTORCH_TUNABLEOP_ENABLED") is not None or not os.path.exists(_TUNINGS):
+        return False
+    import shutil
+    import tempfile
+
+    from torch.cuda import tunable
+
+    # TunableOp may write its database back to the file it was given: hand it a private copy
+    path = os.path.join(tempfile.gettempdir(), f"mi_tunableop_{os.getpid()}.csv")
+    shutil.copyfile(_TUNINGS, path)
+    tunable.enable(True)
+    tunable.tuning_enable(False)
+    tunable.set_filename(path, insert_device_ordinal=False)
+    return bool(tunable.read_file(path))
+
+
 class AverageMeter:
     """rl_games torch_ext.AverageMeter: mean over the last max_size values, updated with
     batches (size, mean)."""
@@ -154,6 +179,8 @@ class A2CAgent:
         self.seed = int(params.get("seed", 42))
 
         torch.manual_seed(self.seed)
+        if self.device.type == "cuda" and bool(cfg.get("tunableop", True)):
+            _use_shipped_gemm_tunings()
         self.model = ModelA2CContinuousLogStd(self.num_obs, self.num_actions, params["network"],
                                               self.normalize_input, self.normalize_value).to(self.device)
         wd = float(cfg.get("weight_decay", 0.0))

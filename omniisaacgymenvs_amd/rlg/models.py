@@ -39,8 +39,11 @@ class RunningMeanStd(nn.Module):
 
     @torch.no_grad()
     def _update(self, x: torch.Tensor) -> None:
-        batch_mean = x.mean(0).double()
-        batch_var = x.var(0).double()          # unbiased, as torch.var's default
+        # per-feature moments as row reductions of the transposed batch ([C, B]: one contiguous
+        # row per feature) instead of strided column reductions over B
+        bv, bm = torch.var_mean(x.detach().transpose(0, 1).contiguous(), dim=1)  # unbiased
+        batch_mean = bm.double()
+        batch_var = bv.double()
         batch_count = float(x.shape[0])
         delta = batch_mean - self.running_mean
         tot = self.count + batch_count
