@@ -1,4 +1,5 @@
 #!/bin/bash
+# iteration loop: GPU tests, Humanoid / Ant bench, phase stamps, Humanoid PMC traffic passes
 source "$(dirname "$0")/gpu_lib.sh"
 run pytest_gpu 400 python -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread
 run bench_humanoid 200 python -u bench.py --steps 300 --warmup 50 --no-cpu-baseline --fuse-envs 0
