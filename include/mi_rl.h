@@ -52,6 +52,29 @@ int32_t mi_rl_sample_gauss(const float* mu, const float* logstd, int32_t logstd_
                            const int64_t* counter_base, uint64_t counter_offset, float* actions,
                            float* neglogp, void* stream);
 
+/* The PPO loss of rl_games a2c_continuous.calc_gradients (algos_torch/a2c_continuous.py: clipped
+ * surrogate, value loss — clipped when clip_value —, entropy, bound loss with soft bound 1.1,
+ * policy KL against the stored mu / sigma) fused for one minibatch of num_rows rows, together
+ * with the gradient of  grad_scale x loss  w.r.t. the network heads, for autograd to carry
+ * through the MLP:
+ *   mu [B,A], value [B]        network heads, f16 (mu_half / value_half = 1) or f32
+ *   logstd [A]                 the fixed-sigma log-std parameter (f32)
+ *   actions [B,A], old_logp, advantages, old_values, returns [B], old_mu, old_sigma [B,A]  f32
+ *   grad_scale                 device f32 scalar (GradScaler scale) or NULL (1)
+ * Outputs: grad_mu (dtype of mu), grad_value (dtype of value); grad_logstd_part [nblk][A] and
+ * sums_part [nblk][5] (a_loss, c_loss, entropy, b_loss, kl row sums) per 256-row block,
+ * nblk = ceil(B / 256), summed by the caller; mu_out / sigma_out [B,A] f32 = mu, exp(logstd)
+ * (may alias old_mu / old_sigma: each element is read before it is written).
+ * loss = mean(a) + 0.5 critic_coef mean(c) - entropy_coef mean(entropy) + bounds_coef mean(b). */
+int32_t mi_rl_ppo_loss(const void* mu, int32_t mu_half, const float* logstd, const void* value,
+                       int32_t value_half, const float* actions, const float* old_logp,
+                       const float* advantages, const float* old_values, const float* returns,
+                       const float* old_mu, const float* old_sigma, int32_t num_rows,
+                       int32_t num_actions, float e_clip, int32_t clip_value, float critic_coef,
+                       float entropy_coef, float bounds_coef, const float* grad_scale,
+                       void* grad_mu, void* grad_value, float* grad_logstd_part,
+                       float* sums_part, float* mu_out, float* sigma_out, void* stream);
+
 #ifdef __cplusplus
 }
 #endif

@@ -196,6 +196,11 @@ class A2CAgent:
             self.optimizer = torch.optim.Adam(self.model.parameters(), lr=self.last_lr, eps=1e-08,
                                               weight_decay=wd)
         self.scaler = torch.amp.GradScaler("cuda", enabled=self.mixed_precision)
+        if self.mixed_precision:     # materialise the device scale now (the fused loss reads it)
+            self.scaler.scale(torch.zeros((), device=self.device))
+        # loss + head gradients as one HIP launch (mi_rl_ppo_loss); needs the fixed log-std head
+        self.fused_loss = (self.device.type == "cuda" and bool(cfg.get("fused_loss", True))
+                           and self.model.a2c_network.fixed_sigma)
         self.sample_gen = torch.Generator(device="cpu").manual_seed(self.seed)
         self.sample_seed = (self.seed * 0x9E3779B97F4A7C15 + 1) & ((1 << 64) - 1)
 
@@ -368,9 +373,12 @@ class A2CAgent:
         s, e = i * self.minibatch_size, (i + 1) * self.minibatch_size
         data = self._data
         mb = {k: v[s:e] for k, v in data.items()}
-        a_loss, c_loss, ent, kl, cmu, csigma, b_loss = self.calc_gradients(mb)
-        data["mu"][s:e].copy_(cmu)
-        data["sigma"][s:e].copy_(csigma)
+        if self.fused_loss:        # mu / sigma written back by the loss kernel itself
+            a_loss, c_loss, ent, kl, b_loss = self._calc_gradients_fused(mb)
+        else:
+            a_loss, c_loss, ent, kl, cmu, csigma, b_loss = self.calc_gradients(mb)
+            data["mu"][s:e].copy_(cmu)
+            data["sigma"][s:e].copy_(csigma)
         if self.scheduler is not None:
             self._lr_update_device(kl)
         self._mb_out[i].copy_(torch.stack([a_loss.float(), c_loss.float(), ent.float(), kl.float(),
@@ -386,6 +394,35 @@ class A2CAgent:
                 self._minibatch_device(i)
             self.upd_graphs[key] = g
         g.replay()
+
+    def _optimizer_step(self) -> None:
+        if self.truncate_grads:
+            self.scaler.unscale_(self.optimizer)
+            nn.utils.clip_grad_norm_(self.model.parameters(), self.grad_norm)
+        self.scaler.step(self.optimizer)
+        self.scaler.update()
+
+    def _calc_gradients_fused(self, mb: Dict[str, torch.Tensor]):
+        """calc_gradients with the loss and its head gradients in one HIP launch
+        (mi_rl_ppo_loss): the MLP forward under autocast, the fused loss, autograd from the
+        heads down, then the same GradScaler / clip / Adam step. Writes mu / sigma into mb."""
+        net = self.model.a2c_network
+        with torch.autocast(device_type=self.device.type, dtype=torch.float16, enabled=self.mixed_precision,
+                            cache_enabled=False):
+            out = net.actor_mlp(self.model.norm_obs(mb["obs"]))
+            mu = net.mu(out)
+            value = net.value(out).view(-1)
+        gscale = self.scaler._scale if self.mixed_precision else None   # device scale, no sync
+        g_mu, g_val, g_ls, sums = ops.ppo_loss(
+            mu, net.sigma.detach(), value, mb, self.e_clip, self.clip_value, self.critic_coef,
+            self.entropy_coef, float(self.bounds_loss_coef or 0.0), gscale)
+        for p in self.model.parameters():
+            p.grad = None
+        torch.autograd.backward([mu, value], [g_mu, g_val])
+        net.sigma.grad = g_ls        # logstd = mu * 0 + sigma: the rows' log-std grads sum here
+        self._optimizer_step()
+        b_loss = sums[3] if self.bounds_loss_coef is not None else sums[3] * 0.0
+        return sums[0], sums[1], sums[2], sums[4], b_loss
 
     def calc_gradients(self, mb: Dict[str, torch.Tensor]):
         # autocast's weight cast cache off: every cast is a recorded launch (graph replay)
@@ -416,11 +453,7 @@ class A2CAgent:
         for p in self.model.parameters():
             p.grad = None
         self.scaler.scale(loss).backward()
-        if self.truncate_grads:
-            self.scaler.unscale_(self.optimizer)
-            nn.utils.clip_grad_norm_(self.model.parameters(), self.grad_norm)
-        self.scaler.step(self.optimizer)
-        self.scaler.update()
+        self._optimizer_step()
         with torch.no_grad():
             kl = policy_kl(mu.detach().float(), sigma.detach().float(), mb["mu"], mb["sigma"])
         return a_loss.detach(), c_loss.detach(), entropy.detach(), kl, mu.detach().float(), sigma.detach().float(), b_loss.detach()

@@ -45,6 +45,8 @@ def load_library() -> C.CDLL:
         lib.mi_rl_gae.argtypes = [vp, vp, vp, vp, vp, i32, i32, f, f, vp, vp, vp]
         lib.mi_rl_sample_gauss.restype = i32
         lib.mi_rl_sample_gauss.argtypes = [vp, vp, i32, i32, i32, u64, vp, u64, vp, vp, vp]
+        lib.mi_rl_ppo_loss.restype = i32
+        lib.mi_rl_ppo_loss.argtypes = [vp, i32, vp, vp, i32] + [vp] * 7 + [i32, i32, f, i32, f, f, f] + [vp] * 8
         _LIB = lib
     return _LIB
 
@@ -146,3 +148,41 @@ def sample_gauss(mu: torch.Tensor, logstd: torch.Tensor, seed: int,
                                         int(counter_offset), act.data_ptr(), nlp.data_ptr(),
                                         _stream(mu)), "mi_rl_sample_gauss")
     return act, nlp
+
+
+# ------------------------------------------------------------------------------ PPO loss
+def ppo_loss(mu: torch.Tensor, logstd: torch.Tensor, value: torch.Tensor, mb: dict,
+             e_clip: float, clip_value: bool, critic_coef: float, entropy_coef: float,
+             bounds_coef: float, grad_scale: Optional[torch.Tensor]):
+    """rl_games calc_gradients' loss, fused (mi_rl_ppo_loss): returns (grad_mu, grad_value,
+    grad_logstd [A], sums [5] = mean a_loss, c_loss, entropy, b_loss, kl) and writes mu /
+    exp(logstd) into mb["mu"] / mb["sigma"] (the next mini-epoch's KL reference). The gradients
+    are those of grad_scale x loss w.r.t. the heads; mu / value may be f16 (autocast)."""
+    B, A = mu.shape
+    for t, dt in ((mu, None), (value, None)):
+        if t.dtype not in (torch.float16, torch.float32) or not t.is_contiguous():
+            raise ValueError("ppo_loss: mu / value must be contiguous f16 or f32")
+    if value.numel() != B or logstd.numel() != A or logstd.dtype != torch.float32:
+        raise ValueError(f"ppo_loss: value {tuple(value.shape)} / logstd {tuple(logstd.shape)} vs mu {tuple(mu.shape)}")
+    keys = ("actions", "old_logp_actions", "advantages", "old_values", "returns", "mu", "sigma")
+    for k in keys:
+        t = mb[k]
+        if t.dtype != torch.float32 or not t.is_contiguous() or t.numel() not in (B, B * A):
+            raise ValueError(f"ppo_loss: mb[{k!r}] must be contiguous f32 with B or B*A elements")
+    if grad_scale is not None and (grad_scale.dtype != torch.float32 or grad_scale.numel() != 1):
+        raise ValueError("ppo_loss: grad_scale must be a 1-element f32 tensor")
+    nblk = (B + 255) // 256
+    g_mu = torch.empty_like(mu)
+    g_val = torch.empty_like(value)
+    part_ls = torch.empty((nblk, A), device=mu.device, dtype=torch.float32)
+    part_sums = torch.empty((nblk, 5), device=mu.device, dtype=torch.float32)
+    ls = logstd.contiguous()
+    _check(kernels().mi_rl_ppo_loss(
+        mu.data_ptr(), int(mu.dtype == torch.float16), ls.data_ptr(), value.data_ptr(),
+        int(value.dtype == torch.float16), mb["actions"].data_ptr(), mb["old_logp_actions"].data_ptr(),
+        mb["advantages"].data_ptr(), mb["old_values"].data_ptr(), mb["returns"].data_ptr(),
+        mb["mu"].data_ptr(), mb["sigma"].data_ptr(), B, A, float(e_clip), int(bool(clip_value)),
+        float(critic_coef), float(entropy_coef), float(bounds_coef), _ptr(grad_scale),
+        g_mu.data_ptr(), g_val.data_ptr(), part_ls.data_ptr(), part_sums.data_ptr(),
+        mb["mu"].data_ptr(), mb["sigma"].data_ptr(), _stream(mu)), "mi_rl_ppo_loss")
+    return g_mu, g_val, part_ls.sum(0), part_sums.sum(0) * (1.0 / B)

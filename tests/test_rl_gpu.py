@@ -125,6 +125,40 @@ def test_graph_update_matches_eager(gpu):
     env_g.close(); env_e.close()
 
 
+@pytest.mark.parametrize("mixed", [False, True])
+def test_fused_loss_matches_torch_loss(gpu, mixed):
+    """mi_rl_ppo_loss (one launch: loss terms, KL, head gradients) against the torch statement
+    of rl_games calc_gradients on the same minibatch and weights: losses / KL, the mu / sigma
+    write-back and every parameter gradient after autograd through the MLP."""
+    env, ag = _agent("Humanoid", 256, False)
+    ag.mixed_precision = mixed
+    if not mixed:
+        ag.scaler = torch.amp.GradScaler("cuda", enabled=False)
+    ag.env_reset()
+    ag.play_steps()
+    ag.model.train()
+    ag.model.running_mean_std.eval()     # freeze the obs statistics: both paths see the same
+    data = ag.prepare_dataset()
+    mb = {k: v[:2048] for k, v in data.items()}
+    mb_f = {k: v.clone() for k, v in mb.items()}
+    mb_t = {k: v.clone() for k, v in mb.items()}
+    mb_f["mu"] += 0.01                   # a non-trivial KL reference
+    mb_t["mu"] += 0.01
+    ag._optimizer_step = lambda: None    # keep the gradients, skip the update
+    a_f, c_f, e_f, kl_f, b_f = (x.item() for x in ag._calc_gradients_fused(mb_f))
+    g_f = [p.grad.detach().float().clone() for p in ag.model.parameters()]
+    a_t, c_t, e_t, kl_t, cmu, csig, b_t = ag.calc_gradients(mb_t)
+    g_t = [p.grad.detach().float().clone() for p in ag.model.parameters()]
+    tol = 2e-2 if mixed else 1e-4
+    for x, y in ((a_f, a_t.item()), (c_f, c_t.item()), (e_f, e_t.item()), (kl_f, kl_t.item()), (b_f, b_t.item())):
+        assert math.isclose(x, y, rel_tol=tol, abs_tol=1e-6), (x, y)
+    torch.testing.assert_close(mb_f["mu"], cmu, rtol=tol, atol=1e-5)
+    torch.testing.assert_close(mb_f["sigma"], csig, rtol=1e-6, atol=1e-7)
+    for (name, _), gf, gt in zip(ag.model.named_parameters(), g_f, g_t):
+        torch.testing.assert_close(gf, gt, rtol=tol, atol=tol * gt.abs().max().item() + 1e-8, msg=name)
+    env.close()
+
+
 def test_ppo_learns_cartpole(gpu):
     env, ag = _agent("Cartpole", 4096, True, seed=5)
     ag.env_reset()
