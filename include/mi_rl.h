@@ -4,12 +4,14 @@
  *
  * The reference trains with rl-games 1.5.2 (setup.py:17; not vendored under /root/reference,
  * absent from this image). Its call sites are scripts/rlgames_train.py:67-84 (Runner over the
- * 'rlgpu' env) and the hyper-parameters in cfg/train/{Humanoid,Ant,Cartpole}PPO.yaml. The two
- * per-sample loops of its a2c_continuous agent that are not GEMMs are fused here:
+ * 'rlgpu' env) and the hyper-parameters in cfg/train/{Humanoid,Ant,Cartpole}PPO.yaml. The
+ * per-sample work of its a2c_continuous agent that is not GEMMs is fused here:
  *   mi_rl_gae          — rl_games common/a2c_common.py discount_values (GAE(gamma, tau)
  *                        over the horizon, returns = advantages + values)
  *   mi_rl_sample_gauss — rl_games algos_torch/models.py ModelA2CContinuousLogStd forward in
  *                        eval mode: action ~ Normal(mu, exp(logstd)) and its neg-log-prob
+ *   mi_rl_ppo_loss     — rl_games algos_torch/a2c_continuous.py calc_gradients: the PPO loss
+ *                        terms, the policy KL and the loss gradient w.r.t. the network heads
  * The MLP GEMMs stay in hipBLASLt (torch.nn.Linear).
  *
  * Conventions: as mi_sim.h — 0 on success or a negative MI_E_* code (mi_rl_last_error());

@@ -1,10 +1,10 @@
 // mi_rl.hip — fused per-sample kernels of the PPO learner (include/mi_rl.h).
 //
-// Both ops are HBM/latency-trivial elementwise work next to the learner's GEMMs; they exist
-// so a rollout step (policy GEMMs + sampling + env step) and the GAE pass are a handful of
-// stream-ordered launches that a HIP graph can capture, instead of ~15 small torch kernels
-// each. One lane per env row: rows are independent, and every access of a lane walks its own
-// row (GAE: time-major columns, coalesced across lanes).
+// The ops are HBM/latency-trivial elementwise work next to the learner's GEMMs; they exist
+// so a rollout step (policy GEMMs + sampling + env step), the GAE pass and a minibatch's loss
+// are a handful of stream-ordered launches that a HIP graph can capture, instead of tens of
+// small torch kernels each. One lane per row: rows are independent, and every access of a lane
+// walks its own row (GAE: time-major columns, coalesced across lanes).
 #include <hip/hip_runtime.h>
 
 #include <cmath>
