@@ -76,6 +76,16 @@ def main():
             for k in ("SQ_INSTS_VALU", "SQ_INSTS_SALU", "SQ_INSTS_LDS", "SQ_INSTS_VMEM_RD", "SQ_INSTS_VMEM_WR"):
                 if k in sq:
                     lines.append(f"{k:24s} {sq[k] / w:9.1f} per wave (per env-step)")
+            if "GRBM_GUI_ACTIVE" in sq:
+                # occupancy (MI355X_MICROARCH.md: GRBM_GUI_ACTIVE sums the 8 XCDs; SQ cycle
+                # counters are quad-cycles): mean resident waves per CU over the dispatch
+                kcyc = sq["GRBM_GUI_ACTIVE"] / 8.0
+                waves_cu = 4.0 * wc / (kcyc * 256.0)
+                lines.append(f"{'kernel cycles / XCD':24s} {kcyc:.4g}")
+                lines.append(f"{'mean wave lifetime':24s} {4.0 * wc / w:.4g} cycles")
+                lines.append(f"{'resident waves / CU':24s} {waves_cu:5.2f} (mean over the dispatch)")
+                lines.append(f"{'occupancy':24s} {100 * waves_cu / 8:5.1f} % of the kernel's 8 waves/CU "
+                             f"(2/SIMD: VGPR + LDS), {100 * waves_cu / 32:5.1f} % of the CDNA4 32 waves/CU cap")
         with open(os.path.join(dst, "sq_counters_humanoid.txt"), "w") as f:
             f.write("\n".join(lines) + "\n")
     for name in ("stamps_humanoid", "stamps_ant", "bench_default"):
