@@ -201,6 +201,8 @@ class A2CAgent:
         # loss + head gradients as one HIP launch (mi_rl_ppo_loss); needs the fixed log-std head
         self.fused_loss = (self.device.type == "cuda" and bool(cfg.get("fused_loss", True))
                            and self.model.a2c_network.fixed_sigma)
+        # split-K weight gradients of the minibatch GEMMs (models.linear_train); 1 = one GEMM
+        self.wgrad_splits = int(cfg.get("wgrad_splits", 32))
         self.sample_gen = torch.Generator(device="cpu").manual_seed(self.seed)
         self.sample_seed = (self.seed * 0x9E3779B97F4A7C15 + 1) & ((1 << 64) - 1)
 
@@ -409,9 +411,8 @@ class A2CAgent:
         net = self.model.a2c_network
         with torch.autocast(device_type=self.device.type, dtype=torch.float16, enabled=self.mixed_precision,
                             cache_enabled=False):
-            out = net.actor_mlp(self.model.norm_obs(mb["obs"]))
-            mu = net.mu(out)
-            value = net.value(out).view(-1)
+            mu, value = net.heads_train(self.model.norm_obs(mb["obs"]), self.wgrad_splits)
+            value = value.view(-1)
         gscale = self.scaler._scale if self.mixed_precision else None   # device scale, no sync
         g_mu, g_val, g_ls, sums = ops.ppo_loss(
             mu, net.sigma.detach(), value, mb, self.e_clip, self.clip_value, self.critic_coef,
