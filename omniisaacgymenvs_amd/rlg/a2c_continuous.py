@@ -95,7 +95,7 @@ class AverageMeter:
         old_size = min(self.max_size - size, self.current_size)
         size_sum = old_size + size
         self.current_size = size_sum
-        self.mean = (self.mean * old_size + mean * size) / size_sum
+        self.mean = float((self.mean * old_size + mean * size) / size_sum)
 
     def clear(self) -> None:
         self.current_size = 0
@@ -547,9 +547,11 @@ class A2CAgent:
 
     # ------------------------------------------------------------------ checkpoints
     def get_full_state_weights(self) -> Dict:
-        return {"model": self.model.state_dict(), "epoch": self.epoch_num, "frame": self.frame,
-                "optimizer": self.optimizer.state_dict(), "last_mean_rewards": self.last_mean_rewards,
-                "scaler": self.scaler.state_dict(), "last_lr": self.last_lr}
+        # plain Python scalars only: the file must load with torch.load(weights_only=True)
+        return {"model": self.model.state_dict(), "epoch": int(self.epoch_num), "frame": int(self.frame),
+                "optimizer": self.optimizer.state_dict(),
+                "last_mean_rewards": float(self.last_mean_rewards),
+                "scaler": self.scaler.state_dict(), "last_lr": float(self.last_lr)}
 
     def save(self, fn: str) -> str:
         os.makedirs(os.path.dirname(fn) or ".", exist_ok=True)
@@ -577,7 +579,11 @@ class A2CPlayer:
     """rl_games PpoPlayerContinuous: deterministic policy (mu) rollouts of a checkpoint."""
 
     def __init__(self, env, params: Dict) -> None:
-        self.agent = A2CAgent(env, params)
+        # a player never trains: the training batch geometry (minibatch | horizon x actors) of
+        # the config does not constrain it (play runs typically use few envs)
+        cfg = dict(params["config"])
+        cfg["minibatch_size"] = int(cfg["horizon_length"]) * int(cfg["num_actors"])
+        self.agent = A2CAgent(env, {**params, "config": cfg})
         self.env = env
 
     def restore(self, fn: str) -> None:

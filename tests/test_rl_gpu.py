@@ -159,6 +159,26 @@ def test_fused_loss_matches_torch_loss(gpu, mixed):
     env.close()
 
 
+def test_train_checkpoint_resume_play(gpu, tmp_path, monkeypatch):
+    """scripts/rlgames_train end to end (rlgames_train.py:67-84 flow): train a few epochs with
+    best-checkpoint saving, resume training from the checkpoint (optimizer state with the device
+    LR, fresh graphs), then play it (test=True)."""
+    import os
+
+    from omniisaacgymenvs_amd.scripts.rlgames_train import main
+
+    monkeypatch.chdir(tmp_path)
+    base = ["task=Cartpole", "num_envs=512", "train.params.config.minibatch_size=2048",
+            "train.params.config.save_best_after=1"]
+    assert main(base + ["train.params.config.max_epochs=4"]) == 0
+    ck = os.path.join("runs", "Cartpole", "nn", "Cartpole.pth")
+    assert os.path.exists(ck)
+    sd = torch.load(ck, map_location="cuda:0", weights_only=True)
+    assert sd["epoch"] >= 1 and "optimizer" in sd and "scaler" in sd
+    assert main(base + ["train.params.config.max_epochs=6", f"checkpoint={ck}"]) == 0
+    assert main(["task=Cartpole", "num_envs=64", "test=True", f"checkpoint={ck}"]) == 0
+
+
 def test_ppo_learns_cartpole(gpu):
     env, ag = _agent("Cartpole", 4096, True, seed=5)
     ag.env_reset()
