@@ -40,10 +40,11 @@ def parse():
     ap.add_argument("--num-envs", type=int, default=4096, help="envs per GPU")
     ap.add_argument("--seed", type=int, default=42)
     ap.add_argument("--gather-every", type=int, default=32, help="rollout gather period (N>1)")
-    ap.add_argument("--cpu-seconds", type=float, default=10.0, help="CPU baseline sample budget")
+    ap.add_argument("--cpu-seconds", type=float, default=30.0,
+                    help="CPU baseline sample budget (split over the 1 / 4 / all-thread legs)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--modular", action="store_true", help="method-by-method path, not fused")
-    ap.add_argument("--fuse-envs", type=int, default=262144,
+    ap.add_argument("--fuse-envs", type=int, default=1048576,
                     help="envs of the obs/reward-fuse HBM roofline side measurement (0: skip)")
     return ap.parse_args()
 

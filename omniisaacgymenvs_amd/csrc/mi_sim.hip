@@ -68,6 +68,7 @@ struct mi_sim {
     float* rows = nullptr;  // per-env global constraint-row slab of the wave path
     size_t lds_bytes = 0;
     void* kp_dev = nullptr;  // device copy of KParams (wave path)
+    int num_cu = 0;          // compute units of the device (queried on first use)
     std::vector<float> lower, upper;  // host copy for mi_sim_info
     std::vector<void*> allocs;
 };
@@ -297,24 +298,160 @@ __global__ __launch_bounds__(64) void k_loco_post_tiled(DevModel m, DevState st,
     }
 }
 
+// k_loco_post_tiled<32, true> with the HBM latency hidden behind the math: each workgroup walks
+// the tiles t = blockIdx.x, + gridDim.x, ... (grid = resident workgroups) and, while it computes
+// tile t from LDS, holds the global loads of tile t + gridDim.x in registers (records, action
+// rows, per-env scalars). The counters of the one-tile kernel showed 62 % of wave cycles
+// waiting on memory at 2 resident workgroups per SIMD (LDS-bound). Same arithmetic and
+// write order per env as k_loco_post_tiled<32, true> (bit-identical outputs).
+// Host-checked: es % 4 == 0, es <= 128 (MI_PIPE_R float4 per lane), 1 <= A <= 32.
+constexpr int MI_PIPE_R = 16;   // 32 records x 128 floats / 4 / 64 lanes
+constexpr int MI_PIPE_A = 16;   // 32 envs x 32 actions / 64 lanes
+// floor(x / d) for 0 <= x < 4096, 1 <= d <= 128: (x * ceil(2^20 / d)) >> 20 (exact there)
+MI_D int div_small(int x, unsigned magic) { return (int)(((unsigned)x * magic) >> 20); }
+
+__global__ __launch_bounds__(64) void k_loco_post_pipe(DevModel m, DevState st, DevTask tp,
+                                                      const float* __restrict__ actions,
+                                                      float* obs, float* rew, int64_t* reset_buf,
+                                                      int64_t* progress_buf, float* pot,
+                                                      float* prev) {
+    constexpr int TE = 32;
+    extern __shared__ __attribute__((aligned(16))) float sm[];
+    const int lane = threadIdx.x;
+    const int O = tp.O, A = tp.A, D = m.D, S = m.S, es = st.es, N = st.N;
+    const int ntiles = (N + TE - 1) / TE;
+    const int k0 = 13 + 2 * D, s0 = 13 + 3 * D, ns = 6 * S, PC = k0 + ns + 1;
+    const int ka = 12 + 2 * D + ns;                        // obs column of actions[0]
+    const unsigned mag_es = ((1u << 20) + es - 1) / es, mag_a = ((1u << 20) + A - 1) / A;
+    float* srec = sm;
+    float* sobs = sm + TE * PC;
+    float* sterm = sobs + TE * O;                          // [TE][3] sums
+    float* spot = sterm + 3 * TE;                          // [TE] potentials (in / out)
+    float* sprev = spot + TE;                              // [TE] prev_potentials (out)
+    float4 rr[MI_PIPE_R];
+    float ra[MI_PIPE_A];
+    int64_t pg = 0, rs = 0;
+    int nf = 0;
+    float pt = 0.0f;
+    auto issue = [&](int t) {   // global loads of tile t into registers (no wait here)
+        const int e0 = t * TE, n = min(TE, N - e0);
+        const int c4 = n * es / 4, ca = n * A;
+        const float4* s4 = (const float4*)(st.root_pos + (size_t)e0 * es);
+        const float* ga = actions + (size_t)e0 * A;
+#pragma unroll
+        for (int r = 0; r < MI_PIPE_R; ++r) {
+            const int k = lane + 64 * r;
+            if (k < c4) rr[r] = s4[k];
+        }
+#pragma unroll
+        for (int r = 0; r < MI_PIPE_A; ++r) {
+            const int k = lane + 64 * r;
+            if (k < ca) ra[r] = ga[k];
+        }
+        if (lane < n) {
+            const int i = e0 + lane;
+            pg = progress_buf[i];
+            rs = reset_buf[i];
+            nf = st.nan_flag[i];
+            pt = pot[i];
+        }
+    };
+    int t = blockIdx.x;
+    if (t < ntiles) issue(t);
+    for (; t < ntiles; t += gridDim.x) {
+        const int e0 = t * TE, n = min(TE, N - e0);
+        {   // registers -> LDS: compact records, actions into the obs rows' action columns
+            const int c4 = n * es / 4, ca = n * A;
+#pragma unroll
+            for (int r = 0; r < MI_PIPE_R; ++r) {
+                const int k = lane + 64 * r;
+                if (k < c4) {
+                    const float vv[4] = {rr[r].x, rr[r].y, rr[r].z, rr[r].w};
+                    const int f0 = 4 * k, e = div_small(f0, mag_es), c0 = f0 - e * es;
+#pragma unroll
+                    for (int q = 0; q < 4; ++q) {
+                        const int c = c0 + q;
+                        if (c < k0) srec[e * PC + c] = vv[q];
+                        else if (c >= s0 && c < s0 + ns) srec[e * PC + k0 + (c - s0)] = vv[q];
+                    }
+                }
+            }
+#pragma unroll
+            for (int r = 0; r < MI_PIPE_A; ++r) {
+                const int k = lane + 64 * r;
+                if (k < ca) {
+                    const int e = div_small(k, mag_a);
+                    sobs[e * O + ka + (k - e * A)] = ra[r];
+                }
+            }
+        }
+        const int64_t progress = pg + 1, rb = rs;          // rl_task.py:242
+        const int nflag = nf;
+        if (lane < n) spot[lane] = pt;
+        __syncthreads();
+        if (t + (int)gridDim.x < ntiles) issue(t + gridDim.x);   // in flight during the math
+        DevState v = st;                    // the tile's envs, viewed in LDS
+        v.fs = 1; v.es = PC;
+        v.root_pos = srec; v.root_quat = srec + 3; v.root_vel = srec + 7;
+        v.q = srec + 13; v.qd = srec + 13 + D; v.sens = srec + k0;
+        // lanes 0..31: root-frame block of env `lane`; lanes 32..63: per-DOF / sensor block and
+        // the reward's DOF-order sums of env `lane - 32` (as k_loco_post_tiled<32, true>)
+        const int e = lane & 31;
+        float* R = sobs + (size_t)e * O;
+        if (e < n) {
+            if (lane < 32) {
+                loco_obs_root(v, tp, e, R, spot, sprev);
+            } else {
+                loco_obs_dof(m, v, tp, e, R + ka, INFINITY, R);   // actions already in place
+                const LocoTerms lt = loco_reward_terms(tp, D, R, R + ka);
+                sterm[3 * e] = lt.limit_cost; sterm[3 * e + 1] = lt.act_cost; sterm[3 * e + 2] = lt.elec;
+            }
+        }
+        __syncthreads();
+        if (lane < n) {
+            const int i = e0 + lane;
+            const LocoTerms lt{sterm[3 * lane], sterm[3 * lane + 1], sterm[3 * lane + 2]};
+            const float p_new = spot[lane], p_old = sprev[lane];
+            rew[i] = loco_reward_total(tp, R[0], R[10], R[11], p_new, p_old, lt);
+            pot[i] = p_new;
+            prev[i] = p_old;
+            int64_t d = loco_done(tp, R[0], rb, progress);
+            if (nflag) {                                                // nan_guard
+                st.nan_flag[i] = 0;
+                atomicAdd(st.nan_total, 1ull);
+                d = 1;
+            }
+            reset_buf[i] = d;
+            progress_buf[i] = progress;
+        }
+        __syncthreads();
+        float* dst = obs + (size_t)e0 * O;
+        const int cnt = n * O;
+        if ((((uintptr_t)dst) & 15) == 0 && (cnt & 3) == 0) {
+            for (int k = lane; k < cnt / 4; k += 64)
+                ((float4*)dst)[k] = make_float4(sobs[4 * k], sobs[4 * k + 1], sobs[4 * k + 2], sobs[4 * k + 3]);
+        } else {
+            for (int k = lane; k < cnt; k += 64) dst[k] = sobs[k];
+        }
+        __syncthreads();                    // the next tile overwrites the LDS tiles
+    }
+}
+
 static size_t post_tile_lds(int te, bool stage, int es, int A, int O, int D, int S) {
     if (te == 32 && stage)   // compact record tile + obs tile + reward sums
         return sizeof(float) * (size_t)(te * (13 + 2 * D + 6 * S + 1) + te * O + 3 * te);
     return sizeof(float) * (size_t)(te * (es + 1) + te * (A + 1) + (stage ? te * O : 0));
 }
 
-// variant of the tiled post-step (MI_POST_TILE=64s|64d|32s|32d, default below)
+// variant of the tiled post-step (MI_POST_TILE=32p|64s|64d|32s|32d, read per launch so a test
+// can compare variants in one process; default 32p = k_loco_post_pipe)
 static int post_tile_variant() {
-    static int v = -1;
-    if (v < 0) {
-        const char* e = getenv("MI_POST_TILE");
-        v = 2;   // 32s
-        if (e && !strcmp(e, "64s")) v = 0;
-        if (e && !strcmp(e, "64d")) v = 1;
-        if (e && !strcmp(e, "32s")) v = 2;
-        if (e && !strcmp(e, "32d")) v = 3;
-    }
-    return v;
+    const char* e = getenv("MI_POST_TILE");
+    if (e && !strcmp(e, "64s")) return 0;
+    if (e && !strcmp(e, "64d")) return 1;
+    if (e && !strcmp(e, "32s")) return 2;
+    if (e && !strcmp(e, "32d")) return 3;
+    return 4;   // 32p
 }
 
 // the three task methods as separate kernels, for tasks that override some of them
@@ -1185,7 +1322,35 @@ int mi_task_post_step(mi_sim* s, const float* actions, float* obs, float* rew, i
     NEED(s); NEED_TASK(s); NEED(obs); NEED(rew); NEED(reset_buf); NEED(progress_buf);
     if (s->tp.kind != MI_TASK_CARTPOLE) { NEED(actions); NEED(potentials); NEED(prev_potentials); }
     HIP_TRY(hipSetDevice(s->device));
-    const int var = post_tile_variant();
+    int var = post_tile_variant();
+    if (var == 4) {   // 32p: several tiles per resident workgroup, next tile's loads in flight
+        const size_t tile = post_tile_lds(32, true, s->ds.es, s->tp.A, s->tp.O, s->dm.D, s->dm.S) +
+                            2 * 32 * sizeof(float);
+        const int es = s->ds.es;
+        if (s->tp.kind != MI_TASK_CARTPOLE && s->ds.fs == 1 && es % 4 == 0 && es <= 128 &&
+            s->tp.A >= 1 && s->tp.A <= 32 && tile <= 64 * 1024) {
+            if (s->num_cu <= 0)
+                HIP_TRY(hipDeviceGetAttribute(&s->num_cu, hipDeviceAttributeMultiprocessorCount, s->device));
+            const int ntiles = (s->N + 31) / 32;
+            // one resident round: workgroups per CU as registers and LDS allow together
+            int per_cu = 0;
+            HIP_TRY(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k_loco_post_pipe, 64, tile));
+            int grid = std::min(ntiles, s->num_cu * std::max(1, per_cu));
+            const char* g = getenv("MI_POST_GRID");
+            if (g) grid = std::max(1, std::min(grid, atoi(g)));
+            // below ~8 tiles per resident workgroup the overlap does not pay for the one-tile
+            // kernel's higher residency (67 VGPRs vs 253; measured: Ant 262 K envs 2.82 vs
+            // 2.52 TB/s one-tile, Humanoid / Ant 1 M envs 2.09 / 2.59 vs 2.78 / 2.80 TB/s piped)
+            if (!g && ntiles < 8 * grid) goto one_tile;
+            hipLaunchKernelGGL(k_loco_post_pipe, dim3(grid), dim3(64), tile, STREAM(stream), s->dm,
+                               s->ds, s->tp, actions, obs, rew, reset_buf, progress_buf, potentials,
+                               prev_potentials);
+            LAUNCH_CHECK();
+            return MI_OK;
+        }
+    one_tile:
+        var = 2;      // shapes / sizes the pipelined kernel does not take: the one-tile kernel
+    }
     const int te = var < 2 ? 64 : 32;
     const bool stage = (var & 1) == 0;
     const size_t tile = post_tile_lds(te, stage, s->ds.es, s->tp.A, s->tp.O, s->dm.D, s->dm.S);

@@ -294,3 +294,43 @@ def test_self_collision_active_on_device(gpu):
         touching += sum(orc.self_min_gap(e) < 0.02 for e in range(0, 256, 8))
     assert touching > 0
     env.close()
+
+
+@pytest.mark.parametrize("name", ["Humanoid", "Ant"])
+def test_pipelined_post_step_equals_one_tile(gpu, monkeypatch, name):
+    """k_loco_post_pipe (MI_POST_TILE=32p: each workgroup walks several 32-env tiles and holds
+    the next tile's loads in registers) is bit-identical to the one-tile kernel (32s). A grid of
+    7 workgroups over 4113 envs forces many tiles per workgroup and a ragged last tile."""
+    env = make_env(name, num_envs=4113, device="cuda:0", seed=5)
+    t = env.task
+    env.reset()
+    for k in range(3):
+        env.step(rand_actions(t.num_envs, t.num_actions, 40 + k).to("cuda:0"))
+    t.actions = rand_actions(t.num_envs, t.num_actions, 50).to("cuda:0")
+    t.progress_buf[:] = torch.randint(0, 1000, (t.num_envs,), device="cuda:0")
+    t.reset_buf[::3] = 1
+    torch.cuda.synchronize()
+    bufs = ("obs_buf", "rew_buf", "reset_buf", "progress_buf", "potentials", "prev_potentials")
+    start = {b: getattr(t, b).clone() for b in bufs}
+    h, s = t.get_robot().handle, t.get_robot().stream()
+    out = {}
+    for var, grid in (("32s", None), ("32p", "7"), ("32p", None)):
+        for b in bufs:
+            getattr(t, b).copy_(start[b])
+        monkeypatch.setenv("MI_POST_TILE", var)
+        if grid:
+            monkeypatch.setenv("MI_POST_GRID", grid)
+        else:
+            monkeypatch.delenv("MI_POST_GRID", raising=False)
+        N.check(N.lib().mi_task_post_step(h, t.actions.data_ptr(), t.obs_buf.data_ptr(),
+                                          t.rew_buf.data_ptr(), t.reset_buf.data_ptr(),
+                                          t.progress_buf.data_ptr(), t.potentials.data_ptr(),
+                                          t.prev_potentials.data_ptr(), s), "mi_task_post_step")
+        torch.cuda.synchronize()
+        out[(var, grid)] = {b: getattr(t, b).clone() for b in bufs}
+    ref = out[("32s", None)]
+    assert not torch.equal(ref["obs_buf"], start["obs_buf"])
+    for key in (("32p", "7"), ("32p", None)):
+        for b in bufs:
+            assert torch.equal(out[key][b], ref[b]), (key, b)
+    env.close()

@@ -48,7 +48,7 @@ def measure(task_name: str, n: int, launches: int = 30, env=None) -> dict:
     gbs = B * n / (ms * 1e-3) / 1e9
     if own:
         env.close()
-    return {"kernel": "k_loco_post_tiled<" + os.environ.get("MI_POST_TILE", "32s") + ">", "task": task_name, "num_envs": n, "kernel_ms": round(ms, 4),
+    return {"kernel": ("k_loco_post_pipe<" if os.environ.get("MI_POST_TILE", "32p") == "32p" else "k_loco_post_tiled<") + os.environ.get("MI_POST_TILE", "32p") + ">", "task": task_name, "num_envs": n, "kernel_ms": round(ms, 4),
             "algo_bytes_per_env": B, "achieved": round(gbs, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
             "frac": round(gbs / HBM_PEAK_GBS, 4)}
 
