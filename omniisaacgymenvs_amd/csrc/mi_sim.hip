@@ -356,6 +356,12 @@ __global__ __launch_bounds__(64) void k_loco_post_pipe(DevModel m, DevState st, 
             pt = pot[i];
         }
     };
+    // lane constants of the element-wise obs phase (1 <= D, 6S <= 64: host-checked)
+    const int dof_pe = 64 / D, dof_le = lane / D, dof_j = lane - dof_le * D;
+    const bool dof_lane = dof_le < dof_pe;
+    const float dof_lo = dof_lane ? m.lower[dof_j + 1] : 0.0f, dof_hi = dof_lane ? m.upper[dof_j + 1] : 1.0f;
+    const int sen_pe = ns > 0 ? 64 / ns : 0, sen_le = ns > 0 ? lane / ns : 0, sen_c = lane - sen_le * ns;
+    const bool sen_lane = ns > 0 && sen_le < sen_pe;
     int t = blockIdx.x;
     if (t < ntiles) issue(t);
     for (; t < ntiles; t += gridDim.x) {
@@ -394,23 +400,25 @@ __global__ __launch_bounds__(64) void k_loco_post_pipe(DevModel m, DevState st, 
         v.fs = 1; v.es = PC;
         v.root_pos = srec; v.root_quat = srec + 3; v.root_vel = srec + 7;
         v.q = srec + 13; v.qd = srec + 13 + D; v.sens = srec + k0;
-        // lanes 0..31: root-frame block of env `lane`; lanes 32..63: per-DOF / sensor block and
-        // the reward's DOF-order sums of env `lane - 32` (as k_loco_post_tiled<32, true>)
-        const int e = lane & 31;
-        float* R = sobs + (size_t)e * O;
-        if (e < n) {
-            if (lane < 32) {
-                loco_obs_root(v, tp, e, R, spot, sprev);
-            } else {
-                loco_obs_dof(m, v, tp, e, R + ka, INFINITY, R);   // actions already in place
-                const LocoTerms lt = loco_reward_terms(tp, D, R, R + ka);
-                sterm[3 * e] = lt.limit_cost; sterm[3 * e + 1] = lt.act_cost; sterm[3 * e + 2] = lt.elec;
+        // get_observations per-DOF and sensor entries (locomotion.py:226-228), the arithmetic of
+        // loco_obs_dof, on all 64 lanes: lane = (env slot, column), the column a lane constant
+        if (dof_lane)
+            for (int e = dof_le; e < n; e += dof_pe) {
+                const float* r = srec + e * PC;
+                float* o = sobs + e * O;
+                o[12 + dof_j] = ref_unscale(r[13 + dof_j], dof_lo, dof_hi);
+                o[12 + D + dof_j] = r[13 + D + dof_j] * tp.dof_vel_scale;
             }
-        }
+        if (sen_lane)
+            for (int e = sen_le; e < n; e += sen_pe)
+                sobs[e * O + 12 + 2 * D + sen_c] = srec[e * PC + k0 + sen_c] * tp.contact_force_scale;
         __syncthreads();
+        // root-frame block and the reward's DOF-order sums, one lane per env
         if (lane < n) {
             const int i = e0 + lane;
-            const LocoTerms lt{sterm[3 * lane], sterm[3 * lane + 1], sterm[3 * lane + 2]};
+            float* R = sobs + (size_t)lane * O;
+            loco_obs_root(v, tp, lane, R, spot, sprev);
+            const LocoTerms lt = loco_reward_terms(tp, D, R, R + ka);
             const float p_new = spot[lane], p_old = sprev[lane];
             rew[i] = loco_reward_total(tp, R[0], R[10], R[11], p_new, p_old, lt);
             pot[i] = p_new;
@@ -1328,7 +1336,8 @@ int mi_task_post_step(mi_sim* s, const float* actions, float* obs, float* rew, i
                             2 * 32 * sizeof(float);
         const int es = s->ds.es;
         if (s->tp.kind != MI_TASK_CARTPOLE && s->ds.fs == 1 && es % 4 == 0 && es <= 128 &&
-            s->tp.A >= 1 && s->tp.A <= 32 && tile <= 64 * 1024) {
+            s->tp.A >= 1 && s->tp.A <= 32 && s->dm.D >= 1 && s->dm.D <= 64 && 6 * s->dm.S <= 64 &&
+            tile <= 64 * 1024) {
             if (s->num_cu <= 0)
                 HIP_TRY(hipDeviceGetAttribute(&s->num_cu, hipDeviceAttributeMultiprocessorCount, s->device));
             const int ntiles = (s->N + 31) / 32;
@@ -1338,10 +1347,11 @@ int mi_task_post_step(mi_sim* s, const float* actions, float* obs, float* rew, i
             int grid = std::min(ntiles, s->num_cu * std::max(1, per_cu));
             const char* g = getenv("MI_POST_GRID");
             if (g) grid = std::max(1, std::min(grid, atoi(g)));
-            // below ~8 tiles per resident workgroup the overlap does not pay for the one-tile
-            // kernel's higher residency (67 VGPRs vs 253; measured: Ant 262 K envs 2.82 vs
-            // 2.52 TB/s one-tile, Humanoid / Ant 1 M envs 2.09 / 2.59 vs 2.78 / 2.80 TB/s piped)
-            if (!g && ntiles < 8 * grid) goto one_tile;
+            // with one tile per resident workgroup there is nothing to overlap: the one-tile
+            // kernel (67 VGPRs vs 253). Measured crossover (fuse_roofline, MI_POST_PIPE_MIN):
+            // Humanoid 131 K envs 0.039 vs 0.044 ms, 262 K 2.94 vs 2.49 TB/s piped vs one-tile.
+            const char* pm = getenv("MI_POST_PIPE_MIN");   // tiles per workgroup (tuning)
+            if (!g && ntiles < (pm ? atoi(pm) : 2) * grid) goto one_tile;
             hipLaunchKernelGGL(k_loco_post_pipe, dim3(grid), dim3(64), tile, STREAM(stream), s->dm,
                                s->ds, s->tp, actions, obs, rew, reset_buf, progress_buf, potentials,
                                prev_potentials);

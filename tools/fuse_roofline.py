@@ -21,6 +21,17 @@ def fuse_bytes(task) -> int:
     return 4 * (13 + 3 * D + 6 * S + 1) + 16 + 4 * (O + 3) + 16
 
 
+def kernel_label(n: int) -> str:
+    """The kernel mi_task_post_step launches for n envs (mi_sim.hip): the pipelined kernel from two
+    32-env tiles per resident workgroup up (resident = 256 CUs x 8 workgroups for Humanoid and Ant:
+    253 VGPRs -> 2 waves / SIMD), else the one-tile kernel; MI_POST_TILE overrides."""
+    var = os.environ.get("MI_POST_TILE", "32p")
+    tiles = (n + 31) // 32
+    if var == "32p" and tiles >= int(os.environ.get("MI_POST_PIPE_MIN", "2")) * 256 * 8:
+        return "k_loco_post_pipe"
+    return "k_loco_post_tiled<" + ("32s" if var == "32p" else var) + ">"
+
+
 def measure(task_name: str, n: int, launches: int = 30, env=None) -> dict:
     import torch
 
@@ -48,7 +59,7 @@ def measure(task_name: str, n: int, launches: int = 30, env=None) -> dict:
     gbs = B * n / (ms * 1e-3) / 1e9
     if own:
         env.close()
-    return {"kernel": ("k_loco_post_pipe<" if os.environ.get("MI_POST_TILE", "32p") == "32p" else "k_loco_post_tiled<") + os.environ.get("MI_POST_TILE", "32p") + ">", "task": task_name, "num_envs": n, "kernel_ms": round(ms, 4),
+    return {"kernel": kernel_label(n), "task": task_name, "num_envs": n, "kernel_ms": round(ms, 4),
             "algo_bytes_per_env": B, "achieved": round(gbs, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
             "frac": round(gbs / HBM_PEAK_GBS, 4)}
 
