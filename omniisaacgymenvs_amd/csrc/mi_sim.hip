@@ -207,7 +207,7 @@ __global__ __launch_bounds__(64) void k_loco_post_tiled(DevModel m, DevState st,
         // compact tile: each record's used fields only (root 13, q, qd, sensors: the efforts
         // and the line padding are dropped on the way into LDS), actions read in place
         const int D = m.D, S = m.S;
-        const int k0 = 13 + 2 * D, s0 = 13 + 3 * D, ns = 6 * S, PC = k0 + ns + 1;
+        const int k0 = 13 + 2 * D, s0 = 13 + 3 * D, ns = 6 * S, PC = (k0 + ns) | 1;   // odd row stride: no LDS bank aliasing across envs
         float* srec = sm;
         float* sobs = sm + TE * PC;
         float* sterm = sobs + TE * O;                          // [TE][3] sums
@@ -320,7 +320,7 @@ __global__ __launch_bounds__(64) void k_loco_post_pipe(DevModel m, DevState st, 
     const int lane = threadIdx.x;
     const int O = tp.O, A = tp.A, D = m.D, S = m.S, es = st.es, N = st.N;
     const int ntiles = (N + TE - 1) / TE;
-    const int k0 = 13 + 2 * D, s0 = 13 + 3 * D, ns = 6 * S, PC = k0 + ns + 1;
+    const int k0 = 13 + 2 * D, s0 = 13 + 3 * D, ns = 6 * S, PC = (k0 + ns) | 1;   // odd row stride: no LDS bank aliasing across envs
     const int ka = 12 + 2 * D + ns;                        // obs column of actions[0]
     const unsigned mag_es = ((1u << 20) + es - 1) / es, mag_a = ((1u << 20) + A - 1) / A;
     float* srec = sm;
