@@ -257,7 +257,7 @@ __global__ __launch_bounds__(64) void k_loco_post_tiled(DevModel m, DevState st,
         const int cnt = n * O;
         if ((((uintptr_t)dst) & 15) == 0 && (cnt & 3) == 0) {
             for (int k = lane; k < cnt / 4; k += 64)
-                ((float4*)dst)[k] = make_float4(sobs[4 * k], sobs[4 * k + 1], sobs[4 * k + 2], sobs[4 * k + 3]);
+                ((float4*)dst)[k] = ((const float4*)sobs)[k];   // sobs 16-B aligned: ds_read_b128
         } else {
             for (int k = lane; k < cnt; k += 64) dst[k] = sobs[k];
         }
@@ -292,7 +292,7 @@ __global__ __launch_bounds__(64) void k_loco_post_tiled(DevModel m, DevState st,
     const int cnt = n * O;
     if ((((uintptr_t)dst) & 15) == 0 && (cnt & 3) == 0) {
         for (int k = lane; k < cnt / 4; k += 64)
-            ((float4*)dst)[k] = make_float4(sobs[4 * k], sobs[4 * k + 1], sobs[4 * k + 2], sobs[4 * k + 3]);
+            ((float4*)dst)[k] = ((const float4*)sobs)[k];   // sobs 16-B aligned: ds_read_b128
     } else {
         for (int k = lane; k < cnt; k += 64) dst[k] = sobs[k];
     }
@@ -437,7 +437,7 @@ __global__ __launch_bounds__(64) void k_loco_post_pipe(DevModel m, DevState st, 
         const int cnt = n * O;
         if ((((uintptr_t)dst) & 15) == 0 && (cnt & 3) == 0) {
             for (int k = lane; k < cnt / 4; k += 64)
-                ((float4*)dst)[k] = make_float4(sobs[4 * k], sobs[4 * k + 1], sobs[4 * k + 2], sobs[4 * k + 3]);
+                ((float4*)dst)[k] = ((const float4*)sobs)[k];   // sobs 16-B aligned: ds_read_b128
         } else {
             for (int k = lane; k < cnt; k += 64) dst[k] = sobs[k];
         }
