@@ -6,12 +6,15 @@ i.e. one fused mi_env_step launch: mask-driven reset_idx, efforts, controlFreque
 physics substeps, observations, reward, done, obs clamp. Action batches are pre-generated in
 HBM (Philox) before the timed region.
 
-N=1: `python bench.py` (Humanoid, 4096 envs). N>1: launched by torch.distributed.run, one
-rank per GPU; each rank owns 4096 envs of a global grid (weak scaling) and every
---gather-every steps the rollout slab (obs, rew, done), which the fused launch writes in
-place, is all-gathered over RCCL asynchronously while the next horizon steps.
+N=1: `python bench.py` (Humanoid, 4096 envs). N>1: `python bench.py --gpus N` starts
+torch.distributed.run itself (or the driver launches it that way): one rank per GPU, each rank
+owns 4096 envs of a global grid (weak scaling). Every rank writes its rollout slab (done, rew,
+obs) in place from the fused launch and gathers it to the learner rank (rank 0) over RCCL once
+per horizon (HumanoidPPO.yaml:66, 32 steps), asynchronously while the next horizon steps. The
+timed window starts a fresh horizon and ends by gathering any partial one, so every window
+holds at least one complete gather whatever --steps is.
 
-Prints ONE JSON line (rank 0). `roofline` is for the dominant kernel (k_env_step), timed
+Prints ONE JSON line (rank 0). `roofline` is for the dominant kernel (k_env_step_wave), timed
 with HIP events on the stream it is launched on; `cpu_baseline` times the CPU oracle (the
 build's C restatement; the reference's PhysX CPU path is closed and absent) on host cores.
 """
@@ -20,6 +23,8 @@ from __future__ import annotations
 import argparse
 import json
 import os
+import statistics
+import subprocess
 import sys
 import time
 
@@ -29,9 +34,10 @@ sys.path.insert(0, ROOT)
 # algorithmic HBM bytes per env-step of a fully fused step (SURVEY §8d / BASELINE.md)
 ALGO_BYTES = {"Humanoid": 920, "Ant": 552, "Cartpole": 80}
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md)
+BASELINE_METRIC = "env-steps/s (physics+obs+reward) Humanoid 4096 envs @1/2/4/8 MI355X"
 
 
-def parse():
+def parse(argv=None):
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=300)
@@ -39,18 +45,99 @@ def parse():
     ap.add_argument("--task", default="Humanoid", choices=["Humanoid", "Ant", "Cartpole"])
     ap.add_argument("--num-envs", type=int, default=4096, help="envs per GPU")
     ap.add_argument("--seed", type=int, default=42)
-    ap.add_argument("--gather-every", type=int, default=32, help="rollout gather period (N>1)")
+    ap.add_argument("--gather-every", type=int, default=32, help="rollout horizon (N>1)")
     ap.add_argument("--cpu-seconds", type=float, default=30.0,
                     help="CPU baseline sample budget (split over the 1 / 4 / all-thread legs)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-side", action="store_true", help="skip the Cartpole / Ant side runs")
     ap.add_argument("--modular", action="store_true", help="method-by-method path, not fused")
     ap.add_argument("--fuse-envs", type=int, default=1048576,
                     help="envs of the obs/reward-fuse HBM roofline side measurement (0: skip)")
-    return ap.parse_args()
+    return ap.parse_args(argv)
+
+
+def launch_ranks(args) -> int:
+    """`bench.py --gpus N` outside torch.distributed.run: start it as a CHILD process with N ranks
+    (nothing here has touched the GPU) and return its exit code."""
+    import socket
+
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={args.gpus}",
+           "--master-addr", "127.0.0.1", "--master-port", str(port), os.path.abspath(__file__),
+           *sys.argv[1:]]
+    return subprocess.call(cmd)
+
+
+class ShardLoop:
+    """The timed loop of one rank: step the env shard, write each step's (obs, rew, done) into the
+    rollout slab row, gather every full horizon to the learner asynchronously.
+
+    ``env``: a VecEnvRLGames (or any object with ``fused`` and ``step(actions[, out])``);
+    ``actions``: a pool of action batches indexed by global step; ``rollout``: a RolloutGather or
+    None (single process, nothing to gather)."""
+
+    def __init__(self, env, actions, rollout=None, horizon: int = 32):
+        self.env, self.actions, self.rollout = env, actions, rollout
+        self.H = horizon if rollout is None else min(horizon, rollout.H)
+        self.h = 0          # next row of the current horizon
+        self.gathering = True
+
+    def step(self, k: int):
+        a = self.actions[k % len(self.actions)]
+        r = self.rollout
+        if r is None:
+            return self.env.step(a)[0]
+        if self.env.fused:
+            obs = self.env.step(a, out=r.slot(self.h))[0]
+        else:
+            obs, rew, done, _ = self.env.step(a)
+            r.record(self.h, obs["obs"], rew, done)
+        self.h += 1
+        if self.h == self.H:
+            if self.gathering:
+                r.gather(async_op=True)
+            self.h = 0
+        return obs
+
+    def flush(self) -> None:
+        """Gather the partial horizon in progress (its first h rows), so no step of a window is
+        left un-gathered."""
+        if self.rollout is not None and self.h > 0:
+            if self.gathering:
+                self.rollout.gather(async_op=True, rows=self.h)
+            self.h = 0
+
+    def window(self, start: int, steps: int, sync=lambda: None, barrier=lambda: None,
+               gathering: bool = True) -> dict:
+        """Time `steps` steps from a fresh horizon; the window closes after the last gather it
+        issued has completed (barrier + device sync on both sides)."""
+        r = self.rollout
+        self.flush()
+        if r is not None:
+            r.wait()
+        sync(); barrier(); sync()
+        self.gathering = gathering
+        g0 = r.gathers if r is not None else 0
+        b0 = r.bytes_sent if r is not None else 0
+        t0 = time.perf_counter()
+        for k in range(steps):
+            self.step(start + k)
+        self.flush()
+        if r is not None:
+            r.wait()   # every collective issued inside the window completes inside it
+        sync(); barrier(); sync()
+        el = time.perf_counter() - t0
+        self.gathering = True
+        return {"elapsed": el, "gathers": (r.gathers - g0) if r is not None else 0,
+                "bytes": (r.bytes_sent - b0) if r is not None else 0}
 
 
 def cpu_baseline(task_name: str, env, seconds: float) -> dict:
-    """Time the CPU oracle's fused env step on a bounded sample of the same workload."""
+    """Time the CPU oracle's fused env step on a bounded sample of the same workload: per thread
+    count, warm-up steps then the median of 3 timed runs (contract: ~10-30 s of CPU work in all,
+    instead of BASELINE.md's 200 / 2000 / median-of-5, which would take minutes per leg)."""
     import numpy as np
     from oracle.oracle import OracleSim, lib as orc_lib, make_buffers
 
@@ -69,44 +156,46 @@ def cpu_baseline(task_name: str, env, seconds: float) -> dict:
     ncpu = min(ncpu, int(os.environ.get("OMP_NUM_THREADS", ncpu)))
     sweep = sorted({1, min(4, ncpu), ncpu})
     rng = np.random.default_rng(0)
+    warm = 20
     for threads in sweep:
         orc_lib().orc_set_threads(threads)
         orc = OracleSim(task.model, view.sim_params, n, origins, seed=42)
         orc.configure(task.task_params(), keep=task)
         b = make_buffers(n, task.num_observations, task.num_actions)
         acts = rng.uniform(-1, 1, (8, n, task.num_actions)).astype(np.float32)
-        for k in range(3):  # warm-up (first resets)
+        t0 = time.perf_counter()
+        for k in range(warm):   # warm-up (first resets, caches)
             orc.env_step(acts[k % 8], task.control_frequency_inv, b)
-        steps, t0 = 0, time.perf_counter()
-        budget = seconds / len(sweep)
-        while True:
-            orc.env_step(acts[steps % 8], task.control_frequency_inv, b)
-            steps += 1
-            el = time.perf_counter() - t0
-            if el >= budget and steps >= 3:
-                break
-        results[threads] = (n * steps / el, steps, el)
+        per_step = (time.perf_counter() - t0) / warm
+        budget = seconds / len(sweep) / 3
+        steps = max(3, int(budget / per_step))
+        runs = []
+        for _ in range(3):
+            t0 = time.perf_counter()
+            for k in range(steps):
+                orc.env_step(acts[k % 8], task.control_frequency_inv, b)
+            runs.append(n * steps / (time.perf_counter() - t0))
+        results[threads] = (statistics.median(runs), steps)
         orc.close()
-    v1, steps1, el1 = results[1]
+    v1, steps1 = results[1]
     return {
         "value": round(v1, 1), "unit": "env-steps/s", "cores": 1, "kind": "port",
-        "sample": f"{task_name} {n} envs x {steps1} env-steps ({el1:.1f}s), oracle/oracle.c fused "
-                  f"step (2 substeps), 1 thread",
+        "sample": f"{task_name} {n} envs, {warm} warm-up + median of 3 x {steps1} env-steps, 1 thread; "
+                  f"oracle/oracle.c fused step (2 substeps). Algorithm: the oracle's dense CRBA + "
+                  f"Cholesky articulated step (device: tree LTDL), same contacts / limits / PGS and task "
+                  f"math. Protocol: bounded sample, not BASELINE.md's 200 / 2000 / median-of-5",
         "threads_sweep": {str(t): round(v[0], 1) for t, v in results.items()},
     }
 
 
 def kernel_name(view, task) -> str:
-    from omniisaacgymenvs_amd import native as N
     """Name of the fused env-step kernel this configuration launches."""
+    from omniisaacgymenvs_amd import native as N
     path, topo, _ = view.sim_kernel_path()
     if path == 1 and task.task_params().task_kind != N.MI_TASK_CARTPOLE:   # wave path
         return "k_env_step_wave<" + {0: "TopoRuntime", 1: "TopoCT<RobotHumanoid>",
                                      2: "TopoCT<RobotAnt>"}.get(topo, str(topo)) + ">"
     return "k_env_step"
-
-
-BASELINE_METRIC = "env-steps/s (physics+obs+reward) Humanoid 4096 envs @1/2/4/8 MI355X"
 
 
 def read_traffic(task_name: str):
@@ -118,21 +207,74 @@ def read_traffic(task_name: str):
     return None
 
 
+def action_pool(view, n, A, seed, device, pool=16):
+    import torch
+    from omniisaacgymenvs_amd import native as N
+
+    actions = torch.empty((pool, n, A), device=device)
+    for k in range(pool):
+        N.check(N.lib().mi_fill_uniform(view.handle, actions[k].data_ptr(), A, seed, k, -1.0, 1.0,
+                                        view.stream()))
+    return actions
+
+
+def side_run(task_name: str, n: int, steps: int = 200, warmup: int = 30) -> dict:
+    """BASELINE configs 2 and 3 (Cartpole / Ant at 4096 envs on 1 GPU): the same fused step,
+    kernel time from HIP events on the launch stream, algorithmic HBM fraction."""
+    import torch
+    from omniisaacgymenvs_amd.utils.task_util import make_env
+
+    env = make_env(task_name, num_envs=n, device="cuda:0", seed=42)
+    task = env.task
+    view = task.get_robot()
+    actions = action_pool(view, n, task.num_actions, 42, "cuda:0")
+    env.reset()
+    for k in range(warmup):
+        env.step(actions[k % len(actions)])
+    starts = [torch.cuda.Event(enable_timing=True) for _ in range(steps)]
+    ends = [torch.cuda.Event(enable_timing=True) for _ in range(steps)]
+    env.kernel_events = (starts, ends)
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for k in range(steps):
+        env.step(actions[k % len(actions)])
+    torch.cuda.synchronize()
+    el = time.perf_counter() - t0
+    env.kernel_events = None
+    kms = sum(s.elapsed_time(e) for s, e in zip(starts, ends)) / steps
+    ach = ALGO_BYTES[task_name] * n / (kms * 1e-3) / 1e9
+    out = {"workload": f"{task_name} {n} envs, fused env step", "kernel": kernel_name(view, task),
+           "value": round(n * steps / el, 1), "unit": "env-steps/s", "ms_per_step": round(el / steps * 1e3, 4),
+           "kernel_ms": round(kms, 4), "achieved": round(ach, 3), "unit_bw": "GB/s",
+           "frac": round(ach / HBM_PEAK_GBS, 6), "algo_bytes_per_env": ALGO_BYTES[task_name],
+           "lds_bytes_per_env": view.sim_kernel_path()[2], "nan_resets": view.nan_count()}
+    env.close()
+    return out
+
+
 def main():
     args = parse()
+    env_world = os.environ.get("WORLD_SIZE")
+    if env_world is None and args.gpus > 1:
+        sys.exit(launch_ranks(args))
+    world = int(env_world or "1")
+    if env_world is not None and world != args.gpus:
+        print(f"bench.py: --gpus {args.gpus} but WORLD_SIZE={world}", file=sys.stderr)
+        sys.exit(2)
     import torch
     import torch.distributed as dist
 
-    world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
-    if world > 1:
+    # under torch.distributed.run (even one rank) the RCCL process group and the rollout gather run
+    distributed = world > 1 or "TORCHELASTIC_RUN_ID" in os.environ
+    if distributed:
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
         torch.cuda.set_device(local)
         dist.init_process_group("nccl", device_id=torch.device(f"cuda:{local}"))
     device = f"cuda:{local}"
 
-    from omniisaacgymenvs_amd import native as N
+    from omniisaacgymenvs_amd.utils.distributed import RolloutGather
     from omniisaacgymenvs_amd.utils.task_util import make_env
 
     n_local = args.num_envs
@@ -143,59 +285,49 @@ def main():
     task = env.task
     view = task.get_robot()
     A, O = task.num_actions, task.num_observations
-    pool = 16
-    actions = torch.empty((pool, n_local, A), device=device)
-    for k in range(pool):
-        N.check(N.lib().mi_fill_uniform(view.handle, actions[k].data_ptr(), A, args.seed, k, -1.0, 1.0,
-                                        view.stream()))
+    actions = action_pool(view, n_local, A, args.seed, device)
     env.reset()
-    from omniisaacgymenvs_amd.utils.distributed import RolloutGather
-
-    rollout = RolloutGather(args.gather_every, n_local, O, device, world) if world > 1 else None
-
-    def one_step(k):
-        if rollout is None:
-            return env.step(actions[k % pool])[0]
-        # the launch writes obs/rew/done straight into the rollout slab row (no copies); a full
-        # horizon is all-gathered asynchronously over RCCL while the next one steps
-        h = k % args.gather_every
-        if env.fused:
-            obs = env.step(actions[k % pool], out=rollout.slot(h))[0]
-        else:
-            obs, rew, done, _ = env.step(actions[k % pool])
-            rollout.record(h, obs["obs"], rew, done)
-        if h == args.gather_every - 1:
-            rollout.gather(async_op=True)
-        return obs
+    rollout = RolloutGather(args.gather_every, n_local, O, device, world, mode="gather", dst=0) \
+        if distributed else None
+    loop = ShardLoop(env, actions, rollout, args.gather_every)
+    sync = torch.cuda.synchronize
+    barrier = dist.barrier if distributed else (lambda: None)
 
     for k in range(args.warmup):
-        one_step(k)
-    if rollout is not None:
-        rollout.wait()
-    torch.cuda.synchronize()
-    if world > 1:
-        dist.barrier()
-    torch.cuda.synchronize()
+        loop.step(k)
     # kernel events around every fused launch inside the timed region (same stream)
     starts = [torch.cuda.Event(enable_timing=True) for _ in range(args.steps)]
     ends = [torch.cuda.Event(enable_timing=True) for _ in range(args.steps)]
     env.kernel_events = (starts, ends)
-    t0 = time.perf_counter()
-    for k in range(args.steps):
-        one_step(args.warmup + k)
-    if rollout is not None:
-        rollout.wait()   # every collective issued inside the window completes inside it
-    torch.cuda.synchronize()
-    if world > 1:
-        dist.barrier()
-    torch.cuda.synchronize()
-    elapsed = time.perf_counter() - t0
+    env._ev_i = 0
+    win = loop.window(args.warmup, args.steps, sync, barrier)
     env.kernel_events = None
-    if world > 1:
+    elapsed = win["elapsed"]
+    kernel_ms = sum(s.elapsed_time(e) for s, e in zip(starts, ends)) / args.steps if env.fused else None
+    gather_info = None
+    if distributed:
         t = torch.tensor([elapsed], device=device, dtype=torch.float64)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
-    kernel_ms = sum(s.elapsed_time(e) for s, e in zip(starts, ends)) / args.steps if env.fused else None
+        # the same window without gathers (exposed gather time = difference), and one
+        # synchronous horizon gather on its own
+        nog = loop.window(args.warmup + args.steps, args.steps, sync, barrier, gathering=False)
+        t = torch.tensor([nog["elapsed"]], device=device, dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        nog_el = float(t.item())
+        sync(); barrier(); sync()
+        t0 = time.perf_counter()
+        rollout.gather(async_op=False)
+        sync(); barrier(); sync()
+        g_ms = (time.perf_counter() - t0) * 1e3
+        gather_info = {"collective": "gather to rank 0 (learner), RCCL" if dist.get_backend() == "nccl"
+                       else f"gather to rank 0, {dist.get_backend()}",
+                       "horizon": loop.H, "gathers_in_window": win["gathers"],
+                       "gather_bytes_per_rank": win["bytes"] // max(1, win["gathers"]),
+                       "bytes_per_rank_in_window": win["bytes"],
+                       "window_ms_no_gather": round(nog_el * 1e3, 3),
+                       "exposed_gather_ms": round((elapsed - nog_el) * 1e3, 3),
+                       "standalone_horizon_gather_ms": round(g_ms, 3)}
     total_env_steps = world * n_local * args.steps
     value = total_env_steps / elapsed
     nan = view.nan_count()
@@ -204,12 +336,17 @@ def main():
     if rank == 0:
         roof = None
         if kernel_ms:
-            achieved = ALGO_BYTES[args.task] * n_local / (kernel_ms * 1e-3) / 1e9
+            algo = ALGO_BYTES[args.task] * n_local
+            achieved = algo / (kernel_ms * 1e-3) / 1e9
+            traffic = read_traffic(args.task)
             roof = {"bound": "hbm", "achieved": round(achieved, 3), "peak": HBM_PEAK_GBS,
-                    "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 6),
-                    "traffic": read_traffic(args.task), "kernel": kernel_name(view, task),
-                    "kernel_ms": round(kernel_ms, 4),
-                    "algo_bytes_per_launch": ALGO_BYTES[args.task] * n_local}
+                    "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 6), "traffic": traffic,
+                    "kernel": kernel_name(view, task), "kernel_ms": round(kernel_ms, 4),
+                    "algo_bytes_per_launch": algo,
+                    "limiter": "latency: dependent per-env chains at the resident-wave count "
+                               "(DESIGN.md §2, §6); HBM is not the limiter at 4096 envs"}
+            if traffic:
+                roof["traffic_gbs"] = round(traffic / (kernel_ms * 1e-3) / 1e9, 3)
         out = {
             "metric": BASELINE_METRIC if args.task == "Humanoid" else
                       f"env-steps/s (physics+obs+reward) {args.task} {args.num_envs} envs (side run)",
@@ -222,10 +359,20 @@ def main():
                        "task": args.task, "num_envs_per_gpu": n_local, "global_envs": world * n_local,
                        "substeps": task.control_frequency_inv, "path": "fused" if env.fused else "modular",
                        "lds_bytes_per_env": view.sim_kernel_path()[2],
-                       "parallelism": f"env-shard x{world}" + (f" + async RCCL all_gather of the rollout slab every {args.gather_every} steps" if world > 1 else "")},
+                       "parallelism": f"env-shard x{world}" + (
+                           f" + async RCCL gather of the rollout slab to the learner rank every "
+                           f"{loop.H} steps" if distributed else "")},
             "roofline": roof,
             "nan_resets": nan,
         }
+        if gather_info:
+            out["rollout_gather"] = gather_info
+    if distributed:
+        dist.barrier()
+        dist.destroy_process_group()
+    if rank == 0:
+        if world == 1 and not args.no_side and args.task == "Humanoid":
+            out["side_configs"] = [side_run("Cartpole", 4096), side_run("Ant", 4096)]
         if world == 1 and args.fuse_envs > 0 and args.task != "Cartpole":
             # north_star: achieved HBM GB/s of the obs/reward fuse (RLTask.post_physics_step as ONE
             # streaming kernel, the method-by-method path) where its working set streams from HBM
@@ -236,9 +383,6 @@ def main():
             out["cpu_baseline"] = cpu_baseline(args.task, env, args.cpu_seconds)
         print(json.dumps(out), flush=True)
     env.close()
-    if world > 1:
-        dist.barrier()
-        dist.destroy_process_group()
 
 
 if __name__ == "__main__":

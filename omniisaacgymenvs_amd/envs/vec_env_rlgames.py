@@ -75,6 +75,10 @@ class VecEnvRLGames:
         """Force the reference's method-by-method path (False) or the fused launch (True,
         only when the task supports it)."""
         self._fused = bool(on) and self._task.supports_fused_step()
+        if not self._fused:
+            # the fused launch may have bound task.obs_buf to a returned obs tensor (clip_obs =
+            # inf, single write); the method-by-method path writes obs_buf in place
+            self._task.obs_buf = self._task.obs_buf.clone()
 
     # ------------------------------------------------------------------ RL API
     def _process_data(self) -> None:

@@ -165,11 +165,17 @@ class LocomotionTask(RLTask):
         the copies _process_data hands back (vec_env_rlgames.py:41-46)."""
         a = actions.to(self._device, dtype=torch.float32).contiguous()
         obs_out, rew_out, reset_out = self._step_outputs(out)
+        # clip_obs = inf (locomotion default, rl_task.py:69): the clamped copy equals obs_buf, so
+        # the launch writes the row once and obs_buf becomes that tensor (no second HBM write)
+        single = math.isinf(self.clip_obs)
         N.check(N.lib().mi_env_step(self._h(), a.data_ptr(), int(self.control_frequency_inv),
-                                    obs_out.data_ptr(), self.obs_buf.data_ptr(), self.rew_buf.data_ptr(),
+                                    obs_out.data_ptr(), 0 if single else self.obs_buf.data_ptr(),
+                                    self.rew_buf.data_ptr(),
                                     self.reset_buf.data_ptr(), self.progress_buf.data_ptr(),
                                     self.potentials.data_ptr(), self.prev_potentials.data_ptr(),
                                     self.actions.data_ptr(), rew_out.data_ptr(), reset_out.data_ptr(),
                                     self._stream()), "mi_env_step")
+        if single:
+            self.obs_buf = obs_out
         return obs_out, rew_out, reset_out
 

@@ -72,13 +72,13 @@ def test_two_rank_shard_and_gather_equals_single_process():
     np.testing.assert_array_equal(got, ref)
 
 
-def _async_worker(rank, world, port, q):
+def _async_worker(rank, world, port, q, mode):
     """Three horizons through the double-buffered slabs with async gathers: every gathered
     horizon must hold each rank's rows exactly, even while the next horizon is being written."""
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     dist.init_process_group("gloo", rank=rank, world_size=world)
     n, O, Hh = 5, 3, 4
-    g = RolloutGather(Hh, n, O, "cpu", world)
+    g = RolloutGather(Hh, n, O, "cpu", world, mode=mode)
     got = []
     for hz in range(3):
         for h in range(Hh):
@@ -94,6 +94,9 @@ def _async_worker(rank, world, port, q):
 
         def prev_view(o=prev):
             g.wait()
+            if o is None:                  # gather mode, not the learner rank
+                assert mode == "gather" and rank != 0
+                return None
             return (o.obs.clone(), o.rew.clone(), o.done.clone())
     got.append(prev_view())
     if rank == 0:
@@ -102,12 +105,13 @@ def _async_worker(rank, world, port, q):
     dist.destroy_process_group()
 
 
-def test_async_double_buffered_gather_two_ranks():
+@pytest.mark.parametrize("mode", ["gather", "all_gather"])
+def test_async_double_buffered_gather_two_ranks(mode):
     world = 2
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
-    port = 30500 + os.getpid() % 1000
-    procs = [ctx.Process(target=_async_worker, args=(r, world, port, q)) for r in range(world)]
+    port = 30500 + os.getpid() % 1000 + (7 if mode == "gather" else 0)
+    procs = [ctx.Process(target=_async_worker, args=(r, world, port, q, mode)) for r in range(world)]
     for p in procs:
         p.start()
     got = q.get(timeout=120)
@@ -124,3 +128,89 @@ def test_async_double_buffered_gather_two_ranks():
                 np.testing.assert_array_equal(obs[r, h], np.arange(n * O, dtype=np.float32).reshape(n, O) + base)
                 np.testing.assert_array_equal(rew[r, h], np.full(n, base + 0.5, np.float32))
                 np.testing.assert_array_equal(done[r, h], np.full(n, hz + r, np.int64))
+
+
+class _OracleShardEnv:
+    """CPU stand-in for one rank's fused VecEnvRLGames (test infrastructure: the oracle steps the
+    shard): step(actions, out=(obs, rew, done)) writes the returned tensors into `out`."""
+    fused = True
+
+    def __init__(self, offset, n, total):
+        tp, m, _ = task_params_from_cfg(TASK)
+        origins = GridCloner(5.0).get_clone_positions(total, offset, n)
+        self.orc = OracleSim(m, sim_params(rest_offset=0.0), n, origins, seed=42, env_id_offset=offset)
+        self.orc.configure(tp)
+        self.b = make_buffers(n, tp.num_obs, tp.num_actions)
+
+    def step(self, actions, out=None):
+        self.orc.env_step(actions.numpy(), 2, self.b)
+        obs, rew, done = out
+        obs.copy_(torch.from_numpy(self.b["obs"]))
+        rew.copy_(torch.from_numpy(self.b["rew"]))
+        done.copy_(torch.from_numpy(self.b["reset"]))
+        return {"obs": obs}, rew, done, {}
+
+
+STEPS_IN_WINDOW = 5
+
+
+def _bench_loop_worker(rank, world, port, q):
+    """bench.py's own ShardLoop with --steps 5 < horizon 32: the window must hold one complete
+    gather (the partial horizon flushed at its end) whose rows are the global rollout."""
+    import bench
+
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    off, total = shard_range(rank, world, N_PER_RANK)
+    env = _OracleShardEnv(off, N_PER_RANK, total)
+    tp, _, _ = task_params_from_cfg(TASK)
+    acts = [torch.from_numpy(_actions(off, N_PER_RANK, tp.num_actions, h)) for h in range(H)]
+    g = RolloutGather(32, N_PER_RANK, tp.num_obs, "cpu", world, mode="gather", dst=0)
+    loop = bench.ShardLoop(env, acts, g, 32)
+    win = loop.window(0, STEPS_IN_WINDOW, barrier=dist.barrier)
+    res = {"gathers": win["gathers"], "bytes": win["bytes"], "step_bytes": g.step_bytes}
+    if rank == 0:
+        res["rows"] = g.global_view().numpy().copy()
+    else:
+        assert g.out is None          # gather mode: only the learner holds the horizon
+    q.put((rank, res))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def test_bench_window_gathers_partial_horizon_two_ranks():
+    world = 2
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = 31500 + os.getpid() % 1000
+    procs = [ctx.Process(target=_bench_loop_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    got = dict(q.get(timeout=120) for _ in range(world))
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    for r in range(world):
+        assert got[r]["gathers"] == 1
+        assert got[r]["bytes"] == STEPS_IN_WINDOW * got[r]["step_bytes"]
+    ref = _rollout(0, world * N_PER_RANK, world * N_PER_RANK)   # H = 4 steps of actions, cycled
+    ref5 = np.concatenate([ref, _rollout_tail(world)], axis=0)[:STEPS_IN_WINDOW]
+    np.testing.assert_array_equal(got[0]["rows"], ref5)
+
+
+def _rollout_tail(world):
+    """Step 5 of the single-process run (the action pool of H batches cycles: step 4 uses batch 0)."""
+    tp, m, _ = task_params_from_cfg(TASK)
+    n = world * N_PER_RANK
+    origins = GridCloner(5.0).get_clone_positions(n, 0, n)
+    orc = OracleSim(m, sim_params(rest_offset=0.0), n, origins, seed=42)
+    orc.configure(tp)
+    b = make_buffers(n, tp.num_obs, tp.num_actions)
+    for h in range(H + 1):
+        orc.env_step(_actions(0, n, tp.num_actions, h % H), 2, b)
+    orc.close()
+    out = np.zeros((1, n, tp.num_obs + 2), np.float32)
+    out[0, :, : tp.num_obs] = b["obs"]
+    out[0, :, tp.num_obs] = b["rew"]
+    out[0, :, tp.num_obs + 1] = b["reset"]
+    return out
