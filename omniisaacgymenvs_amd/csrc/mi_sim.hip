@@ -550,6 +550,11 @@ static void with_topo(int id, F&& f) {
     }
 }
 
+static inline dim3 wave_block(const mi_sim* s) { return dim3(64 * s->wt.envs_per_wg); }
+static inline dim3 wave_grid(const mi_sim* s) {
+    return dim3((s->N + s->wt.envs_per_wg - 1) / s->wt.envs_per_wg);
+}
+
 // id of the generated topology whose link tree equals the model's (0: none)
 static int match_topology(const mi_model_desc* md, bool self_on) {
     const int nr = md->root_free ? 6 : 0;
@@ -585,30 +590,43 @@ __device__ __forceinline__ const KParams* opaque_kp(const KParams* kp) {
     return kp;
 }
 
-// copy the per-model constant block into this workgroup's LDS (once per launch)
+// copy the per-model constant block into this workgroup's LDS (once per launch; shared by the
+// workgroup's envs). The one workgroup barrier of the wave kernels.
 __device__ __forceinline__ void stage_model_constants(const WaveTabs& t, float* smem) {
-    for (int q = threadIdx.x; q < t.mc_len; q += 64) smem[t.s_mc + q] = t.g_mc[q];
+    for (int q = threadIdx.x; q < t.mc_len; q += blockDim.x) smem[t.s_mc + q] = t.g_mc[q];
     __syncthreads();
 }
 
+// env of this wave (workgroup = envs_per_wg consecutive envs, one wave each)
+__device__ __forceinline__ int wave_env() {
+    return (int)(blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6));
+}
+__device__ __forceinline__ float* wave_env_lds(const WaveTabs& t, float* smem) {
+    return smem + (threadIdx.x >> 6) * t.env_stride;
+}
+
 template <class T>
-__global__ __launch_bounds__(64) void k_sim_step_wave(const KParams* __restrict__ kp, int substeps) {
+__global__ __launch_bounds__(256) void k_sim_step_wave(const KParams* __restrict__ kp, int substeps) {
     extern __shared__ __attribute__((aligned(16))) float smem[];
-    const DevModel& m = kp->m;
     const WaveTabs& t = kp->t;
-    const DevState& st = kp->st;
-    const SimP& p = kp->p;
-    const int i = blockIdx.x;
-    float* gW = kp->rows + (size_t)i * t.g_row_stride;
+    const int i = wave_env();
     stage_model_constants(t, smem);
+    if (i >= kp->st.N) return;
+    float* gW = kp->rows + (size_t)i * t.g_row_stride;
+    float* sm = wave_env_lds(t, smem);
     for (int s = 0; s < substeps; ++s) {
         const KParams* k = opaque_kp(kp);
-        wave_artic_substep<T>(k->m, k->t, k->st, k->p, i, smem, gW, s == 0, s == substeps - 1);
+        wave_artic_substep<T>(k->m, k->t, k->st, k->p, i, smem, sm, gW, s == 0, s == substeps - 1);
     }
 }
 
 template <class T>
-__global__ __launch_bounds__(64) void k_env_step_wave(const KParams* __restrict__ kp,
+#ifdef MI_WAVES4
+#define MI_WAVE_OCC __attribute__((amdgpu_waves_per_eu(4, 4)))
+#else
+#define MI_WAVE_OCC
+#endif
+__global__ __launch_bounds__(256) MI_WAVE_OCC void k_env_step_wave(const KParams* __restrict__ kp,
                                                       const float* actions, int substeps,
                                                       float* obs_out, float* obs_task, float* rew,
                                                       int64_t* reset_buf, int64_t* progress_buf,
@@ -621,23 +639,26 @@ __global__ __launch_bounds__(64) void k_env_step_wave(const KParams* __restrict_
     const SimP& p = kp->p;
     const DevTask& tp = kp->tp;
     float* rows = kp->rows;
-    const int i = blockIdx.x;
-    const int lane = threadIdx.x;
-    // 1. clamp + pre_physics_step (scalar task math on lane 0); model constants into LDS
+    const int i = wave_env();
+    const bool live = i < st.N;
+    // 1. clamp + pre_physics_step (wave-cooperative); model constants into LDS
     STAMP_BEGIN();
-    const float a_lane =
-        wave_task_pre(m, t, st, tp, i, actions, reset_buf, progress_buf, pot, prev, actions_out);
+    float a_lane = 0.0f;
+    if (live)
+        a_lane = wave_task_pre(m, t, st, tp, i, actions, reset_buf, progress_buf, pot, prev, actions_out);
     stage_model_constants(t, smem);
+    if (!live) return;
     STAMP(13);
     // 2. controlFrequencyInv x World.step, wave-cooperative
     float* gW = rows + (size_t)i * t.g_row_stride;
+    float* sm = wave_env_lds(t, smem);
     for (int s = 0; s < substeps; ++s) {
         const KParams* k = opaque_kp(kp);
-        wave_artic_substep<T>(k->m, k->t, k->st, k->p, i, smem, gW, s == 0, s == substeps - 1);
+        wave_artic_substep<T>(k->m, k->t, k->st, k->p, i, smem, sm, gW, s == 0, s == substeps - 1);
     }
     // 3. post_physics_step + obs clamp, wave-cooperative from the LDS-resident state
     STAMP_RESET();
-    wave_loco_post(m, t, st, tp, i, smem, a_lane, obs_out, obs_task, rew, reset_buf, progress_buf,
+    wave_loco_post(m, t, st, tp, i, sm, a_lane, obs_out, obs_task, rew, reset_buf, progress_buf,
                    pot, prev, rew_out, reset_out);
     STAMP(14);
 }
@@ -1039,6 +1060,7 @@ int mi_sim_create(const mi_model_desc* md, const mi_sim_params* prm, int32_t N, 
         // CT path: J rows of up to 64 constraint rows for the PGS (LDS is not the occupancy
         // limit here: registers cap the wave path at 2 waves/SIMD = 8 envs/CU = 20 KB each)
         t.j_rows_lds = ct ? std::min(48, m.max_rows) : 0;
+        if (const char* e = getenv("MI_WAVE_JROWS")) if (ct) t.j_rows_lds = std::min(t.j_rows_lds, atoi(e));
         t.s_J = take(ct ? t.j_rows_lds * m.nv : 4);
         // CT path: W rows for the P9 -> P10 hand-over. First choice: the rest of the dead
         // span; when that holds fewer rows than a one-bank PGS can use and the LDS budget of
@@ -1051,7 +1073,8 @@ int mi_sim_create(const mi_model_desc* md, const mi_sim_params* prm, int32_t N, 
         t.w_rows_a = t.w_rows_lds;
         t.s_W2 = 0;
         {
-            const int want = std::min(64, m.max_rows);
+            int want = std::min(64, m.max_rows);
+            if (const char* e = getenv("MI_WAVE_WROWS")) want = std::min(want, atoi(e));
             const int lds_budget_floats = (160 * 1024 / 8) / (int)sizeof(float);
             if (ct && t.w_rows_lds < want && so + al4(want * m.nv) <= lds_budget_floats) {
                 t.s_W = take(want * m.nv);
@@ -1065,6 +1088,12 @@ int mi_sim_create(const mi_model_desc* md, const mi_sim_params* prm, int32_t N, 
             }
         }
         t.s_total = so;
+        // E envs per workgroup share the constant block [0, s_env); env w's region is shifted
+        // by w * env_stride
+        t.s_env = t.s_R;
+        t.env_stride = so - t.s_env;
+        t.envs_per_wg = 1;
+        if (const char* e = getenv("MI_WAVE_ENVS")) t.envs_per_wg = std::max(1, std::min(4, atoi(e)));
         {   // the sequential regions strictly increase; the row data sits inside the dead
             // span (overlay) or between s_rp and s_xs
             const int offs[] = {t.s_mc, t.s_R, t.s_o, t.s_S, t.s_F, t.s_Ic, t.s_M, t.s_X,
@@ -1085,7 +1114,7 @@ int mi_sim_create(const mi_model_desc* md, const mi_sim_params* prm, int32_t N, 
             t.s_seg = ro;
             t.s_surv = ro + al4(12 * md->num_geoms);
         }
-        s->lds_bytes = (size_t)so * sizeof(float);
+        s->lds_bytes = (size_t)(so + (t.envs_per_wg - 1) * t.env_stride) * sizeof(float);
     }
     s->lower.assign(md->lower, md->lower + L);
     s->upper.assign(md->upper, md->upper + L);
@@ -1143,6 +1172,17 @@ int mi_sim_create(const mi_model_desc* md, const mi_sim_params* prm, int32_t N, 
     hipError_t e = hipDeviceSynchronize();
     if (e != hipSuccess) return cleanup(fail(MI_E_HIP, "init: %s", hipGetErrorString(e)));
     if ((rc = sync_kparams(s))) return cleanup(rc);
+    if (s->wave && s->lds_bytes > 64 * 1024) {   // above the default dynamic-LDS limit
+        hipError_t e1 = hipSuccess, e2 = hipSuccess;
+        with_topo(s->topo, [&](auto T) {
+            e1 = hipFuncSetAttribute((const void*)k_env_step_wave<decltype(T)>,
+                                     hipFuncAttributeMaxDynamicSharedMemorySize, (int)s->lds_bytes);
+            e2 = hipFuncSetAttribute((const void*)k_sim_step_wave<decltype(T)>,
+                                     hipFuncAttributeMaxDynamicSharedMemorySize, (int)s->lds_bytes);
+        });
+        if (e1 != hipSuccess || e2 != hipSuccess)
+            return cleanup(fail(MI_E_HIP, "wave kernels: %zu B of LDS per workgroup refused", s->lds_bytes));
+    }
     *out = s;
     return MI_OK;
 }
@@ -1248,7 +1288,7 @@ int mi_sim_step(mi_sim* s, int32_t substeps, void* stream) {
     HIP_TRY(hipSetDevice(s->device));
     if (s->wave)
         with_topo(s->topo, [&](auto T) {
-            hipLaunchKernelGGL(k_sim_step_wave<decltype(T)>, dim3(s->N), dim3(64), s->lds_bytes,
+            hipLaunchKernelGGL(k_sim_step_wave<decltype(T)>, wave_grid(s), wave_block(s), s->lds_bytes,
                                STREAM(stream), (const KParams*)s->kp_dev, substeps);
         });
     else
@@ -1427,7 +1467,7 @@ int mi_env_step(mi_sim* s, const float* actions, int32_t substeps, float* obs_ou
     HIP_TRY(hipSetDevice(s->device));
     if (s->wave && s->tp.kind != MI_TASK_CARTPOLE)
         with_topo(s->topo, [&](auto T) {
-            hipLaunchKernelGGL(k_env_step_wave<decltype(T)>, dim3(s->N), dim3(64), s->lds_bytes,
+            hipLaunchKernelGGL(k_env_step_wave<decltype(T)>, wave_grid(s), wave_block(s), s->lds_bytes,
                                STREAM(stream), (const KParams*)s->kp_dev, actions, substeps,
                                obs_out, obs_task, rew, reset_buf, progress_buf, potentials,
                                prev_potentials, actions_out, rew_out, reset_out);
@@ -1529,7 +1569,8 @@ int mi_sim_kernel_path(const mi_sim* s, int32_t* path, int32_t* topology, int32_
     NEED(s);
     if (path) *path = s->wave ? 1 : 0;
     if (topology) *topology = s->wave ? s->topo : 0;
-    if (lds_bytes) *lds_bytes = s->wave ? (int32_t)s->lds_bytes : 0;
+    // per env: the workgroup's LDS (shared constants + envs_per_wg env regions) / envs_per_wg
+    if (lds_bytes) *lds_bytes = s->wave ? (int32_t)(s->lds_bytes / s->wt.envs_per_wg) : 0;
     return MI_OK;
 }
 

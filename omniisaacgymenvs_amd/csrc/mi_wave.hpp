@@ -30,12 +30,26 @@ namespace mi {
 
 constexpr int WNV = 32;  // padded DOF count of the wave path
 
+// One wavefront = one env; a workgroup holds E envs (E waves) that share the LDS copy of the
+// model constants and otherwise never interact. Lane id inside the env's wave:
+__device__ __forceinline__ int wave_lane() { return (int)(threadIdx.x & 63u); }
+// Sync point between two phases of ONE env (its wave): every lane's earlier LDS and global
+// accesses are complete and visible to the wave's later accesses. No s_barrier (the other waves
+// of the workgroup are other envs); the workgroup-scope fences order the vector memory ops too
+// (pre-step effort writes read back by other lanes, the global W-row slab).
+__device__ __forceinline__ void wave_sync() {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+}
+
 // Diagnostic phase timers (built only with -DMI_STAMPS into a separate library; the product
 // build compiles them out). Every workgroup adds the s_memtime delta of each phase to its own
 // slot g_phase[block % MI_STAMP_SLOTS][id] (lane 0, plain adds: no contention); [31] counts
 // substeps. The host sums the slots. IDs: see tools/phase_stamps.py.
 #ifdef MI_STAMPS
 #define MI_STAMP_SLOTS 16384
+#define MI_STAMP_ENV (blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6))
 __device__ unsigned long long g_phase[MI_STAMP_SLOTS][32];
 #define STAMP_BEGIN()                                                                     \
     unsigned long long stamp_t_;                                                          \
@@ -49,17 +63,17 @@ __device__ unsigned long long g_phase[MI_STAMP_SLOTS][32];
         __builtin_amdgcn_sched_barrier(0);                                                \
         unsigned long long t_;                                                            \
         asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t_)::"memory");         \
-        if (threadIdx.x == 0) g_phase[blockIdx.x % MI_STAMP_SLOTS][id] += t_ - stamp_t_;  \
+        if ((threadIdx.x & 63) == 0) g_phase[MI_STAMP_ENV % MI_STAMP_SLOTS][id] += t_ - stamp_t_;  \
         stamp_t_ = t_;                                                                    \
         __builtin_amdgcn_sched_barrier(0);                                                \
     } while (0)
 #define STAMP_END()                                                                       \
     do {                                                                                  \
-        if (threadIdx.x == 0) g_phase[blockIdx.x % MI_STAMP_SLOTS][31] += 1ull;           \
+        if ((threadIdx.x & 63) == 0) g_phase[MI_STAMP_ENV % MI_STAMP_SLOTS][31] += 1ull;           \
     } while (0)
 #define STAT(id, v)                                                                       \
     do {                                                                                  \
-        if (threadIdx.x == 0) g_phase[blockIdx.x % MI_STAMP_SLOTS][id] += (unsigned long long)(v); \
+        if ((threadIdx.x & 63) == 0) g_phase[MI_STAMP_ENV % MI_STAMP_SLOTS][id] += (unsigned long long)(v); \
     } while (0)
 #define STAMP_RESET()                                                                     \
     do {                                                                                  \
@@ -99,6 +113,9 @@ struct WaveTabs {
     // span that is dead by then); rows beyond go through the global slab
     int s_W, w_rows_lds;
     int s_W2, w_rows_a;   // rows [w_rows_a, w_rows_lds) in a second segment at s_W2
+    // E envs per workgroup: env w of the workgroup uses [s_env, s_total) shifted by
+    // w * env_stride floats (env_stride = s_total - s_env); [0, s_env) is the shared constant block
+    int envs_per_wg, s_env, env_stride;
     // J rows [0, j_rows_lds) kept in LDS at s_J (stride nv) for the PGS sweeps
     int s_J, j_rows_lds;
     // per-model constant block (see McLayout): global copy, staged into LDS at s_mc once per
@@ -178,10 +195,10 @@ MI_D void contact_row_f(const float* sm, const WaveTabs& t, int r, float (&f)[6]
     f[3] = dir[0]; f[4] = dir[1]; f[5] = dir[2];
 }
 
-MI_D MC make_mc(const WaveTabs& t, float* sm, int L) {
+MI_D MC make_mc(const WaveTabs& t, const float* mcb, int L) {
     MC c;
-    c.b = sm + t.s_mc;
-    c.bi = (const int*)(sm + t.s_mc);
+    c.b = mcb;
+    c.bi = (const int*)mcb;
     c.L = L; c.np = t.npts; c.ns = t.nsens;
     c.t = &t;
     return c;
@@ -540,9 +557,9 @@ MI_D void wave_link_forward(const MC& mc, int nr, const WaveTabs& t, float* sm, 
 // continue from LDS); store_state: write the state and sensor wrenches back (last substep).
 template <class TP>
 MI_D void wave_artic_substep(const DevModel& m, const WaveTabs& t, const DevState& st,
-                             const SimP& p, int i, float* sm, float* gW, bool load_state,
-                             bool store_state) {
-    const int lane = threadIdx.x;
+                             const SimP& p, int i, const float* mcb, float* sm, float* gW,
+                             bool load_state, bool store_state) {
+    const int lane = wave_lane();
     const int N = st.N, L = m.L, D = m.D, nv = m.nv, nr = m.nr;
     const float dt = p.dt;
     float* us = sm + t.s_us;   // u, then u*
@@ -550,7 +567,7 @@ MI_D void wave_artic_substep(const DevModel& m, const WaveTabs& t, const DevStat
     float* Mx = sm + t.s_M;    // M (lower), then dense padded M~^-1 [WNV][WNV]
     float* Dv = sm + t.s_D;
     float* Ss = sm + t.s_S;
-    const MC mc = make_mc(t, sm, L);
+    const MC mc = make_mc(t, mcb, L);
 
     STAMP_BEGIN();
     // ---- load state into LDS (later substeps of a launch start from the state the previous
@@ -568,16 +585,16 @@ MI_D void wave_artic_substep(const DevModel& m, const WaveTabs& t, const DevStat
 #pragma unroll
         for (int c = 0; c < 6; ++c) Ss[6 * lane + c] = s[c];
     }
-    __syncthreads();
+    wave_sync();
 
     STAMP(0);   // load
     // ---- P1a: local joint transforms, every link at once
     for (int l = 1 + lane; l < L; l += 64) wave_link_local(mc, t, sm, l);
-    __syncthreads();
+    wave_sync();
     // ---- P1b+c: world frames / subspaces / velocities along each link's chain, then the
     // link's inertia and Newton-Euler force (same lane: no barrier in between)
     for (int l = lane; l < L; l += 64) wave_link_forward(mc, nr, t, sm, l, p);
-    __syncthreads();
+    wave_sync();
     STAMP(1);   // P1
     // ---- P2: composite inertia / force = own + sum over the subtree (fixed descendant order,
     // every link at once; results into the aux region: Ic at 16 l, F at 16 l + 10)
@@ -598,7 +615,7 @@ MI_D void wave_artic_substep(const DevModel& m, const WaveTabs& t, const DevStat
             o[0] = a0; o[1] = a1; o[2] = a2; o[3] = a3;
         }
     }
-    __syncthreads();
+    wave_sync();
     STAMP(2);   // P2
     // ---- P3: bias + CRBA (lane k = dof k)
     if (lane < nv) {
@@ -647,7 +664,7 @@ MI_D void wave_artic_substep(const DevModel& m, const WaveTabs& t, const DevStat
             }
         }
     }
-    __syncthreads();
+    wave_sync();
     STAMP(3);   // P3
     // ---- P4: LTDL in place (M = L^T D L, L strictly below the diagonal)
     float Mc[TP::nvc];     // CT path: column `lane` of M~, then of its factor (rows 0..nv-1)
@@ -667,19 +684,19 @@ MI_D void wave_artic_substep(const DevModel& m, const WaveTabs& t, const DevStat
                 const int ii = t.anc_list[a0 + t.tri_p[pi]], jj = t.anc_list[a0 + t.tri_q[pi]];
                 Mx[ii * nv + jj] -= (Mx[k * nv + ii] * inv) * Mx[k * nv + jj];
             }
-            __syncthreads();
+            wave_sync();
             if (lane < na) {
                 const int ii = t.anc_list[a0 + lane];
                 Mx[k * nv + ii] = Mx[k * nv + ii] * inv;
             }
-            __syncthreads();
+            wave_sync();
         }
     }
     STAMP(4);   // P4 (+ factor publish)
     // ---- P5: 1/D of the factor
     if constexpr (!TP::kCT) {
         if (lane < nv) Dv[lane] = 1.0f / Mx[lane * nv + lane];
-        __syncthreads();
+        wave_sync();
     }
     STAMP(5);   // P5
 
@@ -731,7 +748,7 @@ MI_D void wave_artic_substep(const DevModel& m, const WaveTabs& t, const DevStat
         // world segments of every geom, once (lanes over geoms)
         float* seg = sm + t.s_seg;
         float* bnd = seg + 8 * t.ngeoms;   // bounding sphere: centre (3), half-length + radius
-        const float* geo = sm + t.s_mc + t.mc_geo;                        // LDS copy
+        const float* geo = mcb + t.mc_geo;                                // LDS copy
         // geom pairs from the global table (cache-resident), the first 256 prefetched ahead of
         // the segment pass
         const int2* gpr = reinterpret_cast<const int2*>(t.g_pairs);
@@ -763,7 +780,7 @@ MI_D void wave_artic_substep(const DevModel& m, const WaveTabs& t, const DevStat
             }
             bnd[4 * g + 3] = 0.5f * sqrtf(e2) + A[7];
         }
-        __syncthreads();
+        wave_sync();
         // broad phase (conservative bounding spheres: the segments' distance is at least the
         // centre distance minus both half-lengths), survivors compacted in pair order
         int* surv = reinterpret_cast<int*>(sm + t.s_surv);
@@ -787,7 +804,7 @@ MI_D void wave_artic_substep(const DevModel& m, const WaveTabs& t, const DevStat
             nsv += __popcll(mask);
         }
         nsv = __builtin_amdgcn_readfirstlane(nsv);
-        __syncthreads();
+        wave_sync();
         // narrow phase on the survivors (mi_geom.h, as the oracle)
         int budget = (MI_MAX_ROWS - 3 * ncon - t.nlimc) / 3;
         for (int sb = 0; sb < nsv && budget > 0; sb += 64) {
@@ -878,7 +895,7 @@ MI_D void wave_artic_substep(const DevModel& m, const WaveTabs& t, const DevStat
         ncon = __builtin_amdgcn_readfirstlane(ncon);
     }
     const int nc = 3 * ncon;
-    __syncthreads();
+    wave_sync();
 
     STAMP(6);   // P8 contacts
     // ---- P7+P9: one batch, lanes over solve vectors b (64 per pass):
@@ -901,7 +918,7 @@ MI_D void wave_artic_substep(const DevModel& m, const WaveTabs& t, const DevStat
             for (int c = 0; c < NR; ++c)
                 if (c < nv) us[c] = us[c] + dt * res[c];
         }
-        __syncthreads();
+        wave_sync();
         // limit rows from u* (lane = joint), compacted after the contact rows
         bool act = false;
         float bl = 0.0f, sg = 0.0f;
@@ -927,7 +944,7 @@ MI_D void wave_artic_substep(const DevModel& m, const WaveTabs& t, const DevStat
             sm[t.s_rk + rl] = 3.0f;
         }
         nrows = __builtin_amdgcn_readfirstlane(nc + __popcll(limact));   // wave-uniform
-        __syncthreads();
+        wave_sync();
     };
     // file this lane's W row: contact row r (A_rr given), or an active limit row with its sign
     auto file_row = [&](const auto& res, bool on, int r, int kd, float a_contact) {
@@ -1057,7 +1074,7 @@ MI_D void wave_artic_substep(const DevModel& m, const WaveTabs& t, const DevStat
         STAMP(10);
     }
     nrows = __builtin_amdgcn_readfirstlane(nrows);
-    __syncthreads();
+    wave_sync();
 
     STAMP(10);  // P9 row filing + trailing barrier
     STAT(15, nrows);
@@ -1298,7 +1315,7 @@ MI_D void wave_artic_substep(const DevModel& m, const WaveTabs& t, const DevStat
         if (lane + 64 < nrows) sm[t.s_ad + lane + 64] = lam1;
     }
 #endif
-    __syncthreads();
+    wave_sync();
 
     STAMP(11);  // P10 PGS
     // ---- P11a: force sensors (lane s)
@@ -1406,7 +1423,7 @@ MI_D void wave_artic_substep(const DevModel& m, const WaveTabs& t, const DevStat
         else if (lane < 13) st.root_vel[sx(st, lane - 7, i)] = us[lane - 7];
     }
     if (__any(!finite) && lane == 0) st.nan_flag[i] = 1;
-    __syncthreads();
+    wave_sync();
     STAMP(12);  // P11
     STAMP_END();
 }
@@ -1425,7 +1442,7 @@ MI_D float wave_task_pre(const DevModel& m, const WaveTabs& t, const DevState& s
                          int64_t* progress_buf, float* potentials, float* prev_potentials,
                          float* actions_out) {
 #pragma clang fp contract(off)
-    const int lane = threadIdx.x, N = st.N, D = m.D, A = tp.A;
+    const int lane = wave_lane(), N = st.N, D = m.D, A = tp.A;
     const bool flagged = reset_buf[i] != 0;      // wave-uniform
     mi_dr_env dre{};
     if (tp.dr_act) dre = dr_begin(st, tp, 1, i, flagged);
@@ -1488,7 +1505,7 @@ MI_D void wave_loco_post(const DevModel& m, const WaveTabs& t, const DevState& s
                          int64_t* progress_buf, float* potentials, float* prev_potentials,
                          float* rew_out, int64_t* reset_out) {
 #pragma clang fp contract(off)
-    const int lane = threadIdx.x, D = m.D, S = m.S, O = tp.O;
+    const int lane = wave_lane(), D = m.D, S = m.S, O = tp.O;
     const float co = tp.clip_obs;
     const float* us = sm + t.s_us;
     float* out = obs_out + (size_t)O * i;
@@ -1535,7 +1552,7 @@ MI_D void wave_loco_post(const DevModel& m, const WaveTabs& t, const DevState& s
         }
     }
     if (lane < 6 * S) put(12 + 2 * D + lane, sm[t.s_rb + lane] * tp.contact_force_scale);
-    __syncthreads();
+    wave_sync();
     if (lane == 0) {
         float rp[3], rq[4], rv[6];
 #pragma unroll
