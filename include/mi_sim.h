@@ -32,7 +32,7 @@
 extern "C" {
 #endif
 
-#define MI_ABI_VERSION 1
+#define MI_ABI_VERSION 2
 
 enum {
     MI_OK = 0,
@@ -112,6 +112,8 @@ typedef struct mi_sim_params {
     float erp;                      /* position-error reduction per substep (0..1)    */
     int32_t enable_self_collisions; /* <Actor>.enable_self_collisions                 */
     float max_angular_velocity;     /* rad/s, PhysX default 5729.58 deg/s             */
+    float angular_damping;          /* 1/s, per-link angular velocity damping, PhysX  */
+                                    /* default 0.05 (docs/transfering_policies_...:74) */
 } mi_sim_params;
 
 /* Task-layer parameters (cfg/task/{Humanoid,Ant,Cartpole}.yaml `env:` + task

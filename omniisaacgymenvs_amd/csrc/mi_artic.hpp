@@ -27,6 +27,7 @@ struct SimP {
     float dt, g[3];
     int iters;
     float contact_offset, rest_offset, friction, max_depen, erp, max_angvel;
+    float ang_damp;   // per-link angular damping (1/s): torque -ang_damp * I_com * omega
 };
 
 MI_D void cartpole_substep(const DevModel& m, const SimP& p, float& x, float& th, float& xd,
@@ -200,6 +201,11 @@ MI_D void artic_substep(const DevModel& m, const DevState& st, const SimP& p, in
             crf(V, IV, t);
 #pragma unroll
             for (int c2 = 0; c2 < 6; ++c2) F[c2] = IA[c2] + t[c2];
+            // link angular damping: the torque -c I_com omega enters the bias as +c I_com omega
+            float Iwv[3];
+            m3_vec(Iw, V, Iwv);
+#pragma unroll
+            for (int c2 = 0; c2 < 3; ++c2) F[c2] = F[c2] + p.ang_damp * Iwv[c2];
         }
 #pragma unroll
         for (int c = 0; c < 10; ++c) w[m.o_Ic + 10 * l + c] = I[c];

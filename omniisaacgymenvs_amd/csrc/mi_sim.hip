@@ -585,9 +585,14 @@ static int sync_kparams(mi_sim* s) {
 // The parameter block is loop-invariant across substeps; laundering its pointer per substep
 // keeps the compiler from hoisting every field it reads into SGPRs for the whole loop
 // (hundreds of values, spilled to VGPR lanes). Fields are re-read (scalar cache hits).
+// The laundering goes through the constant address space: KParams is read-only while kernels
+// run, so the compiler may read its fields with scalar loads (through a generic pointer it
+// would emit flat vector loads, each a full memory round trip, for every parameter read).
+using CKParams = const __attribute__((address_space(4))) KParams;
 __device__ __forceinline__ const KParams* opaque_kp(const KParams* kp) {
-    asm volatile("" : "+s"(kp));
-    return kp;
+    CKParams* c = (CKParams*)kp;
+    asm volatile("" : "+s"(c));
+    return (const KParams*)c;
 }
 
 // copy the per-model constant block into this workgroup's LDS (once per launch; shared by the
@@ -1021,100 +1026,92 @@ int mi_sim_create(const mi_model_desc* md, const mi_sim_params* prm, int32_t N, 
 #undef UPW
         auto al4 = [](int x) { return (x + 3) & ~3; };
         const bool ct = s->topo != 0;
-        int so = 0;
-        auto take = [&](int n) { const int at = so; so += al4(n); return at; };
-        t.s_mc = take(t.mc_len);
-        t.s_R = take(9 * L); t.s_o = take(3 * L); t.s_S = take(6 * m.nv);
-        // P1..P4 working span: link inertias / forces, M, aux (local transforms, composites).
-        // On the compiled-topology path it is dead once P4 has moved M into registers, and
-        // P8/P9 reuse it for the contact and row data and the first W rows.
-        const int span0 = so;
-        t.s_F = take(16 * L);   // per-link records: inertia (10) + Newton-Euler force (6)
-        t.s_Ic = take(4);       // (kept for the layout order; records live at s_F)
-        t.s_M = take(m.nv * m.nv);
-        t.s_X = take(16 * L);
-        const int span1 = so;
-        t.s_D = take(ct ? 4 : WNV); t.s_r = take(WNV); t.s_us = take(WNV);
-        t.s_q = take(WNV); t.s_rp = take(8);
         const int R = m.max_rows;
         // contacts: ground points + self pairs, at most MI_MAX_ROWS / 3 in total
         t.self_on = self_on ? 1 : 0;
         t.npairs = self_on ? md->num_pairs : 0;
         t.ncmax = std::min(m.npts + t.npairs, MI_MAX_ROWS / 3);
         const int C = t.ncmax;
-        const int rows_len = 8 * al4(C) + 4 * al4(R) + WNV;
-        const bool overlay = ct && rows_len <= span1 - span0;
-        int ro = overlay ? span0 : so;
-        auto take_r = [&](int n) { const int at = ro; ro += al4(n); return at; };
-        t.s_cp = take_r(3 * C); t.s_cl = take_r(C); t.s_cl2 = take_r(C); t.s_cn = take_r(3 * C);
-        t.s_rl = take_r(R);
-        t.s_rb = take_r(R); t.s_rk = take_r(R); t.s_ad = take_r(R); t.s_lsg = take_r(WNV);
-        if (!overlay) so = ro;
-        // lane-private solve vectors of the runtime-table solves (CT solves run in registers)
-        t.s_xs = take(ct ? 4 : WNV * 64);
-        {   // CT path: published factor rows (each padded to 4) + 1/D (DofTree::lrow)
-            int lr = 0;
-            for (int k = 0; k < m.nv; ++k) lr += (anc_start[k + 1] - anc_start[k] + 3) & ~3;
-            t.s_L = take(ct ? lr + m.nv : 4);
-        }
-        // CT path: J rows of up to 64 constraint rows for the PGS (LDS is not the occupancy
-        // limit here: registers cap the wave path at 2 waves/SIMD = 8 envs/CU = 20 KB each)
-        t.j_rows_lds = ct ? std::min(48, m.max_rows) : 0;
-        if (const char* e = getenv("MI_WAVE_JROWS")) if (ct) t.j_rows_lds = std::min(t.j_rows_lds, atoi(e));
-        t.s_J = take(ct ? t.j_rows_lds * m.nv : 4);
-        // CT path: W rows for the P9 -> P10 hand-over. First choice: the rest of the dead
-        // span; when that holds fewer rows than a one-bank PGS can use and the LDS budget of
-        // the wave path (8 envs / CU, 20 KB each) has room, a dedicated region instead, so
-        // the global slab is only the fallback of rare row-heavy substeps.
-        // Otherwise, a second segment at the end takes whatever rows the budget still holds
-        // (rows [w_rows_a, w_rows_lds) at s_W2).
-        t.s_W = ro;
-        t.w_rows_lds = overlay ? std::min(64, (span1 - ro) / m.nv) : 0;
-        t.w_rows_a = t.w_rows_lds;
-        t.s_W2 = 0;
-        {
-            int want = std::min(64, m.max_rows);
-            if (const char* e = getenv("MI_WAVE_WROWS")) want = std::min(want, atoi(e));
-            const int lds_budget_floats = (160 * 1024 / 8) / (int)sizeof(float);
-            if (ct && t.w_rows_lds < want && so + al4(want * m.nv) <= lds_budget_floats) {
-                t.s_W = take(want * m.nv);
-                t.w_rows_lds = t.w_rows_a = want;
-            } else if (ct && self_on && t.w_rows_lds < want) {   // (w_row<kSelf> on device)
-                const int extra = std::min(want - t.w_rows_lds, (lds_budget_floats - so - 3) / m.nv);
-                if (extra > 0) {
-                    t.s_W2 = take(extra * m.nv);
-                    t.w_rows_lds += extra;
-                }
+        t.max_rows = m.max_rows;
+        t.g_row_stride = (size_t)m.max_rows * WNV;
+        t.ngeoms = md->num_geoms;
+        t.s_seg = -1; t.s_surv = -1; t.s_W2 = 0;
+        int lr = 0;   // compact factor rows (each padded to 4) + 1/D (DofTree::lrow)
+        for (int k = 0; k < m.nv; ++k) lr += (anc_start[k + 1] - anc_start[k] + 3) & ~3;
+        int so = 0;
+        bool env_region_over = false;
+        auto take = [&](int n) { const int at = so; so += al4(n); return at; };
+        t.s_mc = take(t.mc_len);   // shared by the workgroup's envs
+        if (ct) {
+            // Compiled-topology layout, sized so 16 envs are resident per CU (4 waves / SIMD,
+            // all 4096 envs of a launch in one round): the persistent per-env state, then ONE
+            // work region reused phase by phase — P1..P3 link records / aux; P8..P10 contact and
+            // row data, the row -> lane owner table, then the W rows (or the P8 self-collision
+            // scratch). M~ goes straight into the factor's compact rows (s_L); J rows are never
+            // stored (the Delassus rows are built in registers in P9).
+            t.envs_per_wg = 4;
+            if (const char* e = getenv("MI_WAVE_ENVS")) t.envs_per_wg = std::max(1, std::min(4, atoi(e)));
+            t.s_R = take(9 * L); t.s_o = take(3 * L); t.s_S = take(6 * m.nv);
+            t.s_D = take(4); t.s_r = take(WNV); t.s_us = take(WNV); t.s_q = take(WNV); t.s_rp = take(8);
+            t.s_xs = take(4);
+            t.s_L = take(lr + m.nv);
+            t.s_M = t.s_L;
+            const int work = so;
+            int wo = work;
+            auto take_w = [&](int n) { const int at = wo; wo += al4(n); return at; };
+            t.s_F = take_w(16 * L);   // per-link records: inertia (10) + Newton-Euler force (6)
+            t.s_Ic = take_w(4);
+            t.s_X = take_w(16 * L);
+            const int span_end = wo;
+            wo = work;
+            t.s_cp = take_w(3 * C); t.s_cl = take_w(C); t.s_cl2 = take_w(C); t.s_cn = take_w(3 * C);
+            t.s_rl = take_w(R); t.s_rb = take_w(R); t.s_rk = take_w(R); t.s_ad = take_w(R);
+            t.s_lsg = take_w(WNV); t.s_own = take_w(64);
+            const int rows_end = wo;
+            int seg_end = rows_end;
+            if (self_on) {
+                t.s_seg = rows_end;
+                t.s_surv = rows_end + al4(12 * md->num_geoms);
+                seg_end = t.s_surv + al4(md->num_pairs);
             }
+            // LDS per env: 16 envs / CU = 16 / E workgroups, each with its constant block
+            const int E = t.envs_per_wg;
+            const int wg_floats = (163840 / (int)sizeof(float)) / (16 / E);
+            const int env_floats = (wg_floats - al4(t.mc_len)) / E;
+            int wrows = std::min(64, m.max_rows);
+            if (const char* e = getenv("MI_WAVE_WROWS")) wrows = std::min(wrows, std::max(0, atoi(e)));
+            // whole W region (al4-padded) inside the env's share of the budget
+            wrows = std::max(0, std::min(wrows, (t.s_R + env_floats - rows_end) / m.nv));
+            while (wrows > 0 && rows_end + al4(wrows * m.nv) > t.s_R + env_floats) --wrows;
+            t.s_W = rows_end;
+            t.w_rows_lds = t.w_rows_a = wrows;
+            so = std::max(span_end, std::max(seg_end, rows_end + al4(wrows * m.nv)));
+            env_region_over = so - t.s_R > env_floats;   // fewer than 16 envs / CU fit
+        } else {
+            // runtime tables (models without a generated topology): one env per workgroup,
+            // dense M, lane-private solve vectors, every W row through the global slab
+            t.envs_per_wg = 1;
+            if (const char* e = getenv("MI_WAVE_ENVS")) t.envs_per_wg = std::max(1, std::min(4, atoi(e)));
+            t.s_R = take(9 * L); t.s_o = take(3 * L); t.s_S = take(6 * m.nv);
+            t.s_F = take(16 * L); t.s_Ic = take(4); t.s_M = take(m.nv * m.nv); t.s_X = take(16 * L);
+            t.s_D = take(WNV); t.s_r = take(WNV); t.s_us = take(WNV); t.s_q = take(WNV); t.s_rp = take(8);
+            t.s_cp = take(3 * C); t.s_cl = take(C); t.s_cl2 = take(C); t.s_cn = take(3 * C);
+            t.s_rl = take(R); t.s_rb = take(R); t.s_rk = take(R); t.s_ad = take(R);
+            t.s_lsg = take(WNV); t.s_own = take(64);
+            t.s_xs = take(WNV * 64);
+            t.s_L = take(4);
+            t.s_W = so;
+            t.w_rows_lds = t.w_rows_a = 0;
         }
         t.s_total = so;
         // E envs per workgroup share the constant block [0, s_env); env w's region is shifted
         // by w * env_stride
         t.s_env = t.s_R;
         t.env_stride = so - t.s_env;
-        t.envs_per_wg = 1;
-        if (const char* e = getenv("MI_WAVE_ENVS")) t.envs_per_wg = std::max(1, std::min(4, atoi(e)));
-        {   // the sequential regions strictly increase; the row data sits inside the dead
-            // span (overlay) or between s_rp and s_xs
-            const int offs[] = {t.s_mc, t.s_R, t.s_o, t.s_S, t.s_F, t.s_Ic, t.s_M, t.s_X,
-                                t.s_D, t.s_r, t.s_us, t.s_q, t.s_rp, t.s_xs, t.s_L, t.s_J,
-                                t.s_total};
-            for (size_t c = 1; c < sizeof(offs) / sizeof(offs[0]); ++c)
-                if (offs[c] <= offs[c - 1]) return cleanup(fail(MI_E_STATE, "wave LDS layout: region %zu overlaps", c));
-            const bool rows_ok = overlay ? (t.s_cp == span0 && ro <= span1)
-                                         : (t.s_cp > t.s_rp && ro <= t.s_xs);
-            if (!rows_ok) return cleanup(fail(MI_E_STATE, "wave LDS layout: row data misplaced"));
-        }
-        t.max_rows = m.max_rows;
-        t.g_row_stride = (size_t)m.max_rows * WNV;
-        // P8 self-collision scratch (segments + broad-phase survivors) in the same free span
-        t.ngeoms = md->num_geoms;
-        t.s_seg = -1; t.s_surv = -1;
-        if (overlay && self_on && al4(12 * md->num_geoms) + al4(md->num_pairs) <= span1 - ro) {
-            t.s_seg = ro;
-            t.s_surv = ro + al4(12 * md->num_geoms);
-        }
         s->lds_bytes = (size_t)(so + (t.envs_per_wg - 1) * t.env_stride) * sizeof(float);
+        if (s->lds_bytes > 163840)
+            return cleanup(fail(MI_E_MODEL, "wave path: %zu B of LDS per workgroup exceed the CU's 160 KiB",
+                                s->lds_bytes));
     }
     s->lower.assign(md->lower, md->lower + L);
     s->upper.assign(md->upper, md->upper + L);
@@ -1128,6 +1125,8 @@ int mi_sim_create(const mi_model_desc* md, const mi_sim_params* prm, int32_t N, 
     s->sp.max_depen = prm->max_depenetration_velocity;
     s->sp.erp = prm->erp;
     s->sp.max_angvel = prm->max_angular_velocity;
+    s->sp.ang_damp = prm->angular_damping;
+    if (!(prm->angular_damping >= 0.0f)) return cleanup(fail(MI_E_ARG, "angular_damping must be >= 0"));
     // state
     DevState& st = s->ds;
     st.N = N;

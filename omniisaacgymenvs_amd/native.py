@@ -46,6 +46,7 @@ class MiSimParams(C.Structure):
         ("contact_offset", C.c_float), ("rest_offset", C.c_float), ("friction", C.c_float),
         ("max_depenetration_velocity", C.c_float), ("erp", C.c_float),
         ("enable_self_collisions", C.c_int32), ("max_angular_velocity", C.c_float),
+        ("angular_damping", C.c_float),
     ]
 
 

@@ -30,6 +30,9 @@ default_physx_params: Dict[str, Any] = {
     # PhysX rigid-body default max angular velocity 5729.58 deg/s
     # (docs/transfering_policies_from_isaac_gym.md:73-76)
     "max_angular_velocity": math.radians(5729.58),
+    # PhysX articulation-link default angular damping 0.05
+    # (docs/transfering_policies_from_isaac_gym.md:74); the task YAMLs do not set it
+    "angular_damping": 0.05,
 }
 default_physics_material = {"static_friction": 1.0, "dynamic_friction": 1.0, "restitution": 0.0}
 default_sim_params: Dict[str, Any] = {
@@ -124,4 +127,5 @@ class SimConfig:
         esc = a.get("enable_self_collisions", False)
         p.enable_self_collisions = 1 if esc is True or esc == 1 else 0
         p.max_angular_velocity = float(px.get("max_angular_velocity", math.radians(5729.58)))
+        p.angular_damping = float(a.get("angular_damping", px.get("angular_damping", 0.05)))
         return p

@@ -371,7 +371,7 @@ static void cartpole_substep(const model_t* m, const mi_sim_params* p, float* q,
 /* articulated physics — per-env workspace                                               */
 /* ------------------------------------------------------------------------------------ */
 typedef struct {
-    float *R, *o, *aw, *I6, *S, *V, *A, *J, *M, *Gc, *C, *u, *rhs, *ud;
+    float *R, *o, *aw, *I6, *Iw, *S, *V, *A, *J, *M, *Gc, *C, *u, *rhs, *ud;
     float *Jr, *W, *b, *lam, *Ad, *cpt, *cdir, *tmp;
     int *rkind, *rcon, *clink, *clink2;
     int nrows, ncon;
@@ -383,6 +383,7 @@ static ws_t* ws_new(const model_t* m) {
     int L = m->L, nv = m->nv, R = m->max_rows > 0 ? m->max_rows : 1;
     w->R = (float*)calloc(L * 9, 4); w->o = (float*)calloc(L * 3, 4);
     w->aw = (float*)calloc(L * 3, 4); w->I6 = (float*)calloc(L * 36, 4);
+    w->Iw = (float*)calloc(L * 9, 4);
     w->S = (float*)calloc(nv * 6 + 6, 4); w->V = (float*)calloc(L * 6, 4);
     w->A = (float*)calloc(L * 6, 4); w->J = (float*)calloc((size_t)L * 6 * nv + 1, 4);
     w->M = (float*)calloc(nv * nv + 1, 4); w->Gc = (float*)calloc(nv * nv + 1, 4);
@@ -398,7 +399,7 @@ static ws_t* ws_new(const model_t* m) {
     return w;
 }
 static void ws_free(ws_t* w) {
-    void* p[] = {w->R, w->o, w->aw, w->I6, w->S, w->V, w->A, w->J, w->M, w->Gc, w->C, w->u,
+    void* p[] = {w->R, w->o, w->aw, w->I6, w->Iw, w->S, w->V, w->A, w->J, w->M, w->Gc, w->C, w->u,
                  w->rhs, w->ud, w->Jr, w->W, w->b, w->lam, w->Ad, w->rkind, w->rcon, w->cpt,
                  w->clink, w->clink2, w->cdir, w->tmp};
     for (size_t i = 0; i < sizeof p / sizeof p[0]; ++i) free(p[i]);
@@ -437,6 +438,7 @@ static void kinematics(const model_t* m, ws_t* w, const float* rq, const float* 
     for (int l = 0; l < L; ++l) {
         float* I = w->I6 + 36 * l;
         memset(I, 0, 144);
+        memset(w->Iw + 9 * l, 0, 36);
         float mass = m->mass[l];
         if (mass <= 0.0f) continue;
         float c[3], Ic[9], T[9], Rl[9];
@@ -448,6 +450,7 @@ static void kinematics(const model_t* m, ws_t* w, const float* rq, const float* 
         m3_mul(Rl, Ib, T);
         float Rt[9] = {Rl[0], Rl[3], Rl[6], Rl[1], Rl[4], Rl[7], Rl[2], Rl[5], Rl[8]};
         m3_mul(T, Rt, Ic);
+        memcpy(w->Iw + 9 * l, Ic, 36);   /* world inertia about the COM (link damping) */
         /* Ibar = Ic + m (|c|^2 1 - c c^T) ; [c]x[c]x^T = |c|^2 1 - c c^T */
         float cc = dot3(c, c);
         for (int i = 0; i < 3; ++i)
@@ -533,6 +536,13 @@ static void dynamics_terms(const model_t* m, const mi_sim_params* p, ws_t* w, co
         m6_vec(I, w->V + 6 * l, Iv);
         crf(w->V + 6 * l, Iv, t);
         for (int r = 0; r < 6; ++r) f[r] += t[r];
+        /* link angular damping (PhysX default 0.05, docs/transfering_policies_from_isaac_gym.md:74):
+         * the torque -c I_com omega on the link enters the bias as +c I_com omega */
+        {
+            float Iwv[3];
+            m3_vec(w->Iw + 9 * l, w->V + 6 * l, Iwv);
+            for (int r = 0; r < 3; ++r) f[r] = f[r] + p->angular_damping * Iwv[r];
+        }
         for (int k = 0; k < nv; ++k) {
             float acc = 0.0f;
             for (int r = 0; r < 6; ++r) acc += Jl[r * nv + k] * f[r];
@@ -1235,6 +1245,11 @@ void orc_aba(orc_sim* s, int env, const float* tau, float* udot) {
         crf(w->V + 6 * l, Iv, t);
         m6_vec(w->I6 + 36 * l, gv, fg);
         for (int r = 0; r < 6; ++r) pA[6 * l + r] = t[r] - fg[r];
+        {   /* link angular damping, as in dynamics_terms */
+            float Iwv[3];
+            m3_vec(w->Iw + 9 * l, w->V + 6 * l, Iwv);
+            for (int r = 0; r < 3; ++r) pA[6 * l + r] += p->angular_damping * Iwv[r];
+        }
         if (l == 0) {
             if (m->root_free) {
                 float wv[3];

@@ -30,10 +30,11 @@ def _random_state(sim, m, z, seed, vel_scale=0.5):
     return q, qd
 
 
+@pytest.mark.parametrize("damp", [0.0, 0.05])
 @pytest.mark.parametrize("name", ["Humanoid", "Ant"])
-def test_aba_matches_dense_solve(name):
+def test_aba_matches_dense_solve(name, damp):
     m = load_robot(name)
-    sim = OracleSim(m, sim_params(), 4, np.zeros((4, 3), np.float32))
+    sim = OracleSim(m, sim_params(angular_damping=damp), 4, np.zeros((4, 3), np.float32))
     q, qd = _random_state(sim, m, 3.0, 0)
     rng = np.random.default_rng(1)
     for env in range(4):
@@ -163,3 +164,32 @@ def test_self_collision_limits_penetration():
         worst[esc] = w
     assert worst[1] > -0.06, worst
     assert worst[0] < worst[1] - 0.03, worst
+
+
+SPHERE_XML = """<mujoco model="ball"><compiler angle="degree"/><worldbody>
+<body name="ball" pos="0 0 5"><freejoint name="root"/><geom type="sphere" size="0.3" density="800"/>
+</body></worldbody></mujoco>"""
+
+
+@pytest.mark.parametrize("damp", [0.05, 2.0])
+def test_link_angular_damping_decays_spin(tmp_path, damp):
+    """KAT for the per-link angular damping (PhysX link default 0.05,
+    docs/transfering_policies_from_isaac_gym.md:74): a free sphere (isotropic inertia, so no
+    gyroscopic coupling) spinning without gravity loses angular velocity as
+    omega_{n+1} = (1 - c dt) omega_n (semi-implicit step, damping torque -c I omega), and its
+    linear velocity is untouched."""
+    f = tmp_path / "ball.xml"
+    f.write_text(SPHERE_XML)
+    m = compile_mjcf(str(f))
+    dt, n = 0.0083, 50
+    sim = OracleSim(m, sim_params(gravity=(0.0, 0.0, 0.0), dt=dt, angular_damping=damp), 1,
+                    np.zeros((1, 3), np.float32))
+    w0 = np.array([1.5, -2.0, 0.7], np.float32)
+    v0 = np.array([0.3, 0.1, -0.2], np.float32)
+    sim.set_root_state(np.array([[0.0, 0.0, 5.0]], np.float32), np.array([[1.0, 0, 0, 0]], np.float32),
+                       np.concatenate([v0, w0])[None])
+    for _ in range(n):
+        sim.step(1)
+    _, _, vel = sim.root_state()
+    np.testing.assert_allclose(vel[0, 3:], w0 * (1.0 - damp * dt) ** n, rtol=2e-4, atol=1e-6)
+    np.testing.assert_allclose(vel[0, :3], v0, rtol=1e-5, atol=1e-6)

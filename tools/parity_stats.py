@@ -1,0 +1,73 @@
+#!/usr/bin/env python3
+"""Device-vs-oracle error distribution of the fused env step from identical state (the
+full-size parity test's setting, without the pass/fail): per env the max |obs - obs_oracle|
+and |rew - rew_oracle| over each step, summarised as quantiles, and the worst envs with their
+oracle decision margins. Test infrastructure (imports the oracle as the checker).
+
+usage: parity_stats.py [Task] [num_envs] [steps]
+"""
+import json
+import os
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+
+
+def main():
+    import numpy as np
+    import torch
+
+    from omniisaacgymenvs_amd import native as N
+    from omniisaacgymenvs_amd.utils.task_util import make_env
+    from oracle.oracle import lib as orc_lib
+    from tests.helpers import oracle_twin, sync_oracle, task_buffers
+
+    task_name = sys.argv[1] if len(sys.argv) > 1 else "Humanoid"
+    n = int(sys.argv[2]) if len(sys.argv) > 2 else 4096
+    steps = int(sys.argv[3]) if len(sys.argv) > 3 else 4
+    env = make_env(task_name, num_envs=n, device="cuda:0", seed=3)
+    task = env.task
+    view = task.get_robot()
+
+    def acts(k):
+        a = torch.empty((n, env.num_actions), device="cuda:0")
+        N.check(N.lib().mi_fill_uniform(view.handle, a.data_ptr(), env.num_actions, 42, k, -1.0, 1.0,
+                                        view.stream()))
+        return a
+
+    env.reset()
+    for k in range(3):
+        env.step(acts(k))
+    torch.cuda.synchronize()
+    orc_lib().orc_set_threads(min(16, os.cpu_count() or 1))
+    orc = oracle_twin(env, seed=3)
+    sync_oracle(env, orc)
+    errs, margins = [], []
+    for k in range(3, 3 + steps):
+        b = task_buffers(env)
+        a = acts(k)
+        o, r, d, _ = env.step(a)
+        torch.cuda.synchronize()
+        orc.env_step(a.cpu().numpy(), task.control_frequency_inv, b)
+        e = np.maximum(np.abs(o["obs"].cpu().numpy() - b["obs"]).max(axis=1),
+                       np.abs(r.cpu().numpy() - b["rew"]))
+        errs.append(e)
+        margins.append(orc.decision_margin().copy())
+        sync_oracle(env, orc)
+    e = np.concatenate(errs)
+    m = np.concatenate(margins)
+    q = {f"q{p}": float(np.quantile(e, p / 100)) for p in (50, 90, 99, 99.9)}
+    far = m >= 1e-4
+    worst = np.argsort(-np.where(far, e, 0))[:8]
+    out = {"task": task_name, "envs": n, "steps": steps, **q, "max": float(e.max()),
+           "max_far_from_threshold": float(e[far].max()) if far.any() else None,
+           "frac_gt_2e-3_far": float((e[far] > 2e-3).mean()) if far.any() else None,
+           "worst_far": [(int(i % n), int(i // n), float(e[i]), float(m[i])) for i in worst]}
+    print(json.dumps(out), flush=True)
+    orc.close()
+    env.close()
+
+
+if __name__ == "__main__":
+    main()

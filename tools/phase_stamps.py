@@ -12,7 +12,7 @@ import sys
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
-os.environ["MI_SIM_LIB"] = os.path.join(ROOT, "omniisaacgymenvs_amd", "libmi_sim_stamps.so")
+os.environ["MI_SIM_LIB"] = os.environ.get("MI_STAMPS_LIB", os.path.join(ROOT, "omniisaacgymenvs_amd", "libmi_sim_stamps.so"))
 
 PHASES = {0: "load", 1: "P1 fk+link dynamics", 2: "P2 composite", 3: "P3 crba", 4: "P4 ltdl+publish",
           5: "P5 1/D (runtime path)", 6: "P8 contacts", 7: "P9 J build", 8: "P9 solves",
@@ -53,10 +53,10 @@ def main():
     print(f"{'total (1 env-substep)':26s} {tot:9.0f}")
     stats = {"mean rows": buf[15] / cnt, "frac rows > LDS W rows": buf[16] / cnt,
              "frac rows > 64": buf[17] / cnt, "frac solve vectors > 64": buf[18] / cnt,
-             "frac rows > LDS J rows": buf[19] / cnt, "mean contacts": buf[20] / cnt,
+             "frac u-space PGS": buf[19] / cnt, "mean contacts": buf[20] / cnt,
              "frac rows > 16": buf[21] / cnt, "frac rows > 24": buf[22] / cnt,
              "frac rows > 32": buf[23] / cnt, "frac rows > 40": buf[24] / cnt,
-             "frac rows > 48": buf[25] / cnt, "LDS W rows": buf[26] / cnt, "LDS J rows": buf[27] / cnt}
+             "frac rows > 48": buf[25] / cnt, "LDS W rows": buf[26] / cnt, "Delassus PGS rows max": buf[27] / cnt}
     print(json.dumps({"row_stats_per_env_substep": {k: round(v, 4) for k, v in stats.items()}}))
 
 
