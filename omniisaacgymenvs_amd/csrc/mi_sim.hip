@@ -688,21 +688,47 @@ __global__ void k_reset_idx(DevModel m, DevState st, DevTask tp, const int64_t* 
 }
 
 // state fields (field stride fs, env stride es: DevState) <-> row-major [N,C] torch tensors
-// (gather / scatter with optional indices)
-__global__ void k_soa_to_rows(const float* src, int N, int C, int fs, int es, float* dst) {
-    const int i = blockIdx.x * blockDim.x + threadIdx.x;
-    if (i >= N) return;
-    for (int c = 0; c < C; ++c) dst[(size_t)i * C + c] = src[(size_t)c * fs + (size_t)i * es];
+// (ArticulationView getters / setters, gather / scatter with optional indices). One element per
+// lane with the column fastest, so the row-major side is one contiguous stream; on the
+// per-env-record layout (fs = 1) the state side is too (the C fields of a record are adjacent).
+// The field-major layout of the one-lane-per-env path (es = 1) gathers through an LDS tile:
+// field-major reads in, row-major writes out, both coalesced.
+constexpr int MI_GATHER_TILE = 256, MI_GATHER_MAXC = 32;
+__global__ __launch_bounds__(256) void k_soa_to_rows(const float* __restrict__ src, int N, int C,
+                                                    int fs, int es, float* __restrict__ dst) {
+    const int64_t e0 = (int64_t)blockIdx.x * MI_GATHER_TILE;
+    const int ne = (int)min((int64_t)MI_GATHER_TILE, (int64_t)N - e0);
+    const int tot = ne * C;
+    float* out = dst + e0 * C;
+    if (es != 1 || C > MI_GATHER_MAXC) {           // records (or too wide for the tile)
+        for (int t = threadIdx.x; t < tot; t += blockDim.x) {
+            const int e = t / C, c = t - e * C;
+            out[t] = src[(size_t)c * fs + (size_t)(e0 + e) * es];
+        }
+        return;
+    }
+    __shared__ float tile[MI_GATHER_MAXC * (MI_GATHER_TILE + 1)];   // [c][e], odd stride
+    for (int c = 0; c < C; ++c)
+        if ((int)threadIdx.x < ne) tile[c * (MI_GATHER_TILE + 1) + threadIdx.x] = src[(size_t)c * fs + e0 + threadIdx.x];
+    __syncthreads();
+    for (int t = threadIdx.x; t < tot; t += blockDim.x) {
+        const int e = t / C, c = t - e * C;
+        out[t] = tile[c * (MI_GATHER_TILE + 1) + e];
+    }
 }
 template <typename IDX>
-__global__ void k_rows_to_soa(const float* src, int n, int C, const IDX* idx, int N, int fs, int es,
-                              float* dst) {
-    const int t = blockIdx.x * blockDim.x + threadIdx.x;
-    if (t >= n) return;
-    const int64_t i = idx ? (int64_t)idx[t] : t;
-    if (i < 0 || i >= N) return;
-    for (int c = 0; c < C; ++c) dst[(size_t)c * fs + (size_t)i * es] = src[(size_t)t * C + c];
+__global__ __launch_bounds__(256) void k_rows_to_soa(const float* __restrict__ src, int n, int C,
+                                                    const IDX* __restrict__ idx, int N, int fs, int es,
+                                                    float* __restrict__ dst) {
+    const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (t >= (int64_t)n * C) return;
+    const int r = (int)(t / C), c = (int)(t - (int64_t)r * C);
+    const int64_t i = idx ? (int64_t)idx[r] : r;
+    if (i < 0 || i >= N) return;                   // out-of-range ids are ignored
+    dst[(size_t)c * fs + (size_t)i * es] = src[t];
 }
+static inline dim3 gather_grid(int N) { return dim3((N + MI_GATHER_TILE - 1) / MI_GATHER_TILE); }
+static inline dim3 scatter_grid(int n, int C) { return dim3((unsigned)(((int64_t)n * C + 255) / 256)); }
 
 __global__ void k_init_state(DevState st, int D) {
     const int i = blockIdx.x * blockDim.x + threadIdx.x;
@@ -1215,7 +1241,7 @@ int mi_sim_info(const mi_sim* s, int32_t* num_envs, int32_t* num_dof, int32_t* n
 int mi_get_root_state(mi_sim* s, float* pos, float* quat, float* vel, void* stream) {
     NEED(s);
     HIP_TRY(hipSetDevice(s->device));
-    const dim3 g = grid_for(s, s->N), b(s->block);
+    const dim3 g = gather_grid(s->N), b(256);
     if (pos) hipLaunchKernelGGL(k_soa_to_rows, g, b, 0, STREAM(stream), s->ds.root_pos, s->N, 3, s->ds.fs, s->ds.es, pos);
     if (quat) hipLaunchKernelGGL(k_soa_to_rows, g, b, 0, STREAM(stream), s->ds.root_quat, s->N, 4, s->ds.fs, s->ds.es, quat);
     if (vel) hipLaunchKernelGGL(k_soa_to_rows, g, b, 0, STREAM(stream), s->ds.root_vel, s->N, 6, s->ds.fs, s->ds.es, vel);
@@ -1226,7 +1252,7 @@ int mi_get_root_state(mi_sim* s, float* pos, float* quat, float* vel, void* stre
 int mi_get_dof_state(mi_sim* s, float* q, float* qd, void* stream) {
     NEED(s);
     HIP_TRY(hipSetDevice(s->device));
-    const dim3 g = grid_for(s, s->N), b(s->block);
+    const dim3 g = gather_grid(s->N), b(256);
     if (q) hipLaunchKernelGGL(k_soa_to_rows, g, b, 0, STREAM(stream), s->ds.q, s->N, s->dm.D, s->ds.fs, s->ds.es, q);
     if (qd) hipLaunchKernelGGL(k_soa_to_rows, g, b, 0, STREAM(stream), s->ds.qd, s->N, s->dm.D, s->ds.fs, s->ds.es, qd);
     LAUNCH_CHECK();
@@ -1237,7 +1263,7 @@ int mi_get_sensor_wrench(mi_sim* s, float* out, void* stream) {
     NEED(s); NEED(out);
     HIP_TRY(hipSetDevice(s->device));
     if (s->dm.S == 0) return MI_OK;
-    hipLaunchKernelGGL(k_soa_to_rows, grid_for(s, s->N), dim3(s->block), 0, STREAM(stream),
+    hipLaunchKernelGGL(k_soa_to_rows, gather_grid(s->N), dim3(256), 0, STREAM(stream),
                        s->ds.sens, s->N, 6 * s->dm.S, s->ds.fs, s->ds.es, out);
     LAUNCH_CHECK();
     return MI_OK;
@@ -1248,7 +1274,7 @@ int mi_set_dof_efforts(mi_sim* s, const float* eff, const int32_t* idx, int32_t 
     if (n < 0 || n > s->N || (!idx && n != s->N)) return fail(MI_E_SHAPE, "mi_set_dof_efforts: bad n=%d", n);
     HIP_TRY(hipSetDevice(s->device));
     if (n == 0) return MI_OK;
-    hipLaunchKernelGGL(k_rows_to_soa<int32_t>, grid_for(s, n), dim3(s->block), 0, STREAM(stream),
+    hipLaunchKernelGGL(k_rows_to_soa<int32_t>, scatter_grid(n, s->dm.D), dim3(256), 0, STREAM(stream),
                        eff, n, s->dm.D, idx, s->N, s->ds.fs, s->ds.es, s->ds.eff);
     LAUNCH_CHECK();
     return MI_OK;
@@ -1260,7 +1286,7 @@ int mi_set_dof_state(mi_sim* s, const float* q, const float* qd, const int64_t* 
     if (n < 0 || n > s->N || (!idx && n != s->N)) return fail(MI_E_SHAPE, "mi_set_dof_state: bad n=%d", n);
     HIP_TRY(hipSetDevice(s->device));
     if (n == 0) return MI_OK;
-    const dim3 g = grid_for(s, n), b(s->block);
+    const dim3 g = scatter_grid(n, s->dm.D), b(256);
     if (q) hipLaunchKernelGGL(k_rows_to_soa<int64_t>, g, b, 0, STREAM(stream), q, n, s->dm.D, idx, s->N, s->ds.fs, s->ds.es, s->ds.q);
     if (qd) hipLaunchKernelGGL(k_rows_to_soa<int64_t>, g, b, 0, STREAM(stream), qd, n, s->dm.D, idx, s->N, s->ds.fs, s->ds.es, s->ds.qd);
     LAUNCH_CHECK();
@@ -1273,10 +1299,10 @@ int mi_set_root_state(mi_sim* s, const float* pos, const float* quat, const floa
     if (n < 0 || n > s->N || (!idx && n != s->N)) return fail(MI_E_SHAPE, "mi_set_root_state: bad n=%d", n);
     HIP_TRY(hipSetDevice(s->device));
     if (n == 0) return MI_OK;
-    const dim3 g = grid_for(s, n), b(s->block);
-    if (pos) hipLaunchKernelGGL(k_rows_to_soa<int64_t>, g, b, 0, STREAM(stream), pos, n, 3, idx, s->N, s->ds.fs, s->ds.es, s->ds.root_pos);
-    if (quat) hipLaunchKernelGGL(k_rows_to_soa<int64_t>, g, b, 0, STREAM(stream), quat, n, 4, idx, s->N, s->ds.fs, s->ds.es, s->ds.root_quat);
-    if (vel) hipLaunchKernelGGL(k_rows_to_soa<int64_t>, g, b, 0, STREAM(stream), vel, n, 6, idx, s->N, s->ds.fs, s->ds.es, s->ds.root_vel);
+    const dim3 b(256);
+    if (pos) hipLaunchKernelGGL(k_rows_to_soa<int64_t>, scatter_grid(n, 3), b, 0, STREAM(stream), pos, n, 3, idx, s->N, s->ds.fs, s->ds.es, s->ds.root_pos);
+    if (quat) hipLaunchKernelGGL(k_rows_to_soa<int64_t>, scatter_grid(n, 4), b, 0, STREAM(stream), quat, n, 4, idx, s->N, s->ds.fs, s->ds.es, s->ds.root_quat);
+    if (vel) hipLaunchKernelGGL(k_rows_to_soa<int64_t>, scatter_grid(n, 6), b, 0, STREAM(stream), vel, n, 6, idx, s->N, s->ds.fs, s->ds.es, s->ds.root_vel);
     LAUNCH_CHECK();
     return MI_OK;
 }

@@ -189,6 +189,8 @@ class ArticulationView:
         else:
             idx = torch.as_tensor(indices, device=self.device).to(torch.int32).contiguous()
             n = int(idx.numel())
+            if n == 0:          # empty index list: nothing to write
+                return
         N.check(N.lib().mi_set_dof_efforts(self.handle, e.data_ptr(),
                                            None if idx is None else idx.data_ptr(), n,
                                            self.stream()), "mi_set_dof_efforts")
@@ -196,24 +198,32 @@ class ArticulationView:
     def set_joint_positions(self, positions: torch.Tensor, indices=None) -> None:
         q = self._f32(positions)
         idx, n = self._idx64(indices)
+        if n == 0:              # empty index list: nothing to write
+            return
         N.check(N.lib().mi_set_dof_state(self.handle, q.data_ptr(), None, N.ptr(idx), n,
                                          self.stream()), "mi_set_dof_state")
 
     def set_joint_velocities(self, velocities: torch.Tensor, indices=None) -> None:
         qd = self._f32(velocities)
         idx, n = self._idx64(indices)
+        if n == 0:              # empty index list: nothing to write
+            return
         N.check(N.lib().mi_set_dof_state(self.handle, None, qd.data_ptr(), N.ptr(idx), n,
                                          self.stream()), "mi_set_dof_state")
 
     def set_world_poses(self, positions=None, orientations=None, indices=None) -> None:
         p, r = self._f32(positions), self._f32(orientations)
         idx, n = self._idx64(indices)
+        if n == 0:              # empty index list: nothing to write
+            return
         N.check(N.lib().mi_set_root_state(self.handle, N.ptr(p), N.ptr(r), None, N.ptr(idx), n,
                                           self.stream()), "mi_set_root_state")
 
     def set_velocities(self, velocities: torch.Tensor, indices=None) -> None:
         v = self._f32(velocities)
         idx, n = self._idx64(indices)
+        if n == 0:              # empty index list: nothing to write
+            return
         N.check(N.lib().mi_set_root_state(self.handle, None, None, v.data_ptr(), N.ptr(idx), n,
                                           self.stream()), "mi_set_root_state")
 

@@ -13,7 +13,7 @@ import torch
 
 from omniisaacgymenvs_amd.utils.task_util import make_env
 from tests.helpers import oracle_twin, rand_actions, sync_oracle, task_buffers
-from tests.test_gpu_parity import check_pair
+from tests.test_gpu_parity import check_device_pair
 
 pytestmark = pytest.mark.gpu
 
@@ -62,8 +62,9 @@ def test_fused_env_step_with_dr_matches_oracle(gpu, name):
         torch.cuda.synchronize()
         orc.env_step(acts.numpy(), task.control_frequency_inv, b)
         tol = 1e-4 if name == "Cartpole" else 2e-3
-        check_pair(name, task, obs_dict["obs"].cpu().numpy(), rew.cpu().numpy(), b["obs"], b["rew"],
-                   tol, orc.decision_margin())
+        # 5 steps without re-sync: per-env tolerance (device and oracle rollouts drift apart)
+        check_device_pair(name, obs_dict["obs"].cpu().numpy(), rew.cpu().numpy(), b["obs"], b["rew"],
+                          tol, orc.decision_margin())
         assert np.array_equal(resets.cpu().numpy(), b["reset"]), f"step {step}"
         np.testing.assert_array_equal(_dr_state(env), orc.dr_state(), err_msg=f"step {step}")
         if name != "Cartpole":   # task.actions carries the noisy actions

@@ -2,7 +2,8 @@
 
 Tolerances (fp32): task math from identical state rtol=atol=1e-4
 (transcendentals: device ocml vs glibc differ by a few ulp); one fused env step incl.
-physics atol=2e-3 on obs (CRBA+LTDL on the device vs dense J^T I J + Cholesky in the oracle,
+physics per observation field group (GROUP_TOL: median / 99th percentile / max bounds at ~5x the
+measured device-oracle error; CRBA+LTDL on the device vs dense J^T I J + Cholesky in the oracle,
 4 PGS sweeps amplify rounding); reset / done masks and progress are compared BIT-EXACT.
 """
 import numpy as np
@@ -125,17 +126,62 @@ def _sensor_cols(task):
 # may go either way under a different float summation order (contact model discontinuity).
 DECISION_EPS = 1e-4
 
+# Device-vs-oracle bounds per observation field group after ONE fused env step from identical
+# state: (median, 99th percentile, max over envs away from a decision threshold) of the per-env
+# max |device - oracle| in the group, each ~5x what tools/parity_stats.py measured over
+# 4 steps x 4096 envs (DESIGN.md §4 lists the measured values). The force-sensor columns carry
+# the PGS contact impulses (4 sweeps, ill-conditioned stacks), hence their wider tail.
+GROUP_TOL = {
+    "Humanoid": {"root": (2e-5, 1e-4, 1e-3), "dof_pos": (1e-5, 5e-5, 4e-4),
+                 "dof_vel": (5e-5, 4e-4, 3e-3), "sensors": (5e-5, 3e-3, 3e-2),
+                 "actions": (0.0, 0.0, 0.0), "rew": (2e-6, 5e-5, 2e-2)},
+    "Ant": {"root": (5e-6, 4e-5, 1e-4), "dof_pos": (1e-6, 3e-6, 1e-5),
+            "dof_vel": (3e-6, 4e-5, 2e-4), "sensors": (1e-5, 1.5e-4, 5e-4),
+            "actions": (0.0, 0.0, 0.0), "rew": (1e-6, 2e-6, 1e-5)},
+}
+GROUP_TOL["AntSelf"] = GROUP_TOL["Humanoid"]   # Ant with self-collision pairs (runtime tables)
+
+
+def obs_groups(task):
+    D, S = task.model.num_dof, task.model.num_sensors
+    return {"root": slice(0, 12), "dof_pos": slice(12, 12 + D), "dof_vel": slice(12 + D, 12 + 2 * D),
+            "sensors": slice(12 + 2 * D, 12 + 2 * D + 6 * S), "actions": slice(12 + 2 * D + 6 * S, None)}
+
 
 def check_pair(name, task, obs, rew, obs_ref, rew_ref, tol, margin):
-    """Per-env parity. Every env must agree to `tol` on all observations and the reward,
-    except envs whose oracle `margin` (closest activation decision to its threshold during
-    the step, OracleSim.decision_margin) is below DECISION_EPS: there the discrete branch may
-    legitimately differ. Such envs must stay rare (< 2 %)."""
-    bad = ~np.all(np.isclose(obs, obs_ref, rtol=tol, atol=tol), axis=1)
-    bad |= ~np.isclose(rew, rew_ref, rtol=tol, atol=tol)
+    """Per-env parity after one fused step from identical state.
+
+    Cartpole: every env within `tol` (1e-4). Locomotion: per field group the median / 99th
+    percentile / max (over envs whose oracle `margin` — closest contact or limit activation
+    decision to its threshold during the step, OracleSim.decision_margin — is >= DECISION_EPS)
+    of the per-env max abs error stay within GROUP_TOL; envs at a threshold may take the other
+    discrete branch but must stay rare (< 2 %). `tol` is unused for locomotion (kept for the
+    call sites' signature)."""
     if name == "Cartpole":
+        bad = ~np.all(np.isclose(obs, obs_ref, rtol=tol, atol=tol), axis=1)
+        bad |= ~np.isclose(rew, rew_ref, rtol=tol, atol=tol)
         assert not bad.any(), f"{name}: envs {np.nonzero(bad)[0]}"
         return
+    near = margin < DECISION_EPS
+    err = {g: np.abs(obs[:, sl] - obs_ref[:, sl]).max(axis=1) for g, sl in obs_groups(task).items()}
+    err["rew"] = np.abs(rew - rew_ref)
+    over_near = np.zeros(len(rew), bool)
+    for g, e in err.items():
+        q50, q99, emax = GROUP_TOL[name][g]
+        far = e[~near]
+        assert np.quantile(e, 0.5) <= q50, f"{name} {g}: median error {np.quantile(e, 0.5):.3g} > {q50}"
+        assert np.quantile(e, 0.99) <= q99, f"{name} {g}: q99 error {np.quantile(e, 0.99):.3g} > {q99}"
+        assert far.size == 0 or far.max() <= emax, (
+            f"{name} {g}: env {np.nonzero(~near)[0][far.argmax()]} error {far.max():.3g} > {emax}")
+        over_near |= near & (e > emax)
+    assert over_near.mean() < 0.02, f"{name}: {over_near.sum()} envs at a threshold differ"
+
+
+def check_device_pair(name, obs_a, rew_a, obs_b, rew_b, tol, margin):
+    """Two DEVICE kernels (e.g. wave vs thread path) run several steps without re-sync: per-env
+    within `tol` except envs at a decision threshold (< 2 %)."""
+    bad = ~np.all(np.isclose(obs_a, obs_b, rtol=tol, atol=tol), axis=1)
+    bad |= ~np.isclose(rew_a, rew_b, rtol=tol, atol=tol)
     near = margin < DECISION_EPS
     unexplained = bad & ~near
     assert not unexplained.any(), (
@@ -201,8 +247,8 @@ def test_wave_path_matches_thread_path(gpu, monkeypatch):
             oa, ra, da, _ = ea.step(acts.to("cuda:0"))
             ob, rb, db, _ = eb.step(acts.to("cuda:0"))
             torch.cuda.synchronize()
-            check_pair(name, ea.task, oa["obs"].cpu().numpy(), ra.cpu().numpy(), ob["obs"].cpu().numpy(),
-                       rb.cpu().numpy(), 2e-3, orc.decision_margin())
+            check_device_pair(name, oa["obs"].cpu().numpy(), ra.cpu().numpy(), ob["obs"].cpu().numpy(),
+                              rb.cpu().numpy(), 2e-3, orc.decision_margin())
             assert torch.equal(da, db)
         ea.close()
         eb.close()
@@ -226,8 +272,8 @@ def test_compiled_topology_matches_runtime_tables(gpu, monkeypatch):
             oa, ra, da, _ = ea.step(acts.to("cuda:0"))
             ob, rb, db, _ = eb.step(acts.to("cuda:0"))
             torch.cuda.synchronize()
-            check_pair(name, ea.task, oa["obs"].cpu().numpy(), ra.cpu().numpy(), ob["obs"].cpu().numpy(),
-                       rb.cpu().numpy(), 2e-3, orc.decision_margin())
+            check_device_pair(name, oa["obs"].cpu().numpy(), ra.cpu().numpy(), ob["obs"].cpu().numpy(),
+                              rb.cpu().numpy(), 2e-3, orc.decision_margin())
             assert torch.equal(da, db)
         ea.close()
         eb.close()
@@ -258,7 +304,7 @@ def test_self_collision_on_uncompiled_model_uses_runtime_tables(gpu, monkeypatch
         o, r, d, _ = env.step(acts.to("cuda:0"))
         torch.cuda.synchronize()
         orc.env_step(acts.numpy(), env.task.control_frequency_inv, b)
-        check_pair("Ant", env.task, o["obs"].cpu().numpy(), r.cpu().numpy(), b["obs"], b["rew"],
+        check_pair("AntSelf", env.task, o["obs"].cpu().numpy(), r.cpu().numpy(), b["obs"], b["rew"],
                    2e-3, orc.decision_margin())
     env.close()
 

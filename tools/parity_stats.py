@@ -43,6 +43,13 @@ def main():
     orc_lib().orc_set_threads(min(16, os.cpu_count() or 1))
     orc = oracle_twin(env, seed=3)
     sync_oracle(env, orc)
+    D, S = task.model.num_dof, task.model.num_sensors
+    if task_name == "Cartpole":
+        groups = {"obs": slice(0, 4)}
+    else:
+        groups = {"root": slice(0, 12), "dof_pos": slice(12, 12 + D), "dof_vel": slice(12 + D, 12 + 2 * D),
+                  "sensors": slice(12 + 2 * D, 12 + 2 * D + 6 * S), "actions": slice(12 + 2 * D + 6 * S, None)}
+    gerr = {g: [] for g in list(groups) + ["rew"]}
     errs, margins = [], []
     for k in range(3, 3 + steps):
         b = task_buffers(env)
@@ -50,8 +57,12 @@ def main():
         o, r, d, _ = env.step(a)
         torch.cuda.synchronize()
         orc.env_step(a.cpu().numpy(), task.control_frequency_inv, b)
-        e = np.maximum(np.abs(o["obs"].cpu().numpy() - b["obs"]).max(axis=1),
-                       np.abs(r.cpu().numpy() - b["rew"]))
+        od = np.abs(o["obs"].cpu().numpy() - b["obs"])
+        rd = np.abs(r.cpu().numpy() - b["rew"])
+        for g, sl in groups.items():
+            gerr[g].append(od[:, sl].max(axis=1))
+        gerr["rew"].append(rd)
+        e = np.maximum(od.max(axis=1), rd)
         errs.append(e)
         margins.append(orc.decision_margin().copy())
         sync_oracle(env, orc)
@@ -63,7 +74,10 @@ def main():
     out = {"task": task_name, "envs": n, "steps": steps, **q, "max": float(e.max()),
            "max_far_from_threshold": float(e[far].max()) if far.any() else None,
            "frac_gt_2e-3_far": float((e[far] > 2e-3).mean()) if far.any() else None,
-           "worst_far": [(int(i % n), int(i // n), float(e[i]), float(m[i])) for i in worst]}
+           "worst_far": [(int(i % n), int(i // n), float(e[i]), float(m[i])) for i in worst],
+           "groups": {g: {f"q{p}": float(np.quantile(np.concatenate(v), p / 100)) for p in (50, 99)} |
+                      {"max_far": float(np.concatenate(v)[far].max()) if far.any() else None}
+                      for g, v in gerr.items()}}
     print(json.dumps(out), flush=True)
     orc.close()
     env.close()
