@@ -590,9 +590,14 @@ static int sync_kparams(mi_sim* s) {
 // would emit flat vector loads, each a full memory round trip, for every parameter read).
 using CKParams = const __attribute__((address_space(4))) KParams;
 __device__ __forceinline__ const KParams* opaque_kp(const KParams* kp) {
+#ifdef MI_KP_GENERIC
+    asm volatile("" : "+s"(kp));
+    return kp;
+#else
     CKParams* c = (CKParams*)kp;
     asm volatile("" : "+s"(c));
     return (const KParams*)c;
+#endif
 }
 
 // copy the per-model constant block into this workgroup's LDS (once per launch; shared by the
@@ -607,11 +612,22 @@ __device__ __forceinline__ int wave_env() {
     return (int)(blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6));
 }
 __device__ __forceinline__ float* wave_env_lds(const WaveTabs& t, float* smem) {
+#ifdef MI_E1
+    return smem;
+#else
     return smem + (threadIdx.x >> 6) * t.env_stride;
+#endif
 }
 
+// waves per SIMD the env-step kernel is compiled for (TopoCT::kWaves): 4 = all 16 envs of a
+// CU resident at once (128 VGPRs), 2 = 256 VGPRs
+#ifdef MI_OCC_MINONLY
+#define MI_WAVE_OCC __attribute__((amdgpu_waves_per_eu(T::kWaves)))
+#else
+#define MI_WAVE_OCC __attribute__((amdgpu_waves_per_eu(T::kWaves, T::kWaves)))
+#endif
 template <class T>
-__global__ __launch_bounds__(256) void k_sim_step_wave(const KParams* __restrict__ kp, int substeps) {
+__global__ __launch_bounds__(256) MI_WAVE_OCC void k_sim_step_wave(const KParams* __restrict__ kp, int substeps) {
     extern __shared__ __attribute__((aligned(16))) float smem[];
     const WaveTabs& t = kp->t;
     const int i = wave_env();
@@ -626,11 +642,6 @@ __global__ __launch_bounds__(256) void k_sim_step_wave(const KParams* __restrict
 }
 
 template <class T>
-#ifdef MI_WAVES4
-#define MI_WAVE_OCC __attribute__((amdgpu_waves_per_eu(4, 4)))
-#else
-#define MI_WAVE_OCC
-#endif
 __global__ __launch_bounds__(256) MI_WAVE_OCC void k_env_step_wave(const KParams* __restrict__ kp,
                                                       const float* actions, int substeps,
                                                       float* obs_out, float* obs_task, float* rew,
@@ -1065,9 +1076,39 @@ int mi_sim_create(const mi_model_desc* md, const mi_sim_params* prm, int32_t N, 
         int lr = 0;   // compact factor rows (each padded to 4) + 1/D (DofTree::lrow)
         for (int k = 0; k < m.nv; ++k) lr += (anc_start[k + 1] - anc_start[k] + 3) & ~3;
         int so = 0;
-        bool env_region_over = false;
         auto take = [&](int n) { const int at = so; so += al4(n); return at; };
         t.s_mc = take(t.mc_len);   // shared by the workgroup's envs
+#ifdef MI_OLD_LAYOUT
+        if (ct) {
+            t.s_R = take(9 * L); t.s_o = take(3 * L); t.s_S = take(6 * m.nv);
+            const int span0 = so;
+            t.s_F = take(16 * L); t.s_Ic = take(4); t.s_M = take(m.nv * m.nv); t.s_X = take(16 * L);
+            const int span1 = so;
+            t.s_D = take(4); t.s_r = take(WNV); t.s_us = take(WNV); t.s_q = take(WNV); t.s_rp = take(8);
+            const int rows_len = 8 * al4(C) + 4 * al4(R) + WNV + 64;
+            const bool overlay = rows_len <= span1 - span0;
+            int ro = overlay ? span0 : so;
+            auto take_r = [&](int n) { const int at = ro; ro += al4(n); return at; };
+            t.s_cp = take_r(3 * C); t.s_cl = take_r(C); t.s_cl2 = take_r(C); t.s_cn = take_r(3 * C);
+            t.s_rl = take_r(R); t.s_rb = take_r(R); t.s_rk = take_r(R); t.s_ad = take_r(R);
+            t.s_lsg = take_r(WNV); t.s_own = take_r(64);
+            if (!overlay) so = ro;
+            t.s_xs = take(4);
+            t.s_L = take(lr + m.nv);
+#ifndef MI_DENSE_M
+            t.s_M = t.s_L;
+#endif
+            t.j_rows_lds = std::min(48, m.max_rows);
+            t.s_J = take(t.j_rows_lds * m.nv);
+            t.s_W = take(64 * m.nv);
+            t.w_rows_lds = t.w_rows_a = std::min(64, m.max_rows);
+            if (overlay && self_on && al4(12 * md->num_geoms) + al4(md->num_pairs) <= span1 - ro) {
+                t.s_seg = ro;
+                t.s_surv = ro + al4(12 * md->num_geoms);
+            }
+            t.envs_per_wg = 1;
+        } else
+#endif
         if (ct) {
             // Compiled-topology layout, sized so 16 envs are resident per CU (4 waves / SIMD,
             // all 4096 envs of a launch in one round): the persistent per-env state, then ONE
@@ -1075,13 +1116,19 @@ int mi_sim_create(const mi_model_desc* md, const mi_sim_params* prm, int32_t N, 
             // row data, the row -> lane owner table, then the W rows (or the P8 self-collision
             // scratch). M~ goes straight into the factor's compact rows (s_L); J rows are never
             // stored (the Delassus rows are built in registers in P9).
-            t.envs_per_wg = 4;
-            if (const char* e = getenv("MI_WAVE_ENVS")) t.envs_per_wg = std::max(1, std::min(4, atoi(e)));
             t.s_R = take(9 * L); t.s_o = take(3 * L); t.s_S = take(6 * m.nv);
             t.s_D = take(4); t.s_r = take(WNV); t.s_us = take(WNV); t.s_q = take(WNV); t.s_rp = take(8);
             t.s_xs = take(4);
             t.s_L = take(lr + m.nv);
             t.s_M = t.s_L;
+#ifdef MI_DENSE_M
+            t.s_M = take(m.nv * m.nv);
+#endif
+            int waves = 4;
+            with_topo(s->topo, [&](auto T) { waves = decltype(T)::kWaves; });
+            // 256-VGPR kernels: J rows of the Delassus set-up in LDS (room for 8 envs / CU)
+            t.j_rows_lds = waves <= 2 ? std::min(48, m.max_rows) : 0;
+            t.s_J = take(t.j_rows_lds > 0 ? t.j_rows_lds * m.nv : 4);
             const int work = so;
             int wo = work;
             auto take_w = [&](int n) { const int at = wo; wo += al4(n); return at; };
@@ -1100,19 +1147,32 @@ int mi_sim_create(const mi_model_desc* md, const mi_sim_params* prm, int32_t N, 
                 t.s_surv = rows_end + al4(12 * md->num_geoms);
                 seg_end = t.s_surv + al4(md->num_pairs);
             }
-            // LDS per env: 16 envs / CU = 16 / E workgroups, each with its constant block
-            const int E = t.envs_per_wg;
-            const int wg_floats = (163840 / (int)sizeof(float)) / (16 / E);
-            const int env_floats = (wg_floats - al4(t.mc_len)) / E;
-            int wrows = std::min(64, m.max_rows);
-            if (const char* e = getenv("MI_WAVE_WROWS")) wrows = std::min(wrows, std::max(0, atoi(e)));
-            // whole W region (al4-padded) inside the env's share of the budget
-            wrows = std::max(0, std::min(wrows, (t.s_R + env_floats - rows_end) / m.nv));
-            while (wrows > 0 && rows_end + al4(wrows * m.nv) > t.s_R + env_floats) --wrows;
+            // LDS per env: the resident envs per CU the kernel's register budget allows (4 waves
+            // per SIMD x 4 SIMDs = 16, or 8), i.e. that many / E workgroups, each with its
+            // constant block. E (envs per workgroup, sharing that block) is the smallest of
+            // 1 / 2 / 4 whose share holds 32 W rows: a workgroup's LDS is freed only when its
+            // last env finishes, so larger workgroups cost residency whenever envs run in more
+            // than one round.
+            const int envs_cu = 4 * std::max(1, waves);
+            int want = std::min(64, m.max_rows);
+            if (const char* e = getenv("MI_WAVE_WROWS")) want = std::min(want, std::max(0, atoi(e)));
+            auto fit_rows = [&](int E) {   // W rows that fit each env's share with E envs / WG
+                const int wg_floats = (163840 / (int)sizeof(float)) / std::max(1, envs_cu / E);
+                const int env_floats = (wg_floats - al4(t.mc_len)) / E;
+                int w = std::max(0, std::min(want, (t.s_R + env_floats - rows_end) / m.nv));
+                while (w > 0 && rows_end + al4(w * m.nv) > t.s_R + env_floats) --w;
+                const bool fits = std::max(span_end, seg_end) - t.s_R <= env_floats;
+                return fits ? w : -1;
+            };
+            int E = 4;
+            for (int e : {1, 2, 4})
+                if (e <= envs_cu && fit_rows(e) >= std::min(32, want)) { E = e; break; }
+            if (const char* e = getenv("MI_WAVE_ENVS")) E = std::max(1, std::min(4, atoi(e)));
+            t.envs_per_wg = E;
+            int wrows = std::max(0, fit_rows(E));
             t.s_W = rows_end;
             t.w_rows_lds = t.w_rows_a = wrows;
             so = std::max(span_end, std::max(seg_end, rows_end + al4(wrows * m.nv)));
-            env_region_over = so - t.s_R > env_floats;   // fewer than 16 envs / CU fit
         } else {
             // runtime tables (models without a generated topology): one env per workgroup,
             // dense M, lane-private solve vectors, every W row through the global slab
@@ -1125,6 +1185,7 @@ int mi_sim_create(const mi_model_desc* md, const mi_sim_params* prm, int32_t N, 
             t.s_rl = take(R); t.s_rb = take(R); t.s_rk = take(R); t.s_ad = take(R);
             t.s_lsg = take(WNV); t.s_own = take(64);
             t.s_xs = take(WNV * 64);
+            t.j_rows_lds = 0; t.s_J = take(4);
             t.s_L = take(4);
             t.s_W = so;
             t.w_rows_lds = t.w_rows_a = 0;

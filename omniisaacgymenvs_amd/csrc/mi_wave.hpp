@@ -29,6 +29,9 @@
 namespace mi {
 
 constexpr int WNV = 32;  // padded DOF count of the wave path
+#ifndef MI_ROLLED_USPACE
+#define MI_ROLLED_USPACE 0
+#endif
 
 // Global-memory view of a generic pointer into device memory (state records, the W-row slab):
 // accesses compile to global_load / global_store instead of flat ones.
@@ -40,13 +43,15 @@ __device__ __forceinline__ const gfloat* as_global(const float* p) { return (con
 // model constants and otherwise never interact. Lane id inside the env's wave:
 __device__ __forceinline__ int wave_lane() { return (int)(threadIdx.x & 63u); }
 // Sync point between two phases of ONE env (its wave): every lane's earlier LDS and global
-// accesses are complete and visible to the wave's later accesses. No s_barrier (the other waves
-// of the workgroup are other envs); the workgroup-scope fences order the vector memory ops too
-// (pre-step effort writes read back by other lanes, the global W-row slab).
+// accesses are visible to the wave's later accesses. No s_barrier (the other waves of the
+// workgroup are other envs), and wavefront scope: a wave's memory operations are performed in
+// order (LDS and the vector memory path), so the fences only stop the compiler from moving
+// accesses across the sync and emit no waits. (Workgroup-scope fences would wait for every
+// outstanding vector memory access, loads included, at each phase boundary.)
 __device__ __forceinline__ void wave_sync() {
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
     __builtin_amdgcn_wave_barrier();
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
 }
 
 // Diagnostic phase timers (built only with -DMI_STAMPS into a separate library; the product
@@ -124,6 +129,9 @@ struct WaveTabs {
     int envs_per_wg, s_env, env_stride;
     // row slot -> lane that holds the row's J in P9 (Delassus-space PGS set-up)
     int s_own;
+    // J rows [0, j_rows_lds) kept in LDS at s_J (stride nv) for the Delassus set-up (256-VGPR
+    // kernels, where LDS has room; 0 on the 128-VGPR kernels, which keep J in registers)
+    int s_J, j_rows_lds;
     // per-model constant block (see McLayout): global copy, staged into LDS at s_mc once per
     // launch by every workgroup
     const float* g_mc;
@@ -658,6 +666,21 @@ MI_D void wave_artic_substep(const DevModel& m, const WaveTabs& t, const DevStat
             r += st.eff[sx(st, k - nr, i)] - damp * us[k];
         }
         rhs[k] = r;
+#ifdef MI_DENSE_M
+        if constexpr (TP::kCT) {
+            Mx[k * nv + k] = diag;
+            const unsigned am = k < nr ? (1u << k) - 1u : mc.mask(l) & ~(1u << k);
+            sfor<0, TP::nv>([&](auto J) {
+                constexpr int j = J;
+                if ((am >> j) & 1u) {
+                    float sj[6];
+#pragma unroll
+                    for (int c = 0; c < 6; ++c) sj[c] = Ss[6 * j + c];
+                    Mx[k * nv + j] = dot6(sj, f);
+                }
+            });
+        } else
+#endif
         if constexpr (TP::kCT) {
             // M~ straight into the factor's compact LDS rows (DofTree::lrow; ct_publish_factor):
             // row k's entry for ancestor j at lrow[k] + depth(k) - 1 - depth(j), the diagonal at
@@ -700,7 +723,18 @@ MI_D void wave_artic_substep(const DevModel& m, const WaveTabs& t, const DevStat
     float dvec = 1.0f;    // CT path: lane c holds 1 / D_c
     if constexpr (TP::kCT) {
         const int dj = lane < nr ? lane : __builtin_popcount(mc.mask(lane < nv ? lane - nr + 1 : 0)) - 1;
+#ifdef MI_DENSE_M
+        {
+            const int c = lane < TP::nv ? lane : 0;
+            sfor<0, TP::nv>([&](auto R) {
+                constexpr int r = R;
+                constexpr unsigned long long keep = (unsigned long long)TP::dof.anc_mask[r] | (1ull << r);
+                Mc[r] = ((keep >> lane_here(lane)) & 1ull) ? Mx[r * TP::nv + c] : 0.0f;
+            });
+        }
+#else
         ct_load_columns<TP>(sm + t.s_L, lane, dj, Mc);
+#endif
         ct_ltdl<TP>(lane, Mc);
         dvec = ct_dinv<TP>(lane, Mc);
         ct_publish_factor<TP>(lane, dj, Mc, dvec, sm + t.s_L);
@@ -999,6 +1033,12 @@ MI_D void wave_artic_substep(const DevModel& m, const WaveTabs& t, const DevStat
         }
         if (slot >= 0) {
             sm[t.s_ad + slot] = a > 1e-12f ? a : 1e-12f;
+            if (kd >= 0 && slot < t.j_rows_lds) {    // limit row: J = sg e_kd
+                float* jl = sm + t.s_J + slot * nv;
+#pragma unroll
+                for (int c = 0; c < WNV; ++c)
+                    if (c < nv) jl[c] = c == kd ? sc : 0.0f;
+            }
             if (nrows <= t.w_rows_lds) {   // uniform: every row of this substep fits in LDS
                 float* wl = w_row<TP::kSelf>(t, sm, slot, nv);
 #pragma unroll
@@ -1051,7 +1091,14 @@ MI_D void wave_artic_substep(const DevModel& m, const WaveTabs& t, const DevStat
                     x[c] = bv == 0 ? rhs[c] : (kd == c ? 1.0f : 0.0f);
                 });
             }
-            sfor<0, TP::nv>([&](auto C) { xj[C] = x[C]; });
+            if constexpr (TP::kWaves <= 2) {
+                if (on && r >= 0 && r < t.j_rows_lds) {   // keep J_r for the Delassus set-up
+                    float* jl = sm + t.s_J + r * TP::nv;
+                    sfor<0, TP::nv>([&](auto C) { jl[C] = x[C]; });
+                }
+            } else {
+                sfor<0, TP::nv>([&](auto C) { xj[C] = x[C]; });
+            }
             STAMP(7);   // P9 J build
             float a;                              // J M~^-1 J^T from the half solve
             ct_solve_l<TP>(sm + t.s_L, x, a);     // factor rows from LDS broadcasts
@@ -1112,7 +1159,29 @@ MI_D void wave_artic_substep(const DevModel& m, const WaveTabs& t, const DevStat
     float Ar[RL];
     float vlam = 0.0f;
     bool lam_path = false;
-    if constexpr (TP::kCT) {
+    if constexpr (TP::kCT && TP::kWaves <= 2) {
+        // J and W rows in LDS (uniform; the 256-VGPR kernels' layouts hold 64 of each)
+        if (nrows <= TP::kLamRows && nrows <= t.j_rows_lds && nrows <= t.w_rows_lds) {
+            wave_sync();                             // W / J rows and u* complete
+            const int rl = lane < nrows ? lane : 0;
+            float J[TP::nvc];
+            sfor<0, TP::nv>([&](auto C) { J[C] = sm[t.s_J + rl * TP::nv + C]; });
+            float v = 0.0f;
+            sfor<0, TP::nv>([&](auto C) { v += J[C] * us[C]; });
+            // entries past nrows are never read (the sweeps stop there): an early-exit chain,
+            // so the compiler keeps the Delassus row in registers
+#pragma unroll
+            for (int s2 = 0; s2 < RL; ++s2) {
+                if (s2 >= nrows) break;
+                const float* w = w_row<TP::kSelf>(t, sm, s2, TP::nv);
+                float acc = 0.0f;
+                sfor<0, TP::nv>([&](auto C) { acc += J[C] * w[C]; });
+                Ar[s2] = acc;
+            }
+            vlam = v;
+            lam_path = true;
+        }
+    } else if constexpr (TP::kCT) {
         if (total <= 64 && nrows <= TP::kLamRows) {
             int* own = reinterpret_cast<int*>(sm + t.s_own);
             if (my_slot >= 0) own[my_slot] = lane;   // row slot -> the lane holding its J
@@ -1124,9 +1193,6 @@ MI_D void wave_artic_substep(const DevModel& m, const WaveTabs& t, const DevStat
             const bool wl = nrows <= t.w_rows_lds;
 #pragma unroll
             for (int s2 = 0; s2 < RL; ++s2) {
-                // one W row in flight at a time: without the fence the unrolled loop hoists all
-                // RL x nv loads and the register file spills
-                asm volatile("" ::: "memory");
                 float acc = 0.0f;
                 if (s2 < nrows) {
                     if (wl) {           // (separate branches: a select of an LDS and a global
@@ -1214,7 +1280,6 @@ MI_D void wave_artic_substep(const DevModel& m, const WaveTabs& t, const DevStat
 #pragma unroll
             for (int rr = 0; rr < RL; ++rr) {
                 if (rr >= nrows) break;
-                asm volatile("" ::: "memory");
                 float w;
                 if (wl) w = w_row<TP::kSelf>(t, sm, rr, NV)[kc];
                 else w = as_global(gW)[(size_t)rr * WNV + kc];
@@ -1277,11 +1342,85 @@ MI_D void wave_artic_substep(const DevModel& m, const WaveTabs& t, const DevStat
         }
         const float mu = p.friction;
         float u = kl < nv ? us[kl] : 0.0f;
-        // Rows in order, one at a time (rolled loop over a uniform row counter: this path only
-        // takes the rare row-heavy substeps, so it is built for a small register footprint).
-        // Per row: J_r . u by a DPP half-wave sum, the projected lambda update, u += W_r dlambda.
-        // The friction rows of a contact follow its normal row in the same sweep, so the
-        // normal's current lambda is carried in a wave-uniform value.
+        if constexpr (TP::kWaves <= 2 && TP::kLamRows < 64 && !MI_ROLLED_USPACE) {
+        // 256-VGPR kernels: this lane's W_r[kl] of all 64 rows of its bank in registers, rows
+        // fully unrolled (readlanes at constant lanes); the next row's J is built inside the
+        // current row's schedule region so it overlaps the reduction chain.
+        float Wr[64];
+#pragma unroll
+        for (int rr = 0; rr < 64; ++rr) Wr[rr] = rr < nrows ? wload(min(rr, 63)) : 0.0f;
+        auto sweeps = [&](auto ONE_) {
+            constexpr bool ONE = decltype(ONE_)::value;
+            for (int it = 0; it < p.iters; ++it) {
+                // opaque per sweep: stops the compiler hoisting the loop-invariant readlanes of
+                // every row out of the iteration loop (they would pin hundreds of SGPRs)
+                asm volatile("" : "+v"(b0), "+v"(b1), "+v"(ia0), "+v"(ia1), "+v"(k0), "+v"(k1),
+                             "+v"(ma), "+v"(mb), "+v"(ma2), "+v"(mb2));
+                asm volatile("" : "+v"(fa[0]), "+v"(fa[1]), "+v"(fa[2]), "+v"(fa[3]), "+v"(fa[4]),
+                             "+v"(fa[5]), "+v"(fb[0]), "+v"(fb[1]), "+v"(fb[2]), "+v"(fb[3]),
+                             "+v"(fb[4]), "+v"(fb[5]));
+                int nrow_it = nrows;   // opaque: 128 hoisted "r < nrows" masks would spill
+                asm volatile("" : "+s"(nrow_it));
+                float lamn = 0.0f;
+#pragma unroll
+                for (int h = 0; h < (ONE ? 1 : 2); ++h) {
+                    if (64 * h >= nrow_it) continue;
+                    const float bb = h ? b1 : b0, ii = h ? ia1 : ia0, kk = h ? k1 : k0;
+                    const unsigned mm = h ? mb : ma, mm2 = h ? mb2 : ma2;
+                    auto jrow = [&](int rr, int& kind) -> float {
+                        float fr[6];
+#pragma unroll
+                        for (int q = 0; q < 6; ++q) fr[q] = readlane(h ? fb[q] : fa[q], rr);
+                        const unsigned msk = (unsigned)__builtin_amdgcn_readlane((int)mm, rr);
+                        const unsigned msk2 = (unsigned)__builtin_amdgcn_readlane((int)mm2, rr);
+                        kind = (int)readlane(kk, rr);
+                        const float jc = kind == 3 ? fr[0] : dot6(S6, fr);
+                        return (((msk >> kl) & 1u) ? jc : 0.0f) - (((msk2 >> kl) & 1u) ? jc : 0.0f);
+                    };
+                    int kind_c;
+                    float jc_c = jrow(0, kind_c);
+#pragma unroll
+                    for (int rr = 0; rr < 64; ++rr) {
+                        const int r = rr + 64 * h;
+                        if (r >= nrow_it) continue;
+                        __builtin_amdgcn_sched_barrier(0);
+                        int kind_n = 0;
+                        float jc_n = 0.0f;
+                        if (rr + 1 < 64) jc_n = jrow(rr + 1, kind_n);
+                        const float s = half_sums(jc_c * u);
+                        const float jv = readlane(s, h ? 63 : 31);
+                        const float br = readlane(bb, rr), iar = readlane(ii, rr);
+                        const float l0 = readlane(h ? lam1 : lam0, rr);
+                        float ln = l0 + (br - jv) * iar;
+                        const bool fric = kind_c == 1 || kind_c == 2;
+                        const float lim = mu * lamn;
+                        ln = fmaxf(ln, fric ? -lim : 0.0f);     // normal / limit: lambda >= 0
+                        ln = fric ? fminf(ln, lim) : ln;         // friction: |lambda| <= mu lambda_n
+                        lamn = kind_c == 0 ? ln : lamn;
+                        const float dl = ln - l0;
+                        const int ln_id = lane_here(lane);
+                        if constexpr (ONE) {
+                            u += Wr[rr] * dl;
+                        } else {
+                            if ((ln_id >> 5) == h) u += Wr[rr] * dl;
+                        }
+                        if (ln_id == rr) { if (h) lam1 = ln; else lam0 = ln; }
+                        jc_c = jc_n;
+                        kind_c = kind_n;
+                    }
+                    // hand u to the other half for its sub-sweep
+                    if constexpr (!ONE) u = __shfl(u, kl + 32 * h, 64);
+                }
+            }
+        };
+        if (one_bank) sweeps(std::true_type{});
+        else sweeps(std::false_type{});
+        } else {
+        // 128-VGPR kernels: rows in order, one at a time (rolled loop over a uniform row counter;
+        // this path only takes the rare row-heavy substeps, so it is built for a small register
+        // footprint). Per row: J_r . u by a DPP half-wave sum, the projected lambda update,
+        // u += W_r dlambda. The friction rows of a contact follow its normal row in the same
+        // sweep, so the normal's current lambda is carried in a wave-uniform value.
         const int nbank = one_bank ? 1 : 2;
         for (int it = 0; it < p.iters; ++it) {
             float lamn = 0.0f;
@@ -1314,6 +1453,7 @@ MI_D void wave_artic_substep(const DevModel& m, const WaveTabs& t, const DevStat
                 // hand u to the other half for its sub-sweep
                 if (!one_bank) u = __shfl(u, kl + 32 * h, 64);
             }
+        }
         }
         if (lane < nv) us[lane] = u;
         if (lane < nrows) sm[t.s_ad + lane] = lam0;          // reuse: lambda of row lane
