@@ -590,14 +590,9 @@ static int sync_kparams(mi_sim* s) {
 // would emit flat vector loads, each a full memory round trip, for every parameter read).
 using CKParams = const __attribute__((address_space(4))) KParams;
 __device__ __forceinline__ const KParams* opaque_kp(const KParams* kp) {
-#ifdef MI_KP_GENERIC
-    asm volatile("" : "+s"(kp));
-    return kp;
-#else
     CKParams* c = (CKParams*)kp;
     asm volatile("" : "+s"(c));
     return (const KParams*)c;
-#endif
 }
 
 // copy the per-model constant block into this workgroup's LDS (once per launch; shared by the
@@ -612,22 +607,11 @@ __device__ __forceinline__ int wave_env() {
     return (int)(blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6));
 }
 __device__ __forceinline__ float* wave_env_lds(const WaveTabs& t, float* smem) {
-#ifdef MI_E1
-    return smem;
-#else
     return smem + (threadIdx.x >> 6) * t.env_stride;
-#endif
 }
 
-// waves per SIMD the env-step kernel is compiled for (TopoCT::kWaves): 4 = all 16 envs of a
-// CU resident at once (128 VGPRs), 2 = 256 VGPRs
-#ifdef MI_OCC_MINONLY
-#define MI_WAVE_OCC __attribute__((amdgpu_waves_per_eu(T::kWaves)))
-#else
-#define MI_WAVE_OCC __attribute__((amdgpu_waves_per_eu(T::kWaves, T::kWaves)))
-#endif
 template <class T>
-__global__ __launch_bounds__(256) MI_WAVE_OCC void k_sim_step_wave(const KParams* __restrict__ kp, int substeps) {
+__global__ __launch_bounds__(256) void k_sim_step_wave(const KParams* __restrict__ kp, int substeps) {
     extern __shared__ __attribute__((aligned(16))) float smem[];
     const WaveTabs& t = kp->t;
     const int i = wave_env();
@@ -642,7 +626,7 @@ __global__ __launch_bounds__(256) MI_WAVE_OCC void k_sim_step_wave(const KParams
 }
 
 template <class T>
-__global__ __launch_bounds__(256) MI_WAVE_OCC void k_env_step_wave(const KParams* __restrict__ kp,
+__global__ __launch_bounds__(256) void k_env_step_wave(const KParams* __restrict__ kp,
                                                       const float* actions, int substeps,
                                                       float* obs_out, float* obs_task, float* rew,
                                                       int64_t* reset_buf, int64_t* progress_buf,
@@ -1063,142 +1047,98 @@ int mi_sim_create(const mi_model_desc* md, const mi_sim_params* prm, int32_t N, 
 #undef UPW
         auto al4 = [](int x) { return (x + 3) & ~3; };
         const bool ct = s->topo != 0;
+        int so = 0;
+        auto take = [&](int n) { const int at = so; so += al4(n); return at; };
+        t.s_mc = take(t.mc_len);
+        t.s_R = take(9 * L); t.s_o = take(3 * L); t.s_S = take(6 * m.nv);
+        // P1..P4 working span: link inertias / forces, M, aux (local transforms, composites).
+        // On the compiled-topology path it is dead once P4 has moved M into registers, and
+        // P8/P9 reuse it for the contact and row data and the first W rows.
+        const int span0 = so;
+        t.s_F = take(16 * L);   // per-link records: inertia (10) + Newton-Euler force (6)
+        t.s_Ic = take(4);       // (kept for the layout order; records live at s_F)
+        t.s_M = take(m.nv * m.nv);
+        t.s_X = take(16 * L);
+        const int span1 = so;
+        t.s_D = take(ct ? 4 : WNV); t.s_r = take(WNV); t.s_us = take(WNV);
+        t.s_q = take(WNV); t.s_rp = take(8);
         const int R = m.max_rows;
         // contacts: ground points + self pairs, at most MI_MAX_ROWS / 3 in total
         t.self_on = self_on ? 1 : 0;
         t.npairs = self_on ? md->num_pairs : 0;
         t.ncmax = std::min(m.npts + t.npairs, MI_MAX_ROWS / 3);
         const int C = t.ncmax;
-        t.max_rows = m.max_rows;
-        t.g_row_stride = (size_t)m.max_rows * WNV;
-        t.ngeoms = md->num_geoms;
-        t.s_seg = -1; t.s_surv = -1; t.s_W2 = 0;
-        int lr = 0;   // compact factor rows (each padded to 4) + 1/D (DofTree::lrow)
-        for (int k = 0; k < m.nv; ++k) lr += (anc_start[k + 1] - anc_start[k] + 3) & ~3;
-        int so = 0;
-        auto take = [&](int n) { const int at = so; so += al4(n); return at; };
-        t.s_mc = take(t.mc_len);   // shared by the workgroup's envs
-#ifdef MI_OLD_LAYOUT
-        if (ct) {
-            t.s_R = take(9 * L); t.s_o = take(3 * L); t.s_S = take(6 * m.nv);
-            const int span0 = so;
-            t.s_F = take(16 * L); t.s_Ic = take(4); t.s_M = take(m.nv * m.nv); t.s_X = take(16 * L);
-            const int span1 = so;
-            t.s_D = take(4); t.s_r = take(WNV); t.s_us = take(WNV); t.s_q = take(WNV); t.s_rp = take(8);
-            const int rows_len = 8 * al4(C) + 4 * al4(R) + WNV + 64;
-            const bool overlay = rows_len <= span1 - span0;
-            int ro = overlay ? span0 : so;
-            auto take_r = [&](int n) { const int at = ro; ro += al4(n); return at; };
-            t.s_cp = take_r(3 * C); t.s_cl = take_r(C); t.s_cl2 = take_r(C); t.s_cn = take_r(3 * C);
-            t.s_rl = take_r(R); t.s_rb = take_r(R); t.s_rk = take_r(R); t.s_ad = take_r(R);
-            t.s_lsg = take_r(WNV); t.s_own = take_r(64);
-            if (!overlay) so = ro;
-            t.s_xs = take(4);
-            t.s_L = take(lr + m.nv);
-#ifndef MI_DENSE_M
-            t.s_M = t.s_L;
-#endif
-            t.j_rows_lds = std::min(48, m.max_rows);
-            t.s_J = take(t.j_rows_lds * m.nv);
-            t.s_W = take(64 * m.nv);
-            t.w_rows_lds = t.w_rows_a = std::min(64, m.max_rows);
-            if (overlay && self_on && al4(12 * md->num_geoms) + al4(md->num_pairs) <= span1 - ro) {
-                t.s_seg = ro;
-                t.s_surv = ro + al4(12 * md->num_geoms);
+        const int rows_len = 8 * al4(C) + 4 * al4(R) + WNV;
+        const bool overlay = ct && rows_len <= span1 - span0;
+        int ro = overlay ? span0 : so;
+        auto take_r = [&](int n) { const int at = ro; ro += al4(n); return at; };
+        t.s_cp = take_r(3 * C); t.s_cl = take_r(C); t.s_cl2 = take_r(C); t.s_cn = take_r(3 * C);
+        t.s_rl = take_r(R);
+        t.s_rb = take_r(R); t.s_rk = take_r(R); t.s_ad = take_r(R); t.s_lsg = take_r(WNV);
+        if (!overlay) so = ro;
+        // lane-private solve vectors of the runtime-table solves (CT solves run in registers)
+        t.s_xs = take(ct ? 4 : WNV * 64);
+        {   // CT path: published factor rows (each padded to 4) + 1/D (DofTree::lrow)
+            int lr = 0;
+            for (int k = 0; k < m.nv; ++k) lr += (anc_start[k + 1] - anc_start[k] + 3) & ~3;
+            t.s_L = take(ct ? lr + m.nv : 4);
+        }
+        // CT path: J rows of up to 64 constraint rows for the PGS (LDS is not the occupancy
+        // limit here: registers cap the wave path at 2 waves/SIMD = 8 envs/CU = 20 KB each)
+        t.j_rows_lds = ct ? std::min(48, m.max_rows) : 0;
+        t.s_J = take(ct ? t.j_rows_lds * m.nv : 4);
+        // CT path: W rows for the P9 -> P10 hand-over. First choice: the rest of the dead
+        // span; when that holds fewer rows than a one-bank PGS can use and the LDS budget of
+        // the wave path (8 envs / CU, 20 KB each) has room, a dedicated region instead, so
+        // the global slab is only the fallback of rare row-heavy substeps.
+        // Otherwise, a second segment at the end takes whatever rows the budget still holds
+        // (rows [w_rows_a, w_rows_lds) at s_W2).
+        t.s_W = ro;
+        t.w_rows_lds = overlay ? std::min(64, (span1 - ro) / m.nv) : 0;
+        t.w_rows_a = t.w_rows_lds;
+        t.s_W2 = 0;
+        {
+            const int want = std::min(64, m.max_rows);
+            const int lds_budget_floats = (160 * 1024 / 8) / (int)sizeof(float);
+            if (ct && t.w_rows_lds < want && so + al4(want * m.nv) <= lds_budget_floats) {
+                t.s_W = take(want * m.nv);
+                t.w_rows_lds = t.w_rows_a = want;
+            } else if (ct && self_on && t.w_rows_lds < want) {   // (w_row<kSelf> on device)
+                const int extra = std::min(want - t.w_rows_lds, (lds_budget_floats - so - 3) / m.nv);
+                if (extra > 0) {
+                    t.s_W2 = take(extra * m.nv);
+                    t.w_rows_lds += extra;
+                }
             }
-            t.envs_per_wg = 1;
-        } else
-#endif
-        if (ct) {
-            // Compiled-topology layout, sized so 16 envs are resident per CU (4 waves / SIMD,
-            // all 4096 envs of a launch in one round): the persistent per-env state, then ONE
-            // work region reused phase by phase — P1..P3 link records / aux; P8..P10 contact and
-            // row data, the row -> lane owner table, then the W rows (or the P8 self-collision
-            // scratch). M~ goes straight into the factor's compact rows (s_L); J rows are never
-            // stored (the Delassus rows are built in registers in P9).
-            t.s_R = take(9 * L); t.s_o = take(3 * L); t.s_S = take(6 * m.nv);
-            t.s_D = take(4); t.s_r = take(WNV); t.s_us = take(WNV); t.s_q = take(WNV); t.s_rp = take(8);
-            t.s_xs = take(4);
-            t.s_L = take(lr + m.nv);
-            t.s_M = t.s_L;
-#ifdef MI_DENSE_M
-            t.s_M = take(m.nv * m.nv);
-#endif
-            int waves = 4;
-            with_topo(s->topo, [&](auto T) { waves = decltype(T)::kWaves; });
-            // 256-VGPR kernels: J rows of the Delassus set-up in LDS (room for 8 envs / CU)
-            t.j_rows_lds = waves <= 2 ? std::min(48, m.max_rows) : 0;
-            t.s_J = take(t.j_rows_lds > 0 ? t.j_rows_lds * m.nv : 4);
-            const int work = so;
-            int wo = work;
-            auto take_w = [&](int n) { const int at = wo; wo += al4(n); return at; };
-            t.s_F = take_w(16 * L);   // per-link records: inertia (10) + Newton-Euler force (6)
-            t.s_Ic = take_w(4);
-            t.s_X = take_w(16 * L);
-            const int span_end = wo;
-            wo = work;
-            t.s_cp = take_w(3 * C); t.s_cl = take_w(C); t.s_cl2 = take_w(C); t.s_cn = take_w(3 * C);
-            t.s_rl = take_w(R); t.s_rb = take_w(R); t.s_rk = take_w(R); t.s_ad = take_w(R);
-            t.s_lsg = take_w(WNV); t.s_own = take_w(64);
-            const int rows_end = wo;
-            int seg_end = rows_end;
-            if (self_on) {
-                t.s_seg = rows_end;
-                t.s_surv = rows_end + al4(12 * md->num_geoms);
-                seg_end = t.s_surv + al4(md->num_pairs);
-            }
-            // LDS per env: the resident envs per CU the kernel's register budget allows (4 waves
-            // per SIMD x 4 SIMDs = 16, or 8), i.e. that many / E workgroups, each with its
-            // constant block. E (envs per workgroup, sharing that block) is the smallest of
-            // 1 / 2 / 4 whose share holds 32 W rows: a workgroup's LDS is freed only when its
-            // last env finishes, so larger workgroups cost residency whenever envs run in more
-            // than one round.
-            const int envs_cu = 4 * std::max(1, waves);
-            int want = std::min(64, m.max_rows);
-            if (const char* e = getenv("MI_WAVE_WROWS")) want = std::min(want, std::max(0, atoi(e)));
-            auto fit_rows = [&](int E) {   // W rows that fit each env's share with E envs / WG
-                const int wg_floats = (163840 / (int)sizeof(float)) / std::max(1, envs_cu / E);
-                const int env_floats = (wg_floats - al4(t.mc_len)) / E;
-                int w = std::max(0, std::min(want, (t.s_R + env_floats - rows_end) / m.nv));
-                while (w > 0 && rows_end + al4(w * m.nv) > t.s_R + env_floats) --w;
-                const bool fits = std::max(span_end, seg_end) - t.s_R <= env_floats;
-                return fits ? w : -1;
-            };
-            int E = 4;
-            for (int e : {1, 2, 4})
-                if (e <= envs_cu && fit_rows(e) >= std::min(32, want)) { E = e; break; }
-            if (const char* e = getenv("MI_WAVE_ENVS")) E = std::max(1, std::min(4, atoi(e)));
-            t.envs_per_wg = E;
-            int wrows = std::max(0, fit_rows(E));
-            t.s_W = rows_end;
-            t.w_rows_lds = t.w_rows_a = wrows;
-            so = std::max(span_end, std::max(seg_end, rows_end + al4(wrows * m.nv)));
-        } else {
-            // runtime tables (models without a generated topology): one env per workgroup,
-            // dense M, lane-private solve vectors, every W row through the global slab
-            t.envs_per_wg = 1;
-            if (const char* e = getenv("MI_WAVE_ENVS")) t.envs_per_wg = std::max(1, std::min(4, atoi(e)));
-            t.s_R = take(9 * L); t.s_o = take(3 * L); t.s_S = take(6 * m.nv);
-            t.s_F = take(16 * L); t.s_Ic = take(4); t.s_M = take(m.nv * m.nv); t.s_X = take(16 * L);
-            t.s_D = take(WNV); t.s_r = take(WNV); t.s_us = take(WNV); t.s_q = take(WNV); t.s_rp = take(8);
-            t.s_cp = take(3 * C); t.s_cl = take(C); t.s_cl2 = take(C); t.s_cn = take(3 * C);
-            t.s_rl = take(R); t.s_rb = take(R); t.s_rk = take(R); t.s_ad = take(R);
-            t.s_lsg = take(WNV); t.s_own = take(64);
-            t.s_xs = take(WNV * 64);
-            t.j_rows_lds = 0; t.s_J = take(4);
-            t.s_L = take(4);
-            t.s_W = so;
-            t.w_rows_lds = t.w_rows_a = 0;
         }
         t.s_total = so;
         // E envs per workgroup share the constant block [0, s_env); env w's region is shifted
         // by w * env_stride
         t.s_env = t.s_R;
         t.env_stride = so - t.s_env;
+        t.envs_per_wg = 1;
+        if (const char* e = getenv("MI_WAVE_ENVS")) t.envs_per_wg = std::max(1, std::min(4, atoi(e)));
+        {   // the sequential regions strictly increase; the row data sits inside the dead
+            // span (overlay) or between s_rp and s_xs
+            const int offs[] = {t.s_mc, t.s_R, t.s_o, t.s_S, t.s_F, t.s_Ic, t.s_M, t.s_X,
+                                t.s_D, t.s_r, t.s_us, t.s_q, t.s_rp, t.s_xs, t.s_L, t.s_J,
+                                t.s_total};
+            for (size_t c = 1; c < sizeof(offs) / sizeof(offs[0]); ++c)
+                if (offs[c] <= offs[c - 1]) return cleanup(fail(MI_E_STATE, "wave LDS layout: region %zu overlaps", c));
+            const bool rows_ok = overlay ? (t.s_cp == span0 && ro <= span1)
+                                         : (t.s_cp > t.s_rp && ro <= t.s_xs);
+            if (!rows_ok) return cleanup(fail(MI_E_STATE, "wave LDS layout: row data misplaced"));
+        }
+        t.max_rows = m.max_rows;
+        t.g_row_stride = (size_t)m.max_rows * WNV;
+        // P8 self-collision scratch (segments + broad-phase survivors) in the same free span
+        t.ngeoms = md->num_geoms;
+        t.s_seg = -1; t.s_surv = -1;
+        if (overlay && self_on && al4(12 * md->num_geoms) + al4(md->num_pairs) <= span1 - ro) {
+            t.s_seg = ro;
+            t.s_surv = ro + al4(12 * md->num_geoms);
+        }
         s->lds_bytes = (size_t)(so + (t.envs_per_wg - 1) * t.env_stride) * sizeof(float);
-        if (s->lds_bytes > 163840)
-            return cleanup(fail(MI_E_MODEL, "wave path: %zu B of LDS per workgroup exceed the CU's 160 KiB",
-                                s->lds_bytes));
     }
     s->lower.assign(md->lower, md->lower + L);
     s->upper.assign(md->upper, md->upper + L);
@@ -1258,6 +1198,17 @@ int mi_sim_create(const mi_model_desc* md, const mi_sim_params* prm, int32_t N, 
     hipError_t e = hipDeviceSynchronize();
     if (e != hipSuccess) return cleanup(fail(MI_E_HIP, "init: %s", hipGetErrorString(e)));
     if ((rc = sync_kparams(s))) return cleanup(rc);
+    if (s->wave && s->lds_bytes > 64 * 1024) {   // above the default dynamic-LDS limit
+        hipError_t e1 = hipSuccess, e2 = hipSuccess;
+        with_topo(s->topo, [&](auto T) {
+            e1 = hipFuncSetAttribute((const void*)k_env_step_wave<decltype(T)>,
+                                     hipFuncAttributeMaxDynamicSharedMemorySize, (int)s->lds_bytes);
+            e2 = hipFuncSetAttribute((const void*)k_sim_step_wave<decltype(T)>,
+                                     hipFuncAttributeMaxDynamicSharedMemorySize, (int)s->lds_bytes);
+        });
+        if (e1 != hipSuccess || e2 != hipSuccess)
+            return cleanup(fail(MI_E_HIP, "wave kernels: %zu B of LDS per workgroup refused", s->lds_bytes));
+    }
     if (s->wave && s->lds_bytes > 64 * 1024) {   // above the default dynamic-LDS limit
         hipError_t e1 = hipSuccess, e2 = hipSuccess;
         with_topo(s->topo, [&](auto T) {

@@ -29,15 +29,6 @@
 namespace mi {
 
 constexpr int WNV = 32;  // padded DOF count of the wave path
-#ifndef MI_ROLLED_USPACE
-#define MI_ROLLED_USPACE 0
-#endif
-
-// Global-memory view of a generic pointer into device memory (state records, the W-row slab):
-// accesses compile to global_load / global_store instead of flat ones.
-typedef __attribute__((address_space(1))) float gfloat;
-__device__ __forceinline__ gfloat* as_global(float* p) { return (gfloat*)p; }
-__device__ __forceinline__ const gfloat* as_global(const float* p) { return (const gfloat*)p; }
 
 // One wavefront = one env; a workgroup holds E envs (E waves) that share the LDS copy of the
 // model constants and otherwise never interact. Lane id inside the env's wave:
@@ -46,8 +37,7 @@ __device__ __forceinline__ int wave_lane() { return (int)(threadIdx.x & 63u); }
 // accesses are visible to the wave's later accesses. No s_barrier (the other waves of the
 // workgroup are other envs), and wavefront scope: a wave's memory operations are performed in
 // order (LDS and the vector memory path), so the fences only stop the compiler from moving
-// accesses across the sync and emit no waits. (Workgroup-scope fences would wait for every
-// outstanding vector memory access, loads included, at each phase boundary.)
+// accesses across the sync.
 __device__ __forceinline__ void wave_sync() {
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
     __builtin_amdgcn_wave_barrier();
@@ -127,10 +117,7 @@ struct WaveTabs {
     // E envs per workgroup: env w of the workgroup uses [s_env, s_total) shifted by
     // w * env_stride floats (env_stride = s_total - s_env); [0, s_env) is the shared constant block
     int envs_per_wg, s_env, env_stride;
-    // row slot -> lane that holds the row's J in P9 (Delassus-space PGS set-up)
-    int s_own;
-    // J rows [0, j_rows_lds) kept in LDS at s_J (stride nv) for the Delassus set-up (256-VGPR
-    // kernels, where LDS has room; 0 on the 128-VGPR kernels, which keep J in registers)
+    // J rows [0, j_rows_lds) kept in LDS at s_J (stride nv) for the PGS sweeps
     int s_J, j_rows_lds;
     // per-model constant block (see McLayout): global copy, staged into LDS at s_mc once per
     // launch by every workgroup
@@ -279,6 +266,7 @@ MI_D void tree_solve_lds(const WaveTabs& t, const float* Mx, const float* Dinv, 
 // v_readlane at compile-time (register, lane) pairs, so no LDS or barrier is involved.
 // Arithmetic is operation-for-operation that of the runtime-table path above.
 
+// Mc[r] <- Mx[r][lane] for lane == r or lane an ancestor of r, else 0
 // An opaque copy of the lane id: lane-compare masks built from it cannot be hoisted out of
 // the unrolled step that uses them (dozens of hoisted 64-bit masks would spill SGPRs).
 MI_D int lane_here(int lane) {
@@ -286,20 +274,13 @@ MI_D int lane_here(int lane) {
     return lane;
 }
 
-// Mc[r] <- M~[r][lane] for lane == r or lane an ancestor of r, else 0, from the compact rows
-// P3 wrote (the factor's layout: ancestor entries at lrow[r] + depth(r) - 1 - depth(lane), the
-// diagonal at lrow[nv] + r). dl = depth of this lane's DOF.
 template <class T>
-MI_D void ct_load_columns(const float* Lr, int lane, int dl, float (&Mc)[T::nvc]) {
+MI_D void ct_load_columns(const float* Mx, int lane, float (&Mc)[T::nvc]) {
+    const int c = lane < T::nv ? lane : 0;
     sfor<0, T::nv>([&](auto R) {
         constexpr int r = R;
-        constexpr int dr = T::dof.anc_start[r + 1] - T::dof.anc_start[r];
-        constexpr unsigned long long am = (unsigned long long)T::dof.anc_mask[r];
-        const int ln = lane_here(lane);
-        const bool anc = (am >> ln) & 1ull;
-        const int idx = anc ? T::dof.lrow[r] + dr - 1 - dl : T::dof.lrow[T::nv] + r;
-        const float v = Lr[idx];
-        Mc[r] = (anc || ln == r) ? v : 0.0f;
+        constexpr unsigned long long keep = (unsigned long long)T::dof.anc_mask[r] | (1ull << r);
+        Mc[r] = ((keep >> lane_here(lane)) & 1ull) ? Mx[r * T::nv + c] : 0.0f;
     });
 }
 
@@ -665,10 +646,11 @@ MI_D void wave_artic_substep(const DevModel& m, const WaveTabs& t, const DevStat
             diag += mc.lf(MC_ARM, l) + dt * damp;
             r += st.eff[sx(st, k - nr, i)] - damp * us[k];
         }
+        Mx[k * nv + k] = diag;
         rhs[k] = r;
-#ifdef MI_DENSE_M
         if constexpr (TP::kCT) {
-            Mx[k * nv + k] = diag;
+            // ancestors of k from the link's DOF mask (root DOFs: the root chain below k);
+            // uniform j: the S_j reads are LDS broadcasts
             const unsigned am = k < nr ? (1u << k) - 1u : mc.mask(l) & ~(1u << k);
             sfor<0, TP::nv>([&](auto J) {
                 constexpr int j = J;
@@ -679,34 +661,7 @@ MI_D void wave_artic_substep(const DevModel& m, const WaveTabs& t, const DevStat
                     Mx[k * nv + j] = dot6(sj, f);
                 }
             });
-        } else
-#endif
-        if constexpr (TP::kCT) {
-            // M~ straight into the factor's compact LDS rows (DofTree::lrow; ct_publish_factor):
-            // row k's entry for ancestor j at lrow[k] + depth(k) - 1 - depth(j), the diagonal at
-            // lrow[nv] + k. No dense nv x nv block.
-            float* Lr = sm + t.s_L;
-            Lr[TP::dof.lrow[TP::nv] + k] = diag;
-            int rowk = 0;   // lrow[k] + depth(k) - 1 for this lane's k
-            sfor<0, TP::nv>([&](auto K) {
-                constexpr int kk = K;
-                if (k == kk) rowk = TP::dof.lrow[kk] + (TP::dof.anc_start[kk + 1] - TP::dof.anc_start[kk]) - 1;
-            });
-            // ancestors of k from the link's DOF mask (root DOFs: the root chain below k);
-            // uniform j: the S_j reads are LDS broadcasts
-            const unsigned am = k < nr ? (1u << k) - 1u : mc.mask(l) & ~(1u << k);
-            sfor<0, TP::nv>([&](auto J) {
-                constexpr int j = J;
-                constexpr int dj = TP::dof.anc_start[j + 1] - TP::dof.anc_start[j];
-                if ((am >> j) & 1u) {
-                    float sj[6];
-#pragma unroll
-                    for (int c = 0; c < 6; ++c) sj[c] = Ss[6 * j + c];
-                    Lr[rowk - dj] = dot6(sj, f);
-                }
-            });
         } else {
-            Mx[k * nv + k] = diag;
             for (int a = t.anc_start[k]; a < t.anc_start[k + 1]; ++a) {
                 const int j = t.anc_list[a];
                 float sj[6];
@@ -722,21 +677,10 @@ MI_D void wave_artic_substep(const DevModel& m, const WaveTabs& t, const DevStat
     float Mc[TP::nvc];     // CT path: column `lane` of M~, then of its factor (rows 0..nv-1)
     float dvec = 1.0f;    // CT path: lane c holds 1 / D_c
     if constexpr (TP::kCT) {
-        const int dj = lane < nr ? lane : __builtin_popcount(mc.mask(lane < nv ? lane - nr + 1 : 0)) - 1;
-#ifdef MI_DENSE_M
-        {
-            const int c = lane < TP::nv ? lane : 0;
-            sfor<0, TP::nv>([&](auto R) {
-                constexpr int r = R;
-                constexpr unsigned long long keep = (unsigned long long)TP::dof.anc_mask[r] | (1ull << r);
-                Mc[r] = ((keep >> lane_here(lane)) & 1ull) ? Mx[r * TP::nv + c] : 0.0f;
-            });
-        }
-#else
-        ct_load_columns<TP>(sm + t.s_L, lane, dj, Mc);
-#endif
+        ct_load_columns<TP>(Mx, lane, Mc);
         ct_ltdl<TP>(lane, Mc);
         dvec = ct_dinv<TP>(lane, Mc);
+        const int dj = lane < nr ? lane : __builtin_popcount(mc.mask(lane < nv ? lane - nr + 1 : 0)) - 1;
         ct_publish_factor<TP>(lane, dj, Mc, dvec, sm + t.s_L);
     } else {
         for (int k = nv - 1; k >= 0; --k) {
@@ -1009,14 +953,11 @@ MI_D void wave_artic_substep(const DevModel& m, const WaveTabs& t, const DevStat
         nrows = __builtin_amdgcn_readfirstlane(nc + __popcll(limact));   // wave-uniform
         wave_sync();
     };
-    // file this lane's W row: contact row r (A_rr given), or an active limit row with its sign.
-    // Every row of the substep goes to LDS when they all fit there, else all to the global slab
-    // (uniform). Returns the row's slot (-1: this lane files none) and its sign in sc.
-    auto file_row = [&](const auto& res, bool on, int r, int kd, float a_contact, float& sc) -> int {
+    // file this lane's W row: contact row r (A_rr given), or an active limit row with its sign
+    auto file_row = [&](const auto& res, bool on, int r, int kd, float a_contact) {
         constexpr int NR = sizeof(res) / sizeof(res[0]);
         int slot = -1;
-        float a = 0.0f;
-        sc = 1.0f;
+        float sc = 1.0f, a = 0.0f;
         if (on && r >= 0) {
             slot = r;
             a = a_contact;
@@ -1046,18 +987,10 @@ MI_D void wave_artic_substep(const DevModel& m, const WaveTabs& t, const DevStat
                     if (c < nv) wl[c] = res[c] * sc;
             } else {
 #pragma unroll
-                for (int c = 0; c < WNV; ++c) as_global(gW)[(size_t)slot * WNV + c] = c < NR ? res[c] * sc : 0.0f;
+                for (int c = 0; c < WNV; ++c) gW[(size_t)slot * WNV + c] = c < NR ? res[c] * sc : 0.0f;
             }
         }
-        return slot;
     };
-    // Delassus-space PGS operands (CT path, P10): this lane's Delassus row A[r][.] = J_r W_.^T and
-    // v_r = J_r . u*, in lane = row order. Built in P9 by the lane that already holds J_r in
-    // registers, so no J row is ever stored.
-    constexpr int RL = TP::kLamRows > 0 ? TP::kLamRows : 1;
-    float xj[TP::nvc];      // CT: J of this lane's row (its Delassus row is built after the pass)
-    int my_slot = -1;       // the row this lane filed (-1: none)
-    float my_sc = 1.0f;     // its sign (limit rows)
     for (int base = 0; base < total; base += 64) {
         const int bv = base + lane;
         const bool on = bv < total;
@@ -1091,13 +1024,9 @@ MI_D void wave_artic_substep(const DevModel& m, const WaveTabs& t, const DevStat
                     x[c] = bv == 0 ? rhs[c] : (kd == c ? 1.0f : 0.0f);
                 });
             }
-            if constexpr (TP::kWaves <= 2) {
-                if (on && r >= 0 && r < t.j_rows_lds) {   // keep J_r for the Delassus set-up
-                    float* jl = sm + t.s_J + r * TP::nv;
-                    sfor<0, TP::nv>([&](auto C) { jl[C] = x[C]; });
-                }
-            } else {
-                sfor<0, TP::nv>([&](auto C) { xj[C] = x[C]; });
+            if (on && r >= 0 && r < t.j_rows_lds) {   // keep J_r for the PGS sweeps
+                float* jl = sm + t.s_J + r * TP::nv;
+                sfor<0, TP::nv>([&](auto C) { jl[C] = x[C]; });
             }
             STAMP(7);   // P9 J build
             float a;                              // J M~^-1 J^T from the half solve
@@ -1107,7 +1036,7 @@ MI_D void wave_artic_substep(const DevModel& m, const WaveTabs& t, const DevStat
                 limit_rows(x);
                 STAMP(9);   // P9 u* + limit rows
             }
-            my_slot = file_row(x, on, r, kd, a, my_sc);
+            file_row(x, on, r, kd, a);
         } else {
             float jr[WNV];
 #pragma unroll
@@ -1147,73 +1076,11 @@ MI_D void wave_artic_substep(const DevModel& m, const WaveTabs& t, const DevStat
             float a = 0.0f;
 #pragma unroll
             for (int c = 0; c < WNV; ++c) a += jr[c] * wr[c];
-            float sc;
-            file_row(wr, on, r, kd, a, sc);
+            file_row(wr, on, r, kd, a);
         }
         STAMP(10);
     }
     nrows = __builtin_amdgcn_readfirstlane(nrows);
-    // Delassus-space PGS operands when one pass held every row (so xj / my_slot are this lane's
-    // row) and the rows fit the register Delassus rows (wave-uniform): the lane holding J_r builds
-    // A[r][.] = J_r W_.^T and v_r = J_r . u*, then the rows move to lane = row order.
-    float Ar[RL];
-    float vlam = 0.0f;
-    bool lam_path = false;
-    if constexpr (TP::kCT && TP::kWaves <= 2) {
-        // J and W rows in LDS (uniform; the 256-VGPR kernels' layouts hold 64 of each)
-        if (nrows <= TP::kLamRows && nrows <= t.j_rows_lds && nrows <= t.w_rows_lds) {
-            wave_sync();                             // W / J rows and u* complete
-            const int rl = lane < nrows ? lane : 0;
-            float J[TP::nvc];
-            sfor<0, TP::nv>([&](auto C) { J[C] = sm[t.s_J + rl * TP::nv + C]; });
-            float v = 0.0f;
-            sfor<0, TP::nv>([&](auto C) { v += J[C] * us[C]; });
-            // entries past nrows are never read (the sweeps stop there): an early-exit chain,
-            // so the compiler keeps the Delassus row in registers
-#pragma unroll
-            for (int s2 = 0; s2 < RL; ++s2) {
-                if (s2 >= nrows) break;
-                const float* w = w_row<TP::kSelf>(t, sm, s2, TP::nv);
-                float acc = 0.0f;
-                sfor<0, TP::nv>([&](auto C) { acc += J[C] * w[C]; });
-                Ar[s2] = acc;
-            }
-            vlam = v;
-            lam_path = true;
-        }
-    } else if constexpr (TP::kCT) {
-        if (total <= 64 && nrows <= TP::kLamRows) {
-            int* own = reinterpret_cast<int*>(sm + t.s_own);
-            if (my_slot >= 0) own[my_slot] = lane;   // row slot -> the lane holding its J
-            wave_sync();                             // W rows, u* and the owner table complete
-            float J[TP::nvc];
-            sfor<0, TP::nv>([&](auto C) { J[C] = my_slot >= 0 ? xj[C] * my_sc : 0.0f; });
-            float v = 0.0f;
-            sfor<0, TP::nv>([&](auto C) { v += J[C] * us[C]; });
-            const bool wl = nrows <= t.w_rows_lds;
-#pragma unroll
-            for (int s2 = 0; s2 < RL; ++s2) {
-                float acc = 0.0f;
-                if (s2 < nrows) {
-                    if (wl) {           // (separate branches: a select of an LDS and a global
-                                        // pointer would turn every read into a flat load)
-                        const float* w = w_row<TP::kSelf>(t, sm, s2, TP::nv);
-                        sfor<0, TP::nv>([&](auto C) { acc += J[C] * w[C]; });
-                    } else {
-                        const gfloat* w = as_global(gW) + (size_t)s2 * WNV;
-                        sfor<0, TP::nv>([&](auto C) { acc += J[C] * w[C]; });
-                    }
-                }
-                Ar[s2] = acc;
-            }
-            // to lane = row order (ds_bpermute)
-            const int src = lane < nrows ? own[lane] : lane;
-#pragma unroll
-            for (int s2 = 0; s2 < RL; ++s2) Ar[s2] = __shfl(Ar[s2], src, 64);
-            vlam = __shfl(v, src, 64);
-            lam_path = true;
-        }
-    }
     wave_sync();
 
     STAMP(10);  // P9 row filing + trailing barrier
@@ -1221,7 +1088,7 @@ MI_D void wave_artic_substep(const DevModel& m, const WaveTabs& t, const DevStat
     STAT(16, nrows > t.w_rows_lds);
     STAT(17, nrows > 64);
     STAT(18, total > 64);
-    STAT(19, !lam_path);
+    STAT(19, nrows > t.j_rows_lds);
     STAT(20, ncon);
     STAT(21, nrows > 16);
     STAT(22, nrows > 24);
@@ -1229,26 +1096,46 @@ MI_D void wave_artic_substep(const DevModel& m, const WaveTabs& t, const DevStat
     STAT(24, nrows > 40);
     STAT(25, nrows > 48);
     STAT(26, t.w_rows_lds);
-    STAT(27, TP::kLamRows);
-    // ---- P10: projected Gauss-Seidel (velocity level, p.iters sweeps, rows in order)
+    STAT(27, t.j_rows_lds);
+    // ---- P10: projected Gauss-Seidel. Lane k (mod 32) owns dof k; the wave's lower half
+    // holds J / W of rows 0..63 in registers, the upper half rows 64..127. Rows are swept in
+    // order; only the half owning the current row is active and u is copied across halves
+    // between the two sub-sweeps. Row metadata and lambdas live in lane registers (row r in
+    // lane r % 64, bank r / 64) and are read with readlane.
 #ifndef MI_DIAG_NO_PGS
-    // Delassus-space (lambda-space) sweeps on the compiled-topology path (the common case): lane r
-    // holds row r's v_r = J_r . u and its Delassus row A[r][s] = J_r . W_s (from P9), so a row
-    // update is readlanes + the projection + one FMA per lane, with no cross-lane reduction on
-    // the dependent chain; u = u* + sum_r W_r lambda_r after the sweeps. Same row order,
-    // projection and lambda carry as the u-space sweeps below (equal in exact arithmetic; float
-    // rounding differs).
+    // Delassus-space (lambda-space) sweeps on the compiled-topology path when every row's J and
+    // W sit in LDS (the common case): lane r holds row r's v_r = J_r . u and its Delassus row
+    // A[r][s] = J_r . W_s, so a row update is readlanes + the projection + one FMA per lane,
+    // with no cross-lane reduction on the dependent chain; u = u* + sum_r W_r lambda_r after the
+    // sweeps. Same row order, projection and lambda carry as the u-space sweeps below (equal in
+    // exact arithmetic; float rounding differs).
     bool lam_done = false;
     if constexpr (TP::kCT) {
-        if (lam_path) {                                               // wave-uniform
+        if (nrows <= TP::kLamRows && nrows <= t.j_rows_lds && nrows <= t.w_rows_lds) {   // wave-uniform
             constexpr int NV = TP::nv;
+            constexpr int RMAX = TP::kLamRows;                      // rows of this path
+            const float* sJ = sm + t.s_J;
             float b = 0.0f, ia = 1.0f, kd = 0.0f, lam = 0.0f;
             if (lane < nrows) {
                 b = sm[t.s_rb + lane];
                 ia = 1.0f / sm[t.s_ad + lane];
                 kd = sm[t.s_rk + lane];
             }
-            float v = vlam;
+            const int rl = lane < nrows ? lane : 0;
+            float Jr[NV];
+            sfor<0, NV>([&](auto C) { Jr[C] = sJ[rl * NV + C]; });
+            float v = 0.0f;
+            sfor<0, NV>([&](auto C) { v += Jr[C] * us[C]; });
+            float Ar[RMAX];
+#pragma unroll
+            for (int s2 = 0; s2 < RMAX; ++s2) {
+                float a = 0.0f;
+                if (s2 < nrows) {
+                    const float* w = w_row<TP::kSelf>(t, sm, s2, NV);
+                    sfor<0, NV>([&](auto C) { a += Jr[C] * w[C]; });
+                }
+                Ar[s2] = a;
+            }
             const float mu = p.friction;
             for (int it = 0; it < p.iters; ++it) {
                 // opaque per sweep: keeps the loop-invariant readlanes inside the sweep
@@ -1257,7 +1144,7 @@ MI_D void wave_artic_substep(const DevModel& m, const WaveTabs& t, const DevStat
                 asm volatile("" : "+s"(nrow_it));
                 float lamn = 0.0f;
 #pragma unroll
-                for (int rr = 0; rr < RL; ++rr) {
+                for (int rr = 0; rr < RMAX; ++rr) {
                     if (rr >= nrow_it) break;
                     __builtin_amdgcn_sched_barrier(0);
                     const float vr = readlane(v, rr);
@@ -1276,14 +1163,10 @@ MI_D void wave_artic_substep(const DevModel& m, const WaveTabs& t, const DevStat
             }
             float u = lane < NV ? us[lane] : 0.0f;
             const int kc = lane < NV ? lane : 0;
-            const bool wl = nrows <= t.w_rows_lds;
 #pragma unroll
-            for (int rr = 0; rr < RL; ++rr) {
+            for (int rr = 0; rr < RMAX; ++rr) {
                 if (rr >= nrows) break;
-                float w;
-                if (wl) w = w_row<TP::kSelf>(t, sm, rr, NV)[kc];
-                else w = as_global(gW)[(size_t)rr * WNV + kc];
-                u += w * readlane(lam, rr);
+                u += w_row<TP::kSelf>(t, sm, rr, NV)[kc] * readlane(lam, rr);
             }
             if (lane < NV) us[lane] = u;
             if (lane < nrows) sm[t.s_ad + lane] = lam;           // reuse: lambda of row lane
@@ -1294,27 +1177,39 @@ MI_D void wave_artic_substep(const DevModel& m, const WaveTabs& t, const DevStat
     {
         const int half = lane >> 5, kl = lane & 31;
         // J_r[kl] is rebuilt per row from this lane's DOF subspace and the row's force
-        // direction (the same dot6 as P9); W_r[kl] is read per row from LDS when this substep's
-        // rows all fit there (uniform), else by bounded buffer loads from the slab (the
-        // descriptor covers rows [0, nrows), so slots past the last row read as 0).
-        // one bank (nrows <= 64): both half-waves hold rows 0..63, so every lane applies every
-        // row's update and no half-to-half hand-over is needed; two banks: half h takes rows
-        // 64h .. 64h+63.
+        // direction (the same dot6 as P9), so only W_r occupies registers
         float S6[6];
 #pragma unroll
         for (int q = 0; q < 6; ++q) S6[q] = kl < nv ? Ss[6 * kl + q] : 0.0f;
+        // W rows: from LDS when this substep's rows all fit there (uniform branch), else by
+        // bounded buffer loads from the slab (the descriptor covers rows [0, nrows), so slots
+        // past the last row read as 0 without touching memory).
+        // one bank (nrows <= 64): both half-waves hold rows 0..63, so every lane applies every
+        // row's update and no half-to-half hand-over is needed; two banks: half h holds rows
+        // 64h .. 64h+63.
         const bool one_bank = nrows <= 64;
-        const bool wlds = nrows <= t.w_rows_lds;      // implies one_bank (w_rows_lds <= 64)
-        const float km = kl < nv ? 1.0f : 0.0f;
-        const int kc = kl < nv ? kl : 0;
-        const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
-            (void*)gW, (short)0, nrows * WNV * (int)sizeof(float), 0x00020000);
-        const int vo = ((one_bank ? 0 : 64 * half) * WNV + kl) * (int)sizeof(float);
-        auto wload = [&](int rr) -> float {
-            if (wlds) return w_row<TP::kSelf>(t, sm, rr, nv)[kc] * km;
-            return __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(
-                                                 rs, vo, rr * WNV * (int)sizeof(float), 0));
-        };
+        float Wr[64];
+        if (nrows <= t.w_rows_lds) {                  // implies one_bank (w_rows_lds <= 64)
+            const float km = kl < nv ? 1.0f : 0.0f;
+            const int kc = kl < nv ? kl : 0;
+            if constexpr (TP::kCT) {
+#pragma unroll
+                for (int rr = 0; rr < 64; ++rr)
+                    Wr[rr] = w_row<TP::kSelf>(t, sm, min(rr, t.w_rows_lds - 1), TP::nv)[kc] * km;
+            } else {
+#pragma unroll
+                for (int rr = 0; rr < 64; ++rr)
+                    Wr[rr] = w_row<TP::kSelf>(t, sm, min(rr, t.w_rows_lds - 1), nv)[kc] * km;
+            }
+        } else {
+            const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
+                (void*)gW, (short)0, nrows * WNV * (int)sizeof(float), 0x00020000);
+            const int vo = ((one_bank ? 0 : 64 * half) * WNV + kl) * (int)sizeof(float);
+#pragma unroll
+            for (int rr = 0; rr < 64; ++rr)
+                Wr[rr] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(
+                                                       rs, vo + rr * WNV * (int)sizeof(float), 0, 0));
+        }
         // row r's data in lane r % 64, bank r / 64: b, 1/A_rr, kind, DOF mask, f (6)
         float b0 = 0, b1 = 0, ia0 = 1, ia1 = 1, k0 = 0, k1 = 0, lam0 = 0.0f, lam1 = 0.0f;
         float fa[6] = {0, 0, 0, 0, 0, 0}, fb[6] = {0, 0, 0, 0, 0, 0};
@@ -1342,15 +1237,16 @@ MI_D void wave_artic_substep(const DevModel& m, const WaveTabs& t, const DevStat
         }
         const float mu = p.friction;
         float u = kl < nv ? us[kl] : 0.0f;
-        if constexpr (TP::kWaves <= 2 && TP::kLamRows < 64 && !MI_ROLLED_USPACE) {
-        // 256-VGPR kernels: this lane's W_r[kl] of all 64 rows of its bank in registers, rows
-        // fully unrolled (readlanes at constant lanes); the next row's J is built inside the
-        // current row's schedule region so it overlaps the reduction chain.
-        float Wr[64];
-#pragma unroll
-        for (int rr = 0; rr < 64; ++rr) Wr[rr] = rr < nrows ? wload(min(rr, 63)) : 0.0f;
-        auto sweeps = [&](auto ONE_) {
+        // One Gauss-Seidel sweep schedule. Per row: J_r . u by a DPP half-wave sum, the
+        // projected lambda update, u += W_r dlambda. The next row's J (readlanes + dot6, no
+        // dependence on u) is built inside the current row's schedule region so it overlaps the
+        // reduction chain. The friction rows of a contact follow its normal row in the same
+        // sweep, so the normal's current lambda is carried in a wave-uniform value.
+        const float* sJl = sm + t.s_J + (kl < nv ? kl : 0);
+        const float kin = kl < nv ? 1.0f : 0.0f;
+        auto sweeps = [&](auto ONE_, auto JL_) {
             constexpr bool ONE = decltype(ONE_)::value;
+            constexpr bool JL = decltype(JL_)::value;   // J rows from LDS (one bank only)
             for (int it = 0; it < p.iters; ++it) {
                 // opaque per sweep: stops the compiler hoisting the loop-invariant readlanes of
                 // every row out of the iteration loop (they would pin hundreds of SGPRs)
@@ -1368,6 +1264,10 @@ MI_D void wave_artic_substep(const DevModel& m, const WaveTabs& t, const DevStat
                     const float bb = h ? b1 : b0, ii = h ? ia1 : ia0, kk = h ? k1 : k0;
                     const unsigned mm = h ? mb : ma, mm2 = h ? mb2 : ma2;
                     auto jrow = [&](int rr, int& kind) -> float {
+                        if constexpr (JL) {
+                            kind = (int)readlane(kk, rr);
+                            return sJl[rr * nv] * kin;
+                        }
                         float fr[6];
 #pragma unroll
                         for (int q = 0; q < 6; ++q) fr[q] = readlane(h ? fb[q] : fa[q], rr);
@@ -1379,6 +1279,7 @@ MI_D void wave_artic_substep(const DevModel& m, const WaveTabs& t, const DevStat
                     };
                     int kind_c;
                     float jc_c = jrow(0, kind_c);
+                    // fully unrolled (no early exit) so Wr stays register-indexed
 #pragma unroll
                     for (int rr = 0; rr < 64; ++rr) {
                         const int r = rr + 64 * h;
@@ -1413,48 +1314,9 @@ MI_D void wave_artic_substep(const DevModel& m, const WaveTabs& t, const DevStat
                 }
             }
         };
-        if (one_bank) sweeps(std::true_type{});
-        else sweeps(std::false_type{});
-        } else {
-        // 128-VGPR kernels: rows in order, one at a time (rolled loop over a uniform row counter;
-        // this path only takes the rare row-heavy substeps, so it is built for a small register
-        // footprint). Per row: J_r . u by a DPP half-wave sum, the projected lambda update,
-        // u += W_r dlambda. The friction rows of a contact follow its normal row in the same
-        // sweep, so the normal's current lambda is carried in a wave-uniform value.
-        const int nbank = one_bank ? 1 : 2;
-        for (int it = 0; it < p.iters; ++it) {
-            float lamn = 0.0f;
-            for (int h = 0; h < nbank; ++h) {
-                const int rend = min(64, nrows - 64 * h);
-                for (int rr = 0; rr < rend; ++rr) {
-                    float fr[6];
-#pragma unroll
-                    for (int q = 0; q < 6; ++q) fr[q] = readlane(h ? fb[q] : fa[q], rr);
-                    const unsigned msk = (unsigned)__builtin_amdgcn_readlane((int)(h ? mb : ma), rr);
-                    const unsigned msk2 = (unsigned)__builtin_amdgcn_readlane((int)(h ? mb2 : ma2), rr);
-                    const int kind = (int)readlane(h ? k1 : k0, rr);
-                    const float wv = wload(rr);
-                    const float jd = kind == 3 ? fr[0] : dot6(S6, fr);
-                    const float jc = (((msk >> kl) & 1u) ? jd : 0.0f) - (((msk2 >> kl) & 1u) ? jd : 0.0f);
-                    const float sum = half_sums(jc * u);
-                    const float jv = readlane(sum, h ? 63 : 31);
-                    const float br = readlane(h ? b1 : b0, rr), iar = readlane(h ? ia1 : ia0, rr);
-                    const float l0 = readlane(h ? lam1 : lam0, rr);
-                    float ln = l0 + (br - jv) * iar;
-                    const bool fric = kind == 1 || kind == 2;
-                    const float lim = mu * lamn;
-                    ln = fmaxf(ln, fric ? -lim : 0.0f);     // normal / limit: lambda >= 0
-                    ln = fric ? fminf(ln, lim) : ln;         // friction: |lambda| <= mu lambda_n
-                    lamn = kind == 0 ? ln : lamn;
-                    const float dl = ln - l0;
-                    if (one_bank || half == h) u += wv * dl;
-                    if (lane == rr) { if (h) lam1 = ln; else lam0 = ln; }
-                }
-                // hand u to the other half for its sub-sweep
-                if (!one_bank) u = __shfl(u, kl + 32 * h, 64);
-            }
-        }
-        }
+        if (one_bank && nrows <= t.j_rows_lds) sweeps(std::true_type{}, std::true_type{});
+        else if (one_bank) sweeps(std::true_type{}, std::false_type{});
+        else sweeps(std::false_type{}, std::false_type{});
         if (lane < nv) us[lane] = u;
         if (lane < nrows) sm[t.s_ad + lane] = lam0;          // reuse: lambda of row lane
         if (lane + 64 < nrows) sm[t.s_ad + lane + 64] = lam1;

@@ -53,10 +53,10 @@ def main():
     print(f"{'total (1 env-substep)':26s} {tot:9.0f}")
     stats = {"mean rows": buf[15] / cnt, "frac rows > LDS W rows": buf[16] / cnt,
              "frac rows > 64": buf[17] / cnt, "frac solve vectors > 64": buf[18] / cnt,
-             "frac u-space PGS": buf[19] / cnt, "mean contacts": buf[20] / cnt,
+             "frac rows > LDS J rows": buf[19] / cnt, "mean contacts": buf[20] / cnt,
              "frac rows > 16": buf[21] / cnt, "frac rows > 24": buf[22] / cnt,
              "frac rows > 32": buf[23] / cnt, "frac rows > 40": buf[24] / cnt,
-             "frac rows > 48": buf[25] / cnt, "LDS W rows": buf[26] / cnt, "Delassus PGS rows max": buf[27] / cnt}
+             "frac rows > 48": buf[25] / cnt, "LDS W rows": buf[26] / cnt, "LDS J rows": buf[27] / cnt}
     print(json.dumps({"row_stats_per_env_substep": {k: round(v, 4) for k, v in stats.items()}}))
 
 
