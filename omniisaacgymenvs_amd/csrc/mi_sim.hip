@@ -69,6 +69,7 @@ struct mi_sim {
     size_t lds_bytes = 0;
     void* kp_dev = nullptr;  // device copy of KParams (wave path)
     int num_cu = 0;          // compute units of the device (queried on first use)
+    int post_kernel = -1, post_grid = 0;   // last mi_task_post_step launch (mi_task_post_kernel)
     std::vector<float> lower, upper;  // host copy for mi_sim_info
     std::vector<void*> allocs;
 };
@@ -161,12 +162,6 @@ __global__ void k_post_step(DevModel m, DevState st, DevTask tp, const float* ac
                   progress_buf, pot, prev);
 }
 
-// RLTask.post_physics_step for the locomotion tasks on the per-env record layout (fs = 1,
-// es = record floats): 64 envs per 64-lane workgroup, HBM-streaming. The block's records and
-// action rows are contiguous in HBM: loaded with coalesced float4 reads into padded LDS rows;
-// each lane then runs the same per-env task math as k_post_step (loco_obs_env / loco_reward /
-// loco_done) on an LDS view of its env, into an LDS obs tile that leaves as coalesced float4
-// stores (the [N, O] obs rows of 64 consecutive envs are one contiguous span).
 // RLTask.post_physics_step for the locomotion tasks on the per-env record layout (fs = 1,
 // es = record floats): TE envs per 64-lane workgroup, HBM-streaming. The block's records and
 // action rows are contiguous in HBM: loaded with coalesced float4 reads into padded LDS rows;
@@ -295,153 +290,6 @@ __global__ __launch_bounds__(64) void k_loco_post_tiled(DevModel m, DevState st,
             ((float4*)dst)[k] = ((const float4*)sobs)[k];   // sobs 16-B aligned: ds_read_b128
     } else {
         for (int k = lane; k < cnt; k += 64) dst[k] = sobs[k];
-    }
-}
-
-// k_loco_post_tiled<32, true> with the HBM latency hidden behind the math: each workgroup walks
-// the tiles t = blockIdx.x, + gridDim.x, ... (grid = resident workgroups) and, while it computes
-// tile t from LDS, holds the global loads of tile t + gridDim.x in registers (records, action
-// rows, per-env scalars). The counters of the one-tile kernel showed 62 % of wave cycles
-// waiting on memory at 2 resident workgroups per SIMD (LDS-bound). Same arithmetic and
-// write order per env as k_loco_post_tiled<32, true> (bit-identical outputs).
-// Host-checked: es % 4 == 0, es <= 128 (MI_PIPE_R float4 per lane), 1 <= A <= 32.
-constexpr int MI_PIPE_R = 16;   // 32 records x 128 floats / 4 / 64 lanes
-constexpr int MI_PIPE_A = 16;   // 32 envs x 32 actions / 64 lanes
-// floor(x / d) for 0 <= x < 4096, 1 <= d <= 128: (x * ceil(2^20 / d)) >> 20 (exact there)
-MI_D int div_small(int x, unsigned magic) { return (int)(((unsigned)x * magic) >> 20); }
-
-__global__ __launch_bounds__(64) void k_loco_post_pipe(DevModel m, DevState st, DevTask tp,
-                                                      const float* __restrict__ actions,
-                                                      float* obs, float* rew, int64_t* reset_buf,
-                                                      int64_t* progress_buf, float* pot,
-                                                      float* prev) {
-    constexpr int TE = 32;
-    extern __shared__ __attribute__((aligned(16))) float sm[];
-    const int lane = threadIdx.x;
-    const int O = tp.O, A = tp.A, D = m.D, S = m.S, es = st.es, N = st.N;
-    const int ntiles = (N + TE - 1) / TE;
-    const int k0 = 13 + 2 * D, s0 = 13 + 3 * D, ns = 6 * S, PC = (k0 + ns) | 1;   // odd row stride: no LDS bank aliasing across envs
-    const int ka = 12 + 2 * D + ns;                        // obs column of actions[0]
-    const unsigned mag_es = ((1u << 20) + es - 1) / es, mag_a = ((1u << 20) + A - 1) / A;
-    float* srec = sm;
-    float* sobs = sm + TE * PC;
-    float* sterm = sobs + TE * O;                          // [TE][3] sums
-    float* spot = sterm + 3 * TE;                          // [TE] potentials (in / out)
-    float* sprev = spot + TE;                              // [TE] prev_potentials (out)
-    float4 rr[MI_PIPE_R];
-    float ra[MI_PIPE_A];
-    int64_t pg = 0, rs = 0;
-    int nf = 0;
-    float pt = 0.0f;
-    auto issue = [&](int t) {   // global loads of tile t into registers (no wait here)
-        const int e0 = t * TE, n = min(TE, N - e0);
-        const int c4 = n * es / 4, ca = n * A;
-        const float4* s4 = (const float4*)(st.root_pos + (size_t)e0 * es);
-        const float* ga = actions + (size_t)e0 * A;
-#pragma unroll
-        for (int r = 0; r < MI_PIPE_R; ++r) {
-            const int k = lane + 64 * r;
-            if (k < c4) rr[r] = s4[k];
-        }
-#pragma unroll
-        for (int r = 0; r < MI_PIPE_A; ++r) {
-            const int k = lane + 64 * r;
-            if (k < ca) ra[r] = ga[k];
-        }
-        if (lane < n) {
-            const int i = e0 + lane;
-            pg = progress_buf[i];
-            rs = reset_buf[i];
-            nf = st.nan_flag[i];
-            pt = pot[i];
-        }
-    };
-    // lane constants of the element-wise obs phase (1 <= D, 6S <= 64: host-checked)
-    const int dof_pe = 64 / D, dof_le = lane / D, dof_j = lane - dof_le * D;
-    const bool dof_lane = dof_le < dof_pe;
-    const float dof_lo = dof_lane ? m.lower[dof_j + 1] : 0.0f, dof_hi = dof_lane ? m.upper[dof_j + 1] : 1.0f;
-    const int sen_pe = ns > 0 ? 64 / ns : 0, sen_le = ns > 0 ? lane / ns : 0, sen_c = lane - sen_le * ns;
-    const bool sen_lane = ns > 0 && sen_le < sen_pe;
-    int t = blockIdx.x;
-    if (t < ntiles) issue(t);
-    for (; t < ntiles; t += gridDim.x) {
-        const int e0 = t * TE, n = min(TE, N - e0);
-        {   // registers -> LDS: compact records, actions into the obs rows' action columns
-            const int c4 = n * es / 4, ca = n * A;
-#pragma unroll
-            for (int r = 0; r < MI_PIPE_R; ++r) {
-                const int k = lane + 64 * r;
-                if (k < c4) {
-                    const float vv[4] = {rr[r].x, rr[r].y, rr[r].z, rr[r].w};
-                    const int f0 = 4 * k, e = div_small(f0, mag_es), c0 = f0 - e * es;
-#pragma unroll
-                    for (int q = 0; q < 4; ++q) {
-                        const int c = c0 + q;
-                        if (c < k0) srec[e * PC + c] = vv[q];
-                        else if (c >= s0 && c < s0 + ns) srec[e * PC + k0 + (c - s0)] = vv[q];
-                    }
-                }
-            }
-#pragma unroll
-            for (int r = 0; r < MI_PIPE_A; ++r) {
-                const int k = lane + 64 * r;
-                if (k < ca) {
-                    const int e = div_small(k, mag_a);
-                    sobs[e * O + ka + (k - e * A)] = ra[r];
-                }
-            }
-        }
-        const int64_t progress = pg + 1, rb = rs;          // rl_task.py:242
-        const int nflag = nf;
-        if (lane < n) spot[lane] = pt;
-        __syncthreads();
-        if (t + (int)gridDim.x < ntiles) issue(t + gridDim.x);   // in flight during the math
-        DevState v = st;                    // the tile's envs, viewed in LDS
-        v.fs = 1; v.es = PC;
-        v.root_pos = srec; v.root_quat = srec + 3; v.root_vel = srec + 7;
-        v.q = srec + 13; v.qd = srec + 13 + D; v.sens = srec + k0;
-        // get_observations per-DOF and sensor entries (locomotion.py:226-228), the arithmetic of
-        // loco_obs_dof, on all 64 lanes: lane = (env slot, column), the column a lane constant
-        if (dof_lane)
-            for (int e = dof_le; e < n; e += dof_pe) {
-                const float* r = srec + e * PC;
-                float* o = sobs + e * O;
-                o[12 + dof_j] = ref_unscale(r[13 + dof_j], dof_lo, dof_hi);
-                o[12 + D + dof_j] = r[13 + D + dof_j] * tp.dof_vel_scale;
-            }
-        if (sen_lane)
-            for (int e = sen_le; e < n; e += sen_pe)
-                sobs[e * O + 12 + 2 * D + sen_c] = srec[e * PC + k0 + sen_c] * tp.contact_force_scale;
-        __syncthreads();
-        // root-frame block and the reward's DOF-order sums, one lane per env
-        if (lane < n) {
-            const int i = e0 + lane;
-            float* R = sobs + (size_t)lane * O;
-            loco_obs_root(v, tp, lane, R, spot, sprev);
-            const LocoTerms lt = loco_reward_terms(tp, D, R, R + ka);
-            const float p_new = spot[lane], p_old = sprev[lane];
-            rew[i] = loco_reward_total(tp, R[0], R[10], R[11], p_new, p_old, lt);
-            pot[i] = p_new;
-            prev[i] = p_old;
-            int64_t d = loco_done(tp, R[0], rb, progress);
-            if (nflag) {                                                // nan_guard
-                st.nan_flag[i] = 0;
-                atomicAdd(st.nan_total, 1ull);
-                d = 1;
-            }
-            reset_buf[i] = d;
-            progress_buf[i] = progress;
-        }
-        __syncthreads();
-        float* dst = obs + (size_t)e0 * O;
-        const int cnt = n * O;
-        if ((((uintptr_t)dst) & 15) == 0 && (cnt & 3) == 0) {
-            for (int k = lane; k < cnt / 4; k += 64)
-                ((float4*)dst)[k] = ((const float4*)sobs)[k];   // sobs 16-B aligned: ds_read_b128
-        } else {
-            for (int k = lane; k < cnt; k += 64) dst[k] = sobs[k];
-        }
-        __syncthreads();                    // the next tile overwrites the LDS tiles
     }
 }
 
@@ -608,6 +456,182 @@ __device__ __forceinline__ int wave_env() {
 }
 __device__ __forceinline__ float* wave_env_lds(const WaveTabs& t, float* smem) {
     return smem + (threadIdx.x >> 6) * t.env_stride;
+}
+
+// k_loco_post_tiled<32, true> with the HBM latency hidden behind the math: each workgroup walks
+// the tiles t = blockIdx.x, + gridDim.x, ... (grid = resident workgroups) and, while it computes
+// tile t from LDS, holds the global loads of tile t + gridDim.x in registers (records, action
+// rows, per-env scalars). Same arithmetic and write order per env as k_loco_post_tiled<32, true>
+// (bit-identical outputs).
+// Data movement is whole float4s with wave-uniform trip counts and no per-element guards:
+//  - record tile in LDS: each record's float4s as they sit in HBM, minus the float4s that hold
+//    efforts only (the task never reads them), at an odd float4 stride P4 so one field of 32
+//    envs spreads over the banks; a dropped float4 lands in the record's spare slot P4 - 1;
+//  - loads clamp their index to the tile (a ragged last tile re-reads its last element into
+//    slots nobody reads) instead of branching;
+//  - the parameter block is read through the laundered KParams pointer once per tile (scalar
+//    loads), so no loop-invariant parameter occupies an SGPR across the tile loop.
+// NR4 = float4 per lane per tile (32 records x es floats / 4 / 64 = es / 8), a template
+// constant: the loads of a tile are one straight-line block, every register defined on every
+// path (a guarded block made the compiler stage the tile through scratch). Action rows: always
+// MI_PIPE_A loads per lane, the index clamped to the tile, the overhang written to a spare float.
+// Host-checked: records (fs = 1) of es = 8 NR4 floats; 1 <= A <= 32; D, 6S <= 64.
+constexpr int MI_PIPE_A = 16;   // 32 envs x <= 32 actions / 64 lanes
+// floor(x / d) for 0 <= x < 4096, 1 <= d <= 128: (x * ceil(2^20 / d)) >> 20 (exact there)
+MI_D int div_small(int x, unsigned magic) { return (int)(((unsigned)x * magic) >> 20); }
+
+typedef float v4f __attribute__((ext_vector_type(4)));   // native 16-B vector (no struct copies)
+
+struct PipeGeo {   // record-tile geometry of k_loco_post_pipe (floats unless noted)
+    int es4, ef0, ef1, nd, P4, P, s0;
+};
+__host__ __device__ inline PipeGeo pipe_geo(int es, int D) {
+    PipeGeo g;
+    g.es4 = es >> 2;
+    g.ef0 = (13 + 2 * D + 3) >> 2;                        // first float4 past qd
+    g.ef1 = (13 + 3 * D) >> 2;                            // float4 holding the first sensor value
+    if (g.ef1 < g.ef0) g.ef1 = g.ef0;
+    g.nd = g.ef1 - g.ef0;                                 // float4s of efforts only: dropped
+    g.P4 = ((g.es4 - g.nd) + 1) | 1;                      // odd, with a spare slot P4 - 1
+    g.P = 4 * g.P4;
+    g.s0 = 13 + 3 * D - 4 * g.nd;                         // sensors in the LDS record
+    return g;
+}
+static size_t post_pipe_lds(int es, int A, int O, int D) {
+    const PipeGeo g = pipe_geo(es, D);
+    // records [32][P], obs tile [32][O], reward sums [32][3], potentials in / out, spare float
+    return sizeof(float) * (size_t)(32 * g.P + 32 * O + 3 * 32 + 2 * 32 + 4);
+}
+
+template <int NR4>
+__global__ __launch_bounds__(64) void k_loco_post_pipe(const KParams* __restrict__ kp_arg,
+                                                      const float* __restrict__ actions,
+                                                      float* obs, float* rew, int64_t* reset_buf,
+                                                      int64_t* progress_buf, float* pot,
+                                                      float* prev) {
+    constexpr int TE = 32;
+    extern __shared__ __attribute__((aligned(16))) float sm[];
+    const int lane = threadIdx.x;
+    const KParams* kp = opaque_kp(kp_arg);
+    const int O = kp->tp.O, A = kp->tp.A, D = kp->m.D, S = kp->m.S, es = kp->st.es, N = kp->st.N;
+    const int ntiles = (N + TE - 1) / TE;
+    const PipeGeo g = pipe_geo(es, D);
+    const int ns = 6 * S, ka = 12 + 2 * D + ns;            // obs column of actions[0]
+    const unsigned mag_es = ((1u << 20) + g.es4 - 1) / g.es4, mag_a = ((1u << 20) + A - 1) / A;
+    v4f* srec4 = reinterpret_cast<v4f*>(sm);
+    float* srec = sm;
+    float* sobs = sm + TE * g.P;
+    float* sterm = sobs + TE * O;                          // [TE][3] sums
+    float* spot = sterm + 3 * TE;                          // [TE] potentials (in / out)
+    float* sprev = spot + TE;                              // [TE] prev_potentials (out)
+    const int trash = TE * g.P + TE * O + 5 * TE;          // spare float (action overhang)
+    v4f rr[NR4];
+    float ra[MI_PIPE_A];
+    int64_t pg = 0, rs = 0;
+    int nf = 0;
+    float pt = 0.0f;
+    // global loads of tile T into registers (no wait here). A macro, not a lambda: through a
+    // lambda's by-reference captures the compiler kept rr in scratch.
+#define MI_PIPE_ISSUE(K, T)                                                                     \
+    do {                                                                                        \
+        const int e0_ = (T) * TE, n_ = min(TE, N - e0_);                                        \
+        const int c4_ = n_ * g.es4, ca_ = n_ * A;                                               \
+        const v4f* s4_ = reinterpret_cast<const v4f*>((K)->st.root_pos + (size_t)e0_ * es);       \
+        const float* ga_ = actions + (size_t)e0_ * A;                                           \
+        _Pragma("unroll") for (int r = 0; r < NR4; ++r) rr[r] = s4_[min(lane + 64 * r, c4_ - 1)]; \
+        _Pragma("unroll") for (int r = 0; r < MI_PIPE_A; ++r) ra[r] = ga_[min(lane + 64 * r, ca_ - 1)]; \
+        const int i_ = e0_ + min(lane, n_ - 1);                                                 \
+        pg = progress_buf[i_];                                                                  \
+        rs = reset_buf[i_];                                                                     \
+        nf = (K)->st.nan_flag[i_];                                                              \
+        pt = pot[i_];                                                                           \
+    } while (0)
+    // lane constants of the element-wise obs phase
+    const int dof_pe = 64 / D, dof_le = lane / D, dof_j = lane - dof_le * D;
+    const bool dof_lane = dof_le < dof_pe;
+    const float dof_lo = dof_lane ? kp->m.lower[dof_j + 1] : 0.0f;
+    const float dof_hi = dof_lane ? kp->m.upper[dof_j + 1] : 1.0f;
+    const int sen_pe = ns > 0 ? 64 / ns : 0, sen_le = ns > 0 ? lane / ns : 0, sen_c = lane - sen_le * ns;
+    const bool sen_lane = ns > 0 && sen_le < sen_pe;
+    int t = blockIdx.x;
+    if (t < ntiles) MI_PIPE_ISSUE(kp, t);
+    for (; t < ntiles; t += gridDim.x) {
+        const KParams* k = opaque_kp(kp_arg);
+        const int e0 = t * TE, n = min(TE, N - e0);
+        // registers -> LDS: records (float4 slots), actions into the obs rows' action columns
+#pragma unroll
+        for (int r = 0; r < NR4; ++r) {
+            const int kk = lane + 64 * r, e = div_small(kk, mag_es), k4 = kk - e * g.es4;
+            const int slot = k4 < g.ef0 ? k4 : (k4 < g.ef1 ? g.P4 - 1 : k4 - g.nd);
+            srec4[e * g.P4 + slot] = rr[r];
+        }
+#pragma unroll
+        for (int r = 0; r < MI_PIPE_A; ++r) {
+            const int kk = lane + 64 * r, e = div_small(kk, mag_a);
+            sobs[kk < TE * A ? e * O + ka + (kk - e * A) : trash - TE * g.P] = ra[r];
+        }
+        const int64_t progress = pg + 1, rb = rs;          // rl_task.py:242
+        const int nflag = nf;
+        if (lane < TE) spot[lane] = pt;
+        __syncthreads();
+        if (t + (int)gridDim.x < ntiles) MI_PIPE_ISSUE(k, t + (int)gridDim.x);   // in flight during the math
+        // get_observations per-DOF and sensor entries (locomotion.py:226-228), the arithmetic of
+        // loco_obs_dof, on all 64 lanes: lane = (env slot, column), the column a lane constant
+        if (dof_lane) {
+            const float vs = k->tp.dof_vel_scale;
+            for (int e = dof_le; e < n; e += dof_pe) {
+                const float* r = srec + e * g.P;
+                float* o = sobs + e * O;
+                o[12 + dof_j] = ref_unscale(r[13 + dof_j], dof_lo, dof_hi);
+                o[12 + D + dof_j] = r[13 + D + dof_j] * vs;
+            }
+        }
+        if (sen_lane) {
+            const float cs = k->tp.contact_force_scale;
+            for (int e = sen_le; e < n; e += sen_pe)
+                sobs[e * O + 12 + 2 * D + sen_c] = srec[e * g.P + g.s0 + sen_c] * cs;
+        }
+        __syncthreads();
+        // root-frame block and the reward's DOF-order sums: env lane & 31 on both lane halves
+        {
+            const DevTask& tp = k->tp;
+            const int e = lane & 31;
+            float* R = sobs + (size_t)e * O;
+            loco_obs_root_pair(srec + e * g.P, tp, lane, R, spot, sprev, e < n);
+        }
+        const LocoTerms lt = loco_reward_terms_pair(k->tp, D, sobs + (size_t)(lane & 31) * O,
+                                                    sobs + (size_t)(lane & 31) * O + ka, lane);
+        if (lane < n) {
+            const int i = e0 + lane;
+            const DevTask& tp = k->tp;
+            float* R = sobs + (size_t)lane * O;
+            const float p_new = spot[lane], p_old = sprev[lane];
+            rew[i] = loco_reward_total(tp, R[0], R[10], R[11], p_new, p_old, lt);
+            pot[i] = p_new;
+            prev[i] = p_old;
+            int64_t d = loco_done(tp, R[0], rb, progress);
+            if (nflag) {                                                // nan_guard
+                k->st.nan_flag[i] = 0;
+                atomicAdd(k->st.nan_total, 1ull);
+                d = 1;
+            }
+            reset_buf[i] = d;
+            progress_buf[i] = progress;
+        }
+        __syncthreads();
+        float* dst = obs + (size_t)e0 * O;
+        const int cnt = n * O;
+        if ((((uintptr_t)obs) & 15) == 0) {   // e0 * O * 4 B is a multiple of 128 B
+            const int n4 = cnt >> 2;
+            for (int kk = lane; kk < n4; kk += 64)
+                reinterpret_cast<float4*>(dst)[kk] = reinterpret_cast<const float4*>(sobs)[kk];
+            for (int kk = 4 * n4 + lane; kk < cnt; kk += 64) dst[kk] = sobs[kk];
+        } else {
+            for (int kk = lane; kk < cnt; kk += 64) dst[kk] = sobs[kk];
+        }
+        __syncthreads();                    // the next tile overwrites the LDS tiles
+    }
+#undef MI_PIPE_ISSUE
 }
 
 template <class T>
@@ -1409,30 +1433,40 @@ int mi_task_post_step(mi_sim* s, const float* actions, float* obs, float* rew, i
     HIP_TRY(hipSetDevice(s->device));
     int var = post_tile_variant();
     if (var == 4) {   // 32p: several tiles per resident workgroup, next tile's loads in flight
-        const size_t tile = post_tile_lds(32, true, s->ds.es, s->tp.A, s->tp.O, s->dm.D, s->dm.S) +
-                            2 * 32 * sizeof(float);
         const int es = s->ds.es;
-        if (s->tp.kind != MI_TASK_CARTPOLE && s->ds.fs == 1 && es % 4 == 0 && es <= 128 &&
-            s->tp.A >= 1 && s->tp.A <= 32 && s->dm.D >= 1 && s->dm.D <= 64 && 6 * s->dm.S <= 64 &&
-            tile <= 64 * 1024) {
+        const size_t tile = post_pipe_lds(es, s->tp.A, s->tp.O, s->dm.D);
+        if (s->tp.kind != MI_TASK_CARTPOLE && s->wave && s->kp_dev && s->ds.fs == 1 && es % 32 == 0 &&
+            es >= 32 && es <= 128 && s->tp.A >= 1 && s->tp.A <= 32 && s->dm.D >= 1 && s->dm.D <= 64 &&
+            6 * s->dm.S <= 64 && tile <= 64 * 1024) {
             if (s->num_cu <= 0)
                 HIP_TRY(hipDeviceGetAttribute(&s->num_cu, hipDeviceAttributeMultiprocessorCount, s->device));
             const int ntiles = (s->N + 31) / 32;
+            const void* fn = es == 32 ? (const void*)k_loco_post_pipe<4>
+                           : es == 64 ? (const void*)k_loco_post_pipe<8>
+                           : es == 96 ? (const void*)k_loco_post_pipe<12>
+                                      : (const void*)k_loco_post_pipe<16>;
             // one resident round: workgroups per CU as registers and LDS allow together
             int per_cu = 0;
-            HIP_TRY(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k_loco_post_pipe, 64, tile));
+            HIP_TRY(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, fn, 64, tile));
             int grid = std::min(ntiles, s->num_cu * std::max(1, per_cu));
             const char* g = getenv("MI_POST_GRID");
             if (g) grid = std::max(1, std::min(grid, atoi(g)));
             // with one tile per resident workgroup there is nothing to overlap: the one-tile
-            // kernel (67 VGPRs vs 253). Measured crossover (fuse_roofline, MI_POST_PIPE_MIN):
-            // Humanoid 131 K envs 0.039 vs 0.044 ms, 262 K 2.94 vs 2.49 TB/s piped vs one-tile.
+            // kernel. Crossover: MI_POST_PIPE_MIN tiles per workgroup (default 2).
             const char* pm = getenv("MI_POST_PIPE_MIN");   // tiles per workgroup (tuning)
             if (!g && ntiles < (pm ? atoi(pm) : 2) * grid) goto one_tile;
-            hipLaunchKernelGGL(k_loco_post_pipe, dim3(grid), dim3(64), tile, STREAM(stream), s->dm,
-                               s->ds, s->tp, actions, obs, rew, reset_buf, progress_buf, potentials,
-                               prev_potentials);
+            const KParams* kp = (const KParams*)s->kp_dev;
+#define POST_PIPE(R) hipLaunchKernelGGL(k_loco_post_pipe<R>, dim3(grid), dim3(64), tile, STREAM(stream), kp, \
+            actions, obs, rew, reset_buf, progress_buf, potentials, prev_potentials)
+            switch (es) {
+                case 32: POST_PIPE(4); break;
+                case 64: POST_PIPE(8); break;
+                case 96: POST_PIPE(12); break;
+                default: POST_PIPE(16); break;
+            }
+#undef POST_PIPE
             LAUNCH_CHECK();
+            s->post_kernel = 4; s->post_grid = grid;
             return MI_OK;
         }
     one_tile:
@@ -1452,11 +1486,21 @@ int mi_task_post_step(mi_sim* s, const float* actions, float* obs, float* rew, i
             default: POST_TILED(32, false); break;
         }
 #undef POST_TILED
-    } else
+        s->post_kernel = var; s->post_grid = (int)g.x;
+    } else {
         hipLaunchKernelGGL(k_post_step, grid_for(s, s->N), dim3(s->block), 0, STREAM(stream), s->dm,
                            s->ds, s->tp, actions, obs, rew, reset_buf, progress_buf, potentials,
                            prev_potentials);
+        s->post_kernel = 5; s->post_grid = (int)grid_for(s, s->N).x;
+    }
     LAUNCH_CHECK();
+    return MI_OK;
+}
+
+int mi_task_post_kernel(const mi_sim* s, int32_t* kernel, int32_t* grid) {
+    NEED(s);
+    if (kernel) *kernel = s->post_kernel;
+    if (grid) *grid = s->post_grid;
     return MI_OK;
 }
 

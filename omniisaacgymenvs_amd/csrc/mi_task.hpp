@@ -335,6 +335,102 @@ MI_D int64_t loco_done(const DevTask& tp, float obs0, int64_t reset, int64_t pro
     return r;
 }
 
+// The root-frame block and the reward sums of a 32-env tile on all 64 lanes of a wave (the
+// obs/reward fuse k_loco_post_pipe): lanes e and e + 32 both hold env e. Every value is the
+// same operation sequence as loco_obs_root / loco_reward_terms (bit-identical results); only
+// the assignment of the costly chains to lanes differs:
+//  - get_euler_xyz's roll (lower half) and yaw (upper half) run as ONE instruction stream
+//    (atan2 -> fmod -> normalize_angle on a per-lane selection of the inputs), then the target
+//    angle on every lane with env e's yaw from the upper half (ds_bpermute);
+//  - the energy sum (lower half) and the action cost (upper half) run as one loop of
+//    |x_j y_j| w_j: with x = y = a, w = 1 it is a_j a_j exactly (a square is >= 0; * 1 exact).
+// rec: env e's record in LDS (pos 3, quat 4, vel 6); writes obs[0..11] of orow (obs[7] from the
+// upper half) and potentials / prev_potentials of env e when `write`.
+MI_D void loco_obs_root_pair(const float* rec, const DevTask& tp, int lane, float* orow,
+                             float* potentials, float* prev_potentials, bool write) {
+#pragma clang fp contract(off)
+    const int e = lane & 31;
+    const bool hi = lane >= 32;
+    float rp[3], rq[4], rv[6];
+#pragma unroll
+    for (int k = 0; k < 3; ++k) rp[k] = rec[k];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) rq[k] = rec[3 + k];
+#pragma unroll
+    for (int k = 0; k < 6; ++k) rv[k] = rec[7 + k];
+    float tt[3] = {tp.target[0] - rp[0], tp.target[1] - rp[1], tp.target[2] - rp[2]};
+    tt[2] = 0.0f;
+    const float prev_p = potentials[e];
+    const float nrm = sqrtf(tt[0] * tt[0] + tt[1] * tt[1] + tt[2] * tt[2]);
+    const float new_p = -nrm / tp.task_dt;
+    const float inv_start[4] = {1.0f, -0.0f, -0.0f, -0.0f};
+    float tq[4];
+    ref_quat_mul(rq, inv_start, tq);
+    const float b0[3] = {1.0f, 0.0f, 0.0f}, b1[3] = {0.0f, 0.0f, 1.0f};
+    float up[3], hd[3];
+    ref_quat_rotate<false>(tq, b1, up);
+    ref_quat_rotate<false>(tq, b0, hd);
+    float tn = sqrtf(tt[0] * tt[0] + tt[1] * tt[1] + tt[2] * tt[2]);
+    tn = tn > 1e-9f ? tn : 1e-9f;
+    const float td[3] = {tt[0] / tn, tt[1] / tn, tt[2] / tn};
+    const float heading_proj = hd[0] * td[0] + hd[1] * td[1] + hd[2] * td[2];
+    float vl[3], al[3];
+    ref_quat_rotate<true>(tq, rv, vl);
+    ref_quat_rotate<true>(tq, rv + 3, al);
+    // ref_get_euler_xyz: roll on the lower half, yaw on the upper half
+    const float two_pi = 6.283185307179586f;
+    const float w = tq[0], x = tq[1], y = tq[2], z = tq[3];
+    const float sinr = 2.0f * (w * x + y * z);
+    const float cosr = w * w - x * x - y * y + z * z;
+    const float siny = 2.0f * (w * z + x * y);
+    const float cosy = w * w + x * x - y * y - z * z;
+    const float ang = ref_fmod_pos(atan2f(hi ? siny : sinr, hi ? cosy : cosr), two_pi);
+    const float nang = ref_normalize_angle(ang);                  // obs[8] roll / obs[7] yaw
+    const float yaw = __shfl(ang, e + 32);
+    const float walk = atan2f(tp.target[2] - rp[2], tp.target[0] - rp[0]);
+    const float n_target = ref_normalize_angle(walk - yaw);
+    if (!write) return;
+    if (hi) {
+        orow[7] = nang;
+        return;
+    }
+    orow[0] = rp[2];
+    orow[1] = vl[0]; orow[2] = vl[1]; orow[3] = vl[2];
+    orow[4] = al[0] * tp.angular_velocity_scale;
+    orow[5] = al[1] * tp.angular_velocity_scale;
+    orow[6] = al[2] * tp.angular_velocity_scale;
+    orow[8] = nang;
+    orow[9] = n_target;
+    orow[10] = up[2];
+    orow[11] = heading_proj;
+    potentials[e] = new_p;
+    prev_potentials[e] = prev_p;
+}
+// loco_reward_terms on lane pairs (see above): valid on the lower half
+MI_D LocoTerms loco_reward_terms_pair(const DevTask& tp, int D, const float* orow, const float* act,
+                                      int lane) {
+#pragma clang fp contract(off)
+    const bool hi = lane >= 32;
+    LocoTerms r{0.0f, 0.0f, 0.0f};
+    if (tp.kind == MI_TASK_HUMANOID) {
+        for (int j = 0; j < D; ++j) {
+            const float a = fabsf(orow[12 + j]);
+            const float sc = tp.joints_at_limit_cost * (a - 0.98f) / 0.02f;
+            r.limit_cost += (a > 0.98f ? 1.0f : 0.0f) * sc * tp.ratio[j];
+        }
+    } else {
+        int64_t cnt = 0;
+        for (int j = 0; j < D; ++j) cnt += orow[12 + j] > 0.99f;
+        r.limit_cost = (float)cnt;
+    }
+    const float* yv = hi ? act : orow + 12 + D;
+    float sum = 0.0f;
+    for (int j = 0; j < D; ++j) sum += fabsf(act[j] * yv[j]) * (hi ? 1.0f : tp.ratio[j]);
+    r.elec = sum;
+    r.act_cost = __shfl(sum, (lane & 31) + 32);
+    return r;
+}
+
 // NaN guard: a non-finite physics state forces a reset of that env
 MI_D int64_t nan_guard(const DevState& st, int i, int64_t done) {
     if (st.nan_flag[i]) {

@@ -112,6 +112,7 @@ _SIGS = {
     "mi_task_pre_step": (C.c_int, [C.c_void_p] + [C.c_void_p] * 7),
     "mi_task_reset_idx": (C.c_int, [C.c_void_p, C.c_void_p, C.c_int32] + [C.c_void_p] * 5),
     "mi_task_post_step": (C.c_int, [C.c_void_p] + [C.c_void_p] * 8),
+    "mi_task_post_kernel": (C.c_int, [C.c_void_p, _i32p, _i32p]),
     "mi_task_observations": (C.c_int, [C.c_void_p] + [C.c_void_p] * 5),
     "mi_task_metrics": (C.c_int, [C.c_void_p] + [C.c_void_p] * 6),
     "mi_task_is_done": (C.c_int, [C.c_void_p] + [C.c_void_p] * 4),

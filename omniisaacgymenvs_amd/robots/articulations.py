@@ -239,6 +239,15 @@ class ArticulationView:
                 "mi_sim_kernel_path")
         return int(p.value), int(t.value), int(b.value)
 
+    POST_KERNELS = {0: "k_loco_post_tiled<64s>", 1: "k_loco_post_tiled<64d>", 2: "k_loco_post_tiled<32s>",
+                    3: "k_loco_post_tiled<32d>", 4: "k_loco_post_pipe", 5: "k_post_step"}
+
+    def post_kernel(self) -> tuple:
+        """(kernel name, grid) of the last mi_task_post_step launch (None before the first)."""
+        k, g = C.c_int32(), C.c_int32()
+        N.check(N.lib().mi_task_post_kernel(self.handle, C.byref(k), C.byref(g)), "mi_task_post_kernel")
+        return self.POST_KERNELS.get(int(k.value)), int(g.value)
+
     def sim_topology(self) -> int:
         return self.sim_kernel_path()[1]
 

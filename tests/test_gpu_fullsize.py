@@ -139,6 +139,7 @@ def test_obs_reward_fuse_matches_oracle(gpu, name, n):
                                       t.progress_buf.data_ptr(), t.potentials.data_ptr(),
                                       t.prev_potentials.data_ptr(), view.stream()), "mi_task_post_step")
     torch.cuda.synchronize()
+    assert view.post_kernel()[0] == ("k_loco_post_pipe" if n >= 256 * 1024 else "k_loco_post_tiled<32s>")
     lim = t.model.dof_limits()
     from oracle import oracle as oracle_mod
     ref = oracle_mod.loco_post_math(t.task_params(), *state, acts, lim[:, 0], lim[:, 1],

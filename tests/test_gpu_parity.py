@@ -374,9 +374,59 @@ def test_pipelined_post_step_equals_one_tile(gpu, monkeypatch, name):
                                           t.prev_potentials.data_ptr(), s), "mi_task_post_step")
         torch.cuda.synchronize()
         out[(var, grid)] = {b: getattr(t, b).clone() for b in bufs}
+        kname, kgrid = t.get_robot().post_kernel()
+        # 129 tiles without MI_POST_GRID: under two tiles per resident workgroup, the one-tile kernel
+        assert kname == ("k_loco_post_pipe" if grid else "k_loco_post_tiled<32s>"), (var, grid, kname)
+        if grid:
+            assert kgrid == int(grid)
     ref = out[("32s", None)]
     assert not torch.equal(ref["obs_buf"], start["obs_buf"])
     for key in (("32p", "7"), ("32p", None)):
         for b in bufs:
             assert torch.equal(out[key][b], ref[b]), (key, b)
+    env.close()
+
+
+@pytest.mark.parametrize("var", ["32p", "32s"])
+def test_post_step_nan_guard(gpu, monkeypatch, var):
+    """The NaN guard inlined in the obs/reward fuse kernels (nan_guard: a non-finite physics state
+    forces a reset and counts it): poison the DOF state of a few envs, one physics
+    substep sets their nan_flag, one mi_task_post_step must reset exactly those envs (plus the
+    ones is_done resets anyway) and count each once; the flags are cleared."""
+    env = make_env("Humanoid", num_envs=4113, device="cuda:0", seed=5)
+    t, view = env.task, env.task.get_robot()
+    env.reset()
+    env.step(rand_actions(t.num_envs, t.num_actions, 60).to("cuda:0"))
+    monkeypatch.setenv("MI_POST_TILE", var)
+    if var == "32p":
+        monkeypatch.setenv("MI_POST_GRID", "7")
+    bad = torch.tensor([0, 31, 32, 1000, 4112], device="cuda:0", dtype=torch.int64)
+    q = view.get_joint_positions()[bad].clone()
+    q[:, 3] = float("nan")
+    view.set_joint_positions(q, indices=bad)
+    env._world.step()
+    torch.cuda.synchronize()
+    t.progress_buf.zero_()
+    t.reset_buf.zero_()
+    n0 = view.nan_count()
+    N.check(N.lib().mi_task_post_step(view.handle, t.actions.data_ptr(), t.obs_buf.data_ptr(),
+                                      t.rew_buf.data_ptr(), t.reset_buf.data_ptr(),
+                                      t.progress_buf.data_ptr(), t.potentials.data_ptr(),
+                                      t.prev_potentials.data_ptr(), view.stream()), "mi_task_post_step")
+    torch.cuda.synchronize()
+    assert view.post_kernel()[0] == ("k_loco_post_pipe" if var == "32p" else "k_loco_post_tiled<32s>")
+    assert view.nan_count() - n0 == len(bad)
+    assert (t.reset_buf[bad] == 1).all()
+    ok = torch.ones(t.num_envs, dtype=torch.bool, device="cuda:0")
+    ok[bad] = False
+    # the others reset only where is_done says so (obs[:, 0] = height below the threshold)
+    height_reset = t.obs_buf[:, 0] < t.termination_height
+    assert torch.equal(t.reset_buf[ok].bool(), height_reset[ok])
+    # flags were cleared: a second launch counts nothing new for the poisoned envs' flags
+    N.check(N.lib().mi_task_post_step(view.handle, t.actions.data_ptr(), t.obs_buf.data_ptr(),
+                                      t.rew_buf.data_ptr(), t.reset_buf.data_ptr(),
+                                      t.progress_buf.data_ptr(), t.potentials.data_ptr(),
+                                      t.prev_potentials.data_ptr(), view.stream()), "mi_task_post_step")
+    torch.cuda.synchronize()
+    assert view.nan_count() - n0 == len(bad)
     env.close()
