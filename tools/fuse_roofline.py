@@ -57,9 +57,10 @@ def measure(task_name: str, n: int, launches: int = 30, env=None) -> dict:
     ms = sum(a.elapsed_time(b) for a, b in ev) / launches
     B = fuse_bytes(t)
     gbs = B * n / (ms * 1e-3) / 1e9
+    label = t.get_robot().post_kernel()[0] or kernel_label(n)   # what mi_task_post_step launched
     if own:
         env.close()
-    return {"kernel": kernel_label(n), "task": task_name, "num_envs": n, "kernel_ms": round(ms, 4),
+    return {"kernel": label, "task": task_name, "num_envs": n, "kernel_ms": round(ms, 4),
             "algo_bytes_per_env": B, "achieved": round(gbs, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
             "frac": round(gbs / HBM_PEAK_GBS, 4)}
 

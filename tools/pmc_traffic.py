@@ -51,6 +51,9 @@ def main():
         "fetch_kib_raw": round(fkb, 1), "write_kib_raw": round(wkb, 1),
         "read_bytes_corrected": round(2 * fkb * 1024), "write_bytes": round(wkb * 1024),
         "bytes_per_launch": round(2 * fkb * 1024 + wkb * 1024),
+        # lower estimate: FETCH_SIZE as reported (the x2 correction is calibrated for 16-B-per-lane
+        # streaming reads; narrower per-lane reads are uncalibrated, MI355X_MICROARCH.md HBM)
+        "bytes_per_launch_uncorrected": round(fkb * 1024 + wkb * 1024),
         "method": "rocprofv3 --pmc FETCH_SIZE / --pmc WRITE_SIZE in separate runs, --kernel-trace; "
                   "FETCH doubled per the gfx950 correction; warm-up quarter dropped",
     }
