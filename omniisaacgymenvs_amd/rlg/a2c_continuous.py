@@ -44,6 +44,7 @@ from typing import Dict, Optional
 
 import numpy as np
 import torch
+import torch.distributed as dist
 import torch.nn as nn
 
 from . import ops
@@ -146,7 +147,17 @@ class A2CAgent:
         self.actions_high = torch.as_tensor(np.asarray(info["action_space"].high, np.float32), device=self.device)
         self.num_actors = int(cfg["num_actors"])
         self.horizon = int(cfg["horizon_length"])
-        self.batch_size = self.horizon * self.num_actors
+        # multi-GPU (multi_gpu: True under torch.distributed.run): one process per
+        # GPU steps its env shard with a policy replica; every horizon is gathered to the learner
+        # (rank 0) in ONE collective (utils.distributed.RolloutGather), the learner trains on all
+        # ranks' actors and broadcasts the weights back. (rl_games' multi_gpu runs a learner per
+        # rank and averages gradients instead; here each rollout crosses xGMI once and there is
+        # one optimizer.) num_actors stays the per-rank count, batch_size is the learner's.
+        self.world = (dist.get_world_size() if bool(cfg.get("multi_gpu", False)) and dist.is_available()
+                      and dist.is_initialized() else 1)
+        self.rank = dist.get_rank() if self.world > 1 else 0
+        self.is_learner = self.rank == 0
+        self.batch_size = self.horizon * self.num_actors * self.world
         self.minibatch_size = int(cfg["minibatch_size"])
         if self.batch_size % self.minibatch_size != 0:
             raise ValueError(f"minibatch_size {self.minibatch_size} must divide horizon x actors = "
@@ -203,21 +214,35 @@ class A2CAgent:
                            and self.model.a2c_network.fixed_sigma)
         # split-K weight gradients of the minibatch GEMMs (models.linear_train); 1 = one GEMM
         self.wgrad_splits = int(cfg.get("wgrad_splits", 32))
-        self.sample_gen = torch.Generator(device="cpu").manual_seed(self.seed)
-        self.sample_seed = (self.seed * 0x9E3779B97F4A7C15 + 1) & ((1 << 64) - 1)
+        # action-noise streams: one per rank (replicas must not share exploration noise)
+        self.sample_gen = torch.Generator(device="cpu").manual_seed(self.seed + 7919 * self.rank)
+        self.sample_seed = ((self.seed * 0x9E3779B97F4A7C15 + 1) ^ (self.rank * 0xD1B54A32D192ED03)) & ((1 << 64) - 1)
 
         H, N, O, A = self.horizon, self.num_actors, self.num_obs, self.num_actions
         dev, f32 = self.device, torch.float32
-        self.buf = {
-            "obses": torch.zeros((H, N, O), device=dev, dtype=f32),
-            "dones": torch.zeros((H, N), device=dev, dtype=f32),
-            "actions": torch.zeros((H, N, A), device=dev, dtype=f32),
-            "neglogpacs": torch.zeros((H, N), device=dev, dtype=f32),
-            "values": torch.zeros((H, N), device=dev, dtype=f32),
-            "mus": torch.zeros((H, N, A), device=dev, dtype=f32),
-            "sigmas": torch.zeros((H, N, A), device=dev, dtype=f32),
-            "rewards": torch.zeros((H, N), device=dev, dtype=f32),
-        }
+        self.rollout = None
+        if self.world > 1:
+            # the rollout buffers ARE the gather slab's fields (zero copy; one slab, so the
+            # captured rollout graph keeps writing the same addresses)
+            from ..utils.distributed import RolloutGather
+            self.rollout = RolloutGather(H, N, O, dev, self.world, buffers=1, mode="gather", dst=0,
+                                         extra=self._SLAB_EXTRA(A))
+            v = self.rollout.slabs[0].views
+            self.buf = {"obses": v["obs"], "rewards": v["rew"], "dones": v["dones_f"],
+                        "actions": v["actions"].view(H, N, A), "neglogpacs": v["neglogpacs"],
+                        "values": v["values"], "mus": v["mus"].view(H, N, A),
+                        "sigmas": v["sigmas"].view(H, N, A)}
+        else:
+            self.buf = {
+                "obses": torch.zeros((H, N, O), device=dev, dtype=f32),
+                "dones": torch.zeros((H, N), device=dev, dtype=f32),
+                "actions": torch.zeros((H, N, A), device=dev, dtype=f32),
+                "neglogpacs": torch.zeros((H, N), device=dev, dtype=f32),
+                "values": torch.zeros((H, N), device=dev, dtype=f32),
+                "mus": torch.zeros((H, N, A), device=dev, dtype=f32),
+                "sigmas": torch.zeros((H, N, A), device=dev, dtype=f32),
+                "rewards": torch.zeros((H, N), device=dev, dtype=f32),
+            }
         self.obs = torch.zeros((N, O), device=dev, dtype=f32)      # static rollout input
         self.dones = torch.zeros((N,), device=dev, dtype=f32)
         self.last_values = torch.zeros((N,), device=dev, dtype=f32)
@@ -237,8 +262,44 @@ class A2CAgent:
         self._mb_stats = torch.zeros((self.mini_epochs, self.num_minibatches, 5), device=dev, dtype=f32)
         self.epoch_num = 0
         self.frame = 0
+        if self.world > 1:
+            self._broadcast_weights()   # every replica starts from the learner's initial weights
         self.last_mean_rewards = -100500.0
         self.stats: Dict[str, float] = {}
+
+    @staticmethod
+    def _SLAB_EXTRA(A: int):
+        f32 = torch.float32
+        return [("dones_f", 1, f32), ("actions", A, f32), ("neglogpacs", 1, f32), ("values", 1, f32),
+                ("mus", A, f32), ("sigmas", A, f32)]
+
+    # ------------------------------------------------------------------ multi-GPU
+    def _gather_horizon(self):
+        """The horizon's rollout slab to the learner in one gather, plus the bootstrap values /
+        final dones [2, N] per rank; episode statistics summed over ranks. Returns the learner's
+        global (buffers, last_values, dones) in global actor order (rank-major), else None."""
+        g = self.rollout
+        g.gather(async_op=False)
+        tail = torch.stack([self.last_values, self.dones])
+        lst = [torch.empty_like(tail) for _ in range(self.world)] if self.is_learner else None
+        dist.gather(tail, gather_list=lst, dst=0)
+        dist.all_reduce(self.episode_sums)
+        if not self.is_learner:
+            return None
+        H, A = self.horizon, self.num_actions
+        names = {"obses": "obs", "rewards": "rew", "dones": "dones_f", "actions": "actions",
+                 "neglogpacs": "neglogpacs", "values": "values", "mus": "mus", "sigmas": "sigmas"}
+        b = {k: g.global_field(f) for k, f in names.items()}
+        for k in ("actions", "mus", "sigmas"):
+            b[k] = b[k].reshape(H, -1, A)
+        tails = torch.stack(lst)                     # [world, 2, N]
+        return b, tails[:, 0].reshape(-1), tails[:, 1].reshape(-1)
+
+    def _broadcast_weights(self) -> None:
+        """The learner's parameters and statistics buffers to every policy replica, in place (the
+        captured rollout graphs read them by address)."""
+        for t in self.model.state_dict().values():
+            dist.broadcast(t, src=0)
 
     # ------------------------------------------------------------------ env plumbing
     def _obs_tensor(self, obs) -> torch.Tensor:
@@ -312,6 +373,7 @@ class A2CAgent:
                 self.graph.replay()
             else:
                 self._rollout_body()
+        self._global = self._gather_horizon() if self.world > 1 else None
         ep = self.episode_sums.cpu().numpy()           # the rollout's one host sync
         for cnt, rsum, lsum in ep:
             if cnt > 0:
@@ -334,8 +396,10 @@ class A2CAgent:
 
     # ------------------------------------------------------------------ training
     def prepare_dataset(self) -> Dict[str, torch.Tensor]:
-        b = self.buf
-        adv, ret = ops.gae(b["rewards"], b["values"], b["dones"], self.last_values, self.dones,
+        b, last_values, dones = self.buf, self.last_values, self.dones
+        if self.world > 1:             # the learner: every rank's actors, gathered
+            b, last_values, dones = self._global
+        adv, ret = ops.gae(b["rewards"], b["values"], b["dones"], last_values, dones,
                            self.gamma, self.tau)
         values = swap_and_flatten01(b["values"]).unsqueeze(1)
         returns = swap_and_flatten01(ret).unsqueeze(1)
@@ -470,6 +534,17 @@ class A2CAgent:
         self.epoch_num += 1
         play_time = self.play_steps()
         t0 = time.perf_counter()
+        if not self.is_learner:        # a policy replica: wait for the learner's weights
+            self._broadcast_weights()
+            self.frame += self.batch_size
+            st = {"epoch": self.epoch_num, "frames": self.frame, "play_time": play_time,
+                  "update_time": time.perf_counter() - t0,
+                  "fps_step_inference": self.batch_size / play_time,
+                  "fps_total": self.batch_size / (play_time + time.perf_counter() - t0),
+                  "mean_rewards": self.game_rewards.get_mean(),
+                  "mean_lengths": self.game_lengths.get_mean(), "games": self.game_rewards.current_size}
+            self.stats = st
+            return st
         self.model.train()
         data = self.prepare_dataset()
         if self.device.type == "cuda":
@@ -509,6 +584,8 @@ class A2CAgent:
             a_loss_m, c_loss_m = torch.stack(a_l).mean().item(), torch.stack(c_l).mean().item()
             b_loss_m, ent_m = torch.stack(b_l).mean().item(), torch.stack(ents).mean().item()
             kl_m = torch.stack(kls).mean().item()
+        if self.world > 1:
+            self._broadcast_weights()
         update_time = time.perf_counter() - t0
         self.frame += self.batch_size
         st = {
@@ -535,12 +612,13 @@ class A2CAgent:
                     f"{st['fps_total']:.0f} epoch: {st['epoch']}/{max_epochs} "
                     f"mean reward: {st['mean_rewards']:.3f} mean length: {st['mean_lengths']:.1f}")
             mean_rewards = st["mean_rewards"]
-            if self.save_frequency > 0 and self.epoch_num % self.save_frequency == 0:
+            if self.is_learner and self.save_frequency > 0 and self.epoch_num % self.save_frequency == 0:
                 self.save(os.path.join(self.run_dir, "nn", f"last_{self.name}_ep_{self.epoch_num}"))
             if (self.game_rewards.current_size > 0 and mean_rewards > self.last_mean_rewards
                     and self.epoch_num >= self.save_best_after):
                 self.last_mean_rewards = mean_rewards
-                self.save(os.path.join(self.run_dir, "nn", str(self.name)))
+                if self.is_learner:
+                    self.save(os.path.join(self.run_dir, "nn", str(self.name)))
                 if mean_rewards > self.score_to_win:
                     break
         return st

@@ -1,0 +1,86 @@
+"""Multi-GPU PPO on CPU (world_size-2 gloo): each rank steps its own env shard with a policy
+replica, the horizon is gathered to the learner (rank 0) in one collective, the learner trains on
+every rank's actors and broadcasts the weights back (rlg.a2c_continuous with multi_gpu: True;
+SURVEY §8e "single RCCL gather ... for the rollout buffer"). The env is the oracle-backed Cartpole
+test twin (test infrastructure: the product refuses CPU)."""
+import os
+
+import numpy as np
+import torch
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+from tests.test_cartpole_cpu_rollout import N_ENVS
+
+EPOCHS = 2
+
+
+def _worker(rank, world, port, q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    from omniisaacgymenvs_amd.rlg.a2c_continuous import A2CAgent
+    from omniisaacgymenvs_amd.utils.rlgames.rlgames_utils import RLGPUEnv, register_env
+    from tests.test_cartpole_cpu_rollout import OracleCartpoleVecEnv
+    from tests.test_rl_cpu import _cartpole_cpu_params
+
+    register_env(f"rlgpu_mg{rank}", lambda **kw: OracleCartpoleVecEnv(seed=100 + rank))
+    params = _cartpole_cpu_params()
+    params["config"]["multi_gpu"] = True
+    agent = A2CAgent(RLGPUEnv(f"rlgpu_mg{rank}", N_ENVS), params, run_dir=f"/tmp/mg_{port}_{rank}")
+    res = {"world": agent.world, "batch": agent.batch_size, "minibatches": agent.num_minibatches}
+    agent.env_reset()
+    for _ in range(EPOCHS):
+        st = agent.train_epoch()
+        # this rank's local horizon as it sat in the gathered slab (learner: compared below)
+        local = {k: agent.buf[k].clone() for k in ("obses", "actions", "neglogpacs", "rewards", "dones")}
+        gathered = {k: [torch.empty_like(v) for _ in range(world)] for k, v in local.items()}
+        for k, v in local.items():
+            dist.all_gather(gathered[k], v)
+        if rank == 0:
+            data = agent._data
+            H, N = agent.horizon, agent.num_actors
+            want = {k: torch.cat(gathered[k], dim=1) for k in gathered}   # [H, world * N, ...]
+
+            def flat(x):   # swap_and_flatten01: actor-major rows
+                return x.transpose(0, 1).reshape((H * world * N,) + tuple(x.shape[2:]))
+            assert torch.equal(data["obs"], flat(want["obses"]))
+            assert torch.equal(data["actions"], flat(want["actions"]))
+            assert torch.equal(data["old_logp_actions"], flat(want["neglogpacs"]))
+    state = torch.cat([t.detach().float().reshape(-1) for t in agent.model.state_dict().values()])
+    allst = [torch.empty_like(state) for _ in range(world)]
+    dist.all_gather(allst, state)
+    res["replicas_equal"] = all(torch.equal(allst[0], x) for x in allst[1:])
+    res["games"] = st["games"]
+    res["frames"] = st["frames"]
+    # distinct exploration noise per rank: the two shards' action rows differ
+    res["noise_differs"] = not torch.equal(gathered["actions"][0], gathered["actions"][1])
+    q.put((rank, res))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def test_two_rank_central_learner():
+    world = 2
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    import socket
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    procs = [ctx.Process(target=_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    out = dict(q.get(timeout=300) for _ in range(world))
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    for r in range(world):
+        res = out[r]
+        assert res["world"] == 2
+        assert res["batch"] == 16 * N_ENVS * world          # the learner's batch: both shards
+        assert res["minibatches"] == 2 * 4                  # minibatch 64: twice the single-rank count
+        assert res["replicas_equal"]                         # weights broadcast after every update
+        assert res["frames"] == EPOCHS * res["batch"]
+        assert res["noise_differs"]
+    assert out[0]["games"] == out[1]["games"]               # episode statistics summed over ranks
+    assert np.isfinite(out[0]["games"])
