@@ -178,6 +178,32 @@ def cpu_baseline(task_name: str, env, seconds: float) -> dict:
         results[threads] = (statistics.median(runs), steps)
         orc.close()
     v1, steps1 = results[1]
+    # BASELINE config 1 (Cartpole, 16 envs, CPU): small enough for BASELINE.md's full protocol
+    # (200 warm-up, 2000 timed env-steps, median of 5), 1 thread
+    orc_lib().orc_set_threads(1)
+    c1 = None
+    try:
+        from omniisaacgymenvs_amd.robots.articulations import GridCloner
+        from tests.helpers import sim_params, task_params_from_cfg
+        tp1, m1, _ = task_params_from_cfg("Cartpole")
+        orc = OracleSim(m1, sim_params(rest_offset=0.001), 16, GridCloner(4.0).get_clone_positions(16), seed=42)
+        orc.configure(tp1)
+        b1 = make_buffers(16, tp1.num_obs, tp1.num_actions)
+        a1 = rng.uniform(-1, 1, (8, 16, tp1.num_actions)).astype(np.float32)
+        for k in range(200):
+            orc.env_step(a1[k % 8], 2, b1)
+        runs = []
+        for _ in range(5):
+            t0 = time.perf_counter()
+            for k in range(2000):
+                orc.env_step(a1[k % 8], 2, b1)
+            runs.append(16 * 2000 / (time.perf_counter() - t0))
+        orc.close()
+        c1 = {"value": round(statistics.median(runs), 1), "unit": "env-steps/s", "cores": 1,
+              "sample": "Cartpole 16 envs, 200 warm-up + median of 5 x 2000 env-steps (BASELINE.md protocol), "
+                        "oracle fused step (2 substeps)"}
+    except Exception as e:   # noqa: BLE001 - the side leg must not sink the bench line
+        c1 = {"error": str(e)}
     return {
         "value": round(v1, 1), "unit": "env-steps/s", "cores": 1, "kind": "port",
         "sample": f"{task_name} {n} envs, {warm} warm-up + median of 3 x {steps1} env-steps, 1 thread; "
@@ -185,6 +211,7 @@ def cpu_baseline(task_name: str, env, seconds: float) -> dict:
                   f"Cholesky articulated step (device: tree LTDL), same contacts / limits / PGS and task "
                   f"math. Protocol: bounded sample, not BASELINE.md's 200 / 2000 / median-of-5",
         "threads_sweep": {str(t): round(v[0], 1) for t, v in results.items()},
+        "config1_cartpole16": c1,
     }
 
 

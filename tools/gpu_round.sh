@@ -11,4 +11,5 @@ run fuse_a 300 python -u tools/fuse_roofline.py Ant 4096,65536,131072,262144,104
 cp gpurun_out/fuse_roofline_ant.json gpurun_out/sweep_fuse_ant.json
 run prof_fuse 300 $RP --kernel-trace --stats -d gpurun_out/prof_fuse -o run -- python3 tools/fuse_roofline.py Humanoid 1048576 20
 run bench_default 500 python -u bench.py
+run prof_bench 500 $RP --kernel-trace --stats -d gpurun_out/prof_bench -o run -- python3 bench.py
 echo ALL_DONE
