@@ -35,6 +35,7 @@ class VecEnvRLGames:
         self._world: Optional[World] = None
         self._fused = False
         self._ev_i = 0
+        self._states = None
         self.kernel_events = None  # (start_events, end_events) bracketing each fused launch
 
     # ------------------------------------------------------------------ setup
@@ -114,7 +115,12 @@ class VecEnvRLGames:
             self._rew = rew if rl == str(rew.device) else rew.to(t.rl_device)
             self._resets = resets if rl == str(resets.device) else resets.to(t.rl_device)
             self._extras = t.extras.copy()
-            self._states = torch.clamp(t.get_states(), -t.clip_obs, t.clip_obs).to(t.rl_device).clone()
+            st = t.get_states()
+            if st.numel() == 0:       # no state space (Humanoid / Ant / Cartpole): nothing to clamp
+                if self._states is None or self._states.shape != st.shape or str(self._states.device) != str(t.rl_device):
+                    self._states = st.to(t.rl_device).clone()
+            else:
+                self._states = torch.clamp(st, -t.clip_obs, t.clip_obs).to(t.rl_device).clone()
             return {"obs": self._obs, "states": self._states}, self._rew, self._resets, self._extras
         actions = torch.clamp(actions, -t.clip_actions, t.clip_actions).to(t.device).clone()
         if t.randomize_actions:
