@@ -272,11 +272,30 @@ def side_run(task_name: str, n: int, steps: int = 200, warmup: int = 30) -> dict
     env.kernel_events = None
     kms = sum(s.elapsed_time(e) for s, e in zip(starts, ends)) / steps
     ach = ALGO_BYTES[task_name] * n / (kms * 1e-3) / 1e9
+    # the same steps replayed from a captured HIP graph (as the PPO rollout runs them,
+    # rlg/a2c_continuous.py graph_rollout): no per-step Python / launch overhead
+    G = len(actions)
+    graph = torch.cuda.CUDAGraph()
+    torch.cuda.synchronize()
+    with torch.cuda.graph(graph):
+        for k in range(G):
+            env.step(actions[k])
+    for _ in range(2):
+        graph.replay()
+    reps = max(1, steps // G)
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(reps):
+        graph.replay()
+    torch.cuda.synchronize()
+    el_g = time.perf_counter() - t0
     out = {"workload": f"{task_name} {n} envs, fused env step", "kernel": kernel_name(view, task),
            "value": round(n * steps / el, 1), "unit": "env-steps/s", "ms_per_step": round(el / steps * 1e3, 4),
            "kernel_ms": round(kms, 4), "achieved": round(ach, 3), "unit_bw": "GB/s",
            "frac": round(ach / HBM_PEAK_GBS, 6), "algo_bytes_per_env": ALGO_BYTES[task_name],
-           "lds_bytes_per_env": view.sim_kernel_path()[2], "nan_resets": view.nan_count()}
+           "lds_bytes_per_env": view.sim_kernel_path()[2], "nan_resets": view.nan_count(),
+           "graph_replay": {"value": round(n * reps * G / el_g, 1), "ms_per_step": round(el_g / (reps * G) * 1e3, 4),
+                            "steps": reps * G, "steps_per_graph": G}}
     env.close()
     return out
 
@@ -399,6 +418,26 @@ def main():
         }
         if gather_info:
             out["rollout_gather"] = gather_info
+    if not distributed and env.fused:
+        # the same workload replayed from a captured HIP graph (16 steps per graph, as the PPO
+        # rollout runs it): what the step costs without per-step Python / launch overhead
+        G = len(actions)
+        graph = torch.cuda.CUDAGraph()
+        sync()
+        with torch.cuda.graph(graph):
+            for k in range(G):
+                env.step(actions[k])
+        graph.replay()
+        reps = max(1, args.steps // G)
+        sync()
+        t0 = time.perf_counter()
+        for _ in range(reps):
+            graph.replay()
+        sync()
+        el_g = time.perf_counter() - t0
+        out["graph_replay"] = {"value": round(n_local * reps * G / el_g, 1),
+                               "ms_per_step": round(el_g / (reps * G) * 1e3, 4), "steps": reps * G,
+                               "note": "informational; `value` is the eager per-step loop"}
     if distributed:
         dist.barrier()
         dist.destroy_process_group()
