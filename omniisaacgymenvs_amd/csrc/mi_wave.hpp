@@ -999,31 +999,32 @@ MI_D void wave_artic_substep(const DevModel& m, const WaveTabs& t, const DevStat
         if constexpr (TP::kCT) {
             // solve vector built in place: J_r, e_kd or the rhs
             float x[TP::nvc];
-            if (on && r >= 0) {
-                // J_r = J_a^T f - J_b^T f (b: the second body of a self-contact, else none)
+            // J_r = J_a^T f - J_b^T f (b: the second body of a self-contact, else none). Built
+            // branch-free over the DOFs for every lane at once: S_c comes from wave-uniform LDS
+            // broadcasts, each lane selects its own entry (contact row, rhs or e_kd), so the
+            // contact lanes and the others no longer run as two serialised exec-masked halves
+            // with a divergent branch per DOF. Same operations per entry (last-bit rounding of
+            // the generated code differs; results agree to rounding, see the parity tests).
+            const bool crow = on && r >= 0;
+            float f[6] = {0.0f, 0.0f, 0.0f, 0.0f, 0.0f, 0.0f};
+            unsigned msk = 0u, msk2 = 0u;
+            if (crow) {
                 const int l = (int)sm[t.s_rl + r];
                 const float l2 = TP::kSelf ? sm[t.s_cl2 + r / 3] : -1.0f;
-                const unsigned msk = mc.mask(l), msk2 = l2 >= 0.0f ? mc.mask((int)l2) : 0u;
-                float f[6];
+                msk = mc.mask(l);
+                msk2 = l2 >= 0.0f ? mc.mask((int)l2) : 0u;
                 contact_row_f<TP::kSelf>(sm, t, r, f);
-                sfor<0, TP::nv>([&](auto C) {
-                    constexpr int c = C;
-                    const bool ia = (msk >> c) & 1u, ib = (msk2 >> c) & 1u;
-                    float v = 0.0f;
-                    if (ia || ib) {
-                        float sv[6];
-#pragma unroll
-                        for (int q = 0; q < 6; ++q) sv[q] = Ss[6 * c + q];
-                        v = dot6(sv, f);
-                    }
-                    x[c] = (ia ? v : 0.0f) - (ib ? v : 0.0f);
-                });
-            } else {
-                sfor<0, TP::nv>([&](auto C) {
-                    constexpr int c = C;
-                    x[c] = bv == 0 ? rhs[c] : (kd == c ? 1.0f : 0.0f);
-                });
             }
+            sfor<0, TP::nv>([&](auto C) {
+                constexpr int c = C;
+                float sv[6];
+#pragma unroll
+                for (int q = 0; q < 6; ++q) sv[q] = Ss[6 * c + q];
+                const float v = dot6(sv, f);
+                const bool ia = (msk >> c) & 1u, ib = (msk2 >> c) & 1u;
+                const float xc = (ia ? v : 0.0f) - (ib ? v : 0.0f);
+                x[c] = crow ? xc : (bv == 0 ? rhs[c] : (kd == c ? 1.0f : 0.0f));
+            });
             if (on && r >= 0 && r < t.j_rows_lds) {   // keep J_r for the PGS sweeps
                 float* jl = sm + t.s_J + r * TP::nv;
                 sfor<0, TP::nv>([&](auto C) { jl[C] = x[C]; });
@@ -1126,15 +1127,29 @@ MI_D void wave_artic_substep(const DevModel& m, const WaveTabs& t, const DevStat
             sfor<0, NV>([&](auto C) { Jr[C] = sJ[rl * NV + C]; });
             float v = 0.0f;
             sfor<0, NV>([&](auto C) { v += Jr[C] * us[C]; });
+            // Delassus row of lane r: A[r][s] = J_r . W_s. Four rows s per uniform branch, their
+            // dot products interleaved (four independent FMA chains instead of one per basic
+            // block); each chain keeps its sequential order (the generated code rounds a few
+            // entries differently in the last bit: results agree to rounding, see the parity
+            // tests). Rows past nrows in the last group re-read row nrows - 1 and are never used.
             float Ar[RMAX];
+            static_assert(RMAX % 4 == 0, "Delassus rows are built four at a time");
 #pragma unroll
-            for (int s2 = 0; s2 < RMAX; ++s2) {
-                float a = 0.0f;
-                if (s2 < nrows) {
-                    const float* w = w_row<TP::kSelf>(t, sm, s2, NV);
-                    sfor<0, NV>([&](auto C) { a += Jr[C] * w[C]; });
+            for (int g0 = 0; g0 < RMAX; g0 += 4) {
+                float a0 = 0.0f, a1 = 0.0f, a2 = 0.0f, a3 = 0.0f;
+                if (g0 < nrows) {
+                    const float* w0 = w_row<TP::kSelf>(t, sm, g0, NV);
+                    const float* w1 = w_row<TP::kSelf>(t, sm, min(g0 + 1, nrows - 1), NV);
+                    const float* w2 = w_row<TP::kSelf>(t, sm, min(g0 + 2, nrows - 1), NV);
+                    const float* w3 = w_row<TP::kSelf>(t, sm, min(g0 + 3, nrows - 1), NV);
+                    sfor<0, NV>([&](auto C) {
+                        a0 += Jr[C] * w0[C];
+                        a1 += Jr[C] * w1[C];
+                        a2 += Jr[C] * w2[C];
+                        a3 += Jr[C] * w3[C];
+                    });
                 }
-                Ar[s2] = a;
+                Ar[g0] = a0; Ar[g0 + 1] = a1; Ar[g0 + 2] = a2; Ar[g0 + 3] = a3;
             }
             const float mu = p.friction;
             for (int it = 0; it < p.iters; ++it) {
