@@ -280,7 +280,8 @@ MI_D void ct_load_columns(const float* Mx, int lane, float (&Mc)[T::nvc]) {
     sfor<0, T::nv>([&](auto R) {
         constexpr int r = R;
         constexpr unsigned long long keep = (unsigned long long)T::dof.anc_mask[r] | (1ull << r);
-        Mc[r] = ((keep >> lane_here(lane)) & 1ull) ? Mx[r * T::nv + c] : 0.0f;
+        const float v = Mx[r * T::nv + c];   // loaded by every lane, then selected: no branch
+        Mc[r] = ((keep >> lane_here(lane)) & 1ull) ? v : 0.0f;
     });
 }
 
@@ -646,22 +647,22 @@ MI_D void wave_artic_substep(const DevModel& m, const WaveTabs& t, const DevStat
             diag += mc.lf(MC_ARM, l) + dt * damp;
             r += st.eff[sx(st, k - nr, i)] - damp * us[k];
         }
-        Mx[k * nv + k] = diag;
         rhs[k] = r;
         if constexpr (TP::kCT) {
-            // ancestors of k from the link's DOF mask (root DOFs: the root chain below k);
-            // uniform j: the S_j reads are LDS broadcasts
-            const unsigned am = k < nr ? (1u << k) - 1u : mc.mask(l) & ~(1u << k);
+            // row k of M~: S_j . f for every j, branch-free (uniform j: the S_j reads are LDS
+            // broadcasts). Only the ancestors of k are ever read (ct_load_columns masks the
+            // rest), so the other entries are written but dead; a lane-varying ancestor branch
+            // per j cost more than the 6 FMAs it skipped. The diagonal goes last.
             sfor<0, TP::nv>([&](auto J) {
                 constexpr int j = J;
-                if ((am >> j) & 1u) {
-                    float sj[6];
+                float sj[6];
 #pragma unroll
-                    for (int c = 0; c < 6; ++c) sj[c] = Ss[6 * j + c];
-                    Mx[k * nv + j] = dot6(sj, f);
-                }
+                for (int c = 0; c < 6; ++c) sj[c] = Ss[6 * j + c];
+                Mx[k * nv + j] = dot6(sj, f);
             });
+            Mx[k * nv + k] = diag;
         } else {
+            Mx[k * nv + k] = diag;
             for (int a = t.anc_start[k]; a < t.anc_start[k + 1]; ++a) {
                 const int j = t.anc_list[a];
                 float sj[6];
@@ -1022,8 +1023,12 @@ MI_D void wave_artic_substep(const DevModel& m, const WaveTabs& t, const DevStat
                 for (int q = 0; q < 6; ++q) sv[q] = Ss[6 * c + q];
                 const float v = dot6(sv, f);
                 const bool ia = (msk >> c) & 1u, ib = (msk2 >> c) & 1u;
-                const float xc = (ia ? v : 0.0f) - (ib ? v : 0.0f);
-                x[c] = crow ? xc : (bv == 0 ? rhs[c] : (kd == c ? 1.0f : 0.0f));
+                float xc = (ia ? v : 0.0f) - (ib ? v : 0.0f);
+                float rc = rhs[c];   // uniform LDS broadcast
+                // materialised on every lane: otherwise the compiler sinks the dot product and
+                // the load into a divergent branch per DOF again
+                asm volatile("" : "+v"(xc), "+v"(rc));
+                x[c] = crow ? xc : (bv == 0 ? rc : (kd == c ? 1.0f : 0.0f));
             });
             if (on && r >= 0 && r < t.j_rows_lds) {   // keep J_r for the PGS sweeps
                 float* jl = sm + t.s_J + r * TP::nv;
