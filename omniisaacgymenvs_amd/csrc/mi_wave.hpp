@@ -375,19 +375,48 @@ MI_D void ct_publish_factor(int lane, int dj, const float (&Mc)[T::nvc], float d
 // x <- M~^-1 x on a lane-private register vector (a: see below), factor entries read from the published
 // LDS rows: every read is a wave-uniform broadcast (no VALU readlanes; adjacent entries
 // merge into wide LDS reads). Same operation order as ct_solve / tree_solve_lds.
+// most ancestors of any DOF (size of the one-step prefetch buffers of ct_solve_l)
+template <class T>
+constexpr int ct_max_anc() {
+    int m = 1;
+    for (int i = 0; i < T::nv; ++i) {
+        const int n = T::dof.anc_start[i + 1] - T::dof.anc_start[i];
+        if (n > m) m = n;
+    }
+    return m;
+}
+
+// The step fences keep each step's FMAs in order (and the factor loads from being front-loaded
+// into hundreds of live registers), which also kept every step's LDS broadcast reads behind
+// the previous step: one LDS round trip exposed per step, 2 nv per solve. The factor entries
+// of step s + 1 are therefore read before step s's fence (one step of prefetch, ct_max_anc
+// registers): their latency overlaps step s's FMAs. Same values, same operation order.
 template <class T>
 MI_D void ct_solve_l(const float* Lr, float (&x)[T::nvc], float& a) {
+    constexpr int MA = ct_max_anc<T>();
+    float cur[MA], nxt[MA];
+    auto load = [&](auto I, float (&buf)[MA]) {
+        constexpr int i = I;
+        constexpr int na = T::dof.anc_start[i + 1] - T::dof.anc_start[i];
+        constexpr int off = T::dof.lrow[i];
+        sfor<0, na>([&](auto A) { buf[A] = Lr[off + A]; });
+    };
+    load(std::integral_constant<int, T::nv - 1>{}, cur);
     sfor_down<0, T::nv>([&](auto I) {                 // x <- L^-T x (leaves -> root)
         constexpr int i = I;
         constexpr int a0 = T::dof.anc_start[i], na = T::dof.anc_start[i + 1] - a0;
-        constexpr int off = T::dof.lrow[i];
+        if constexpr (i > 0) load(std::integral_constant<int, i - 1>{}, nxt);
 #pragma unroll
         for (int c = 0; c < T::nv; ++c) asm volatile("" : "+v"(x[c]));   // step fence
         const float xi = x[i];
         sfor<0, na>([&](auto A) {
             constexpr int j = T::dof.anc[a0 + A];
-            x[j] -= Lr[off + A] * xi;
+            x[j] -= cur[A] * xi;
         });
+        if constexpr (i > 0) {
+#pragma unroll
+            for (int m2 = 0; m2 < MA; ++m2) cur[m2] = nxt[m2];
+        }
     });
     // x <- D^-1 x; a = y^T D^-1 y with y = L^-T x_in, i.e. x_in^T M~^-1 x_in (for x_in = J_r^T
     // this is A_rr = J_r W_r, computed before the second pass needs no copy of J_r)
@@ -397,18 +426,23 @@ MI_D void ct_solve_l(const float* Lr, float (&x)[T::nvc], float& a) {
         x[I] = y * Lr[T::dof.lrow[T::nv] + I];
         a += y * x[I];
     });
+    load(std::integral_constant<int, 0>{}, cur);
     sfor<0, T::nv>([&](auto I) {                      // x <- L^-1 x (root -> leaves)
         constexpr int i = I;
         constexpr int a0 = T::dof.anc_start[i], na = T::dof.anc_start[i + 1] - a0;
-        constexpr int off = T::dof.lrow[i];
+        if constexpr (i + 1 < T::nv) load(std::integral_constant<int, i + 1>{}, nxt);
 #pragma unroll
         for (int c = 0; c < T::nv; ++c) asm volatile("" : "+v"(x[c]));
         float xi = x[i];
         sfor<0, na>([&](auto A) {
             constexpr int j = T::dof.anc[a0 + A];
-            xi -= Lr[off + A] * x[j];
+            xi -= cur[A] * x[j];
         });
         x[i] = xi;
+        if constexpr (i + 1 < T::nv) {
+#pragma unroll
+            for (int m2 = 0; m2 < MA; ++m2) cur[m2] = nxt[m2];
+        }
     });
 }
 
@@ -1183,10 +1217,19 @@ MI_D void wave_artic_substep(const DevModel& m, const WaveTabs& t, const DevStat
             }
             float u = lane < NV ? us[lane] : 0.0f;
             const int kc = lane < NV ? lane : 0;
+            // u = u* + sum_r W_r lambda_r in row order; four rows' W loads per uniform branch
+            // (one LDS round trip per group instead of per row); rows past nrows add W 0
 #pragma unroll
-            for (int rr = 0; rr < RMAX; ++rr) {
-                if (rr >= nrows) break;
-                u += w_row<TP::kSelf>(t, sm, rr, NV)[kc] * readlane(lam, rr);
+            for (int g0 = 0; g0 < RMAX; g0 += 4) {
+                if (g0 >= nrows) break;
+                float wq[4], lq[4];
+#pragma unroll
+                for (int q = 0; q < 4; ++q) {
+                    wq[q] = w_row<TP::kSelf>(t, sm, min(g0 + q, nrows - 1), NV)[kc];
+                    lq[q] = g0 + q < nrows ? readlane(lam, g0 + q) : 0.0f;
+                }
+#pragma unroll
+                for (int q = 0; q < 4; ++q) u += wq[q] * lq[q];
             }
             if (lane < NV) us[lane] = u;
             if (lane < nrows) sm[t.s_ad + lane] = lam;           // reuse: lambda of row lane
