@@ -227,13 +227,17 @@ def kernel_name(view, task) -> str:
 
 def read_traffic(task_name: str):
     """HBM bytes per launch from the committed PMC passes (profiles/traffic_<task>.json), if any:
-    (FETCH_SIZE x2 per the gfx950 correction + WRITE_SIZE, the same with FETCH_SIZE as reported)."""
+    (instruction fetch at face value + data reads x2 + WRITE_SIZE, per the calibration of
+    tools/fetch_calib.hip and the env-count sweep of tools/traffic_split.py; FETCH_SIZE as
+    reported + WRITE_SIZE; the split by source)."""
     p = os.path.join(ROOT, "profiles", f"traffic_{task_name}.json")
     if os.path.exists(p):
         with open(p) as f:
             d = json.load(f)
-        return d.get("bytes_per_launch"), d.get("bytes_per_launch_uncorrected")
-    return None, None
+        split = {k: d[k] for k in ("instruction_fetch_bytes", "data_read_bytes", "write_bytes_at_n")
+                 if k in d}
+        return d.get("bytes_per_launch"), d.get("bytes_per_launch_uncorrected"), split
+    return None, None, {}
 
 
 def action_pool(view, n, A, seed, device, pool=16):
@@ -386,7 +390,7 @@ def main():
         if kernel_ms:
             algo = ALGO_BYTES[args.task] * n_local
             achieved = algo / (kernel_ms * 1e-3) / 1e9
-            traffic, traffic_raw = read_traffic(args.task)
+            traffic, traffic_raw, split = read_traffic(args.task)
             roof = {"bound": "hbm", "achieved": round(achieved, 3), "peak": HBM_PEAK_GBS,
                     "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 6), "traffic": traffic,
                     "kernel": kernel_name(view, task), "kernel_ms": round(kernel_ms, 4),
@@ -396,8 +400,9 @@ def main():
             if traffic:
                 roof["traffic_gbs"] = round(traffic / (kernel_ms * 1e-3) / 1e9, 3)
             if traffic_raw:
-                # the x2 FETCH correction is calibrated for 16-B-per-lane streaming reads only
                 roof["traffic_uncorrected_fetch"] = traffic_raw
+            if split:
+                roof["traffic_split"] = split
         out = {
             "metric": BASELINE_METRIC if args.task == "Humanoid" else
                       f"env-steps/s (physics+obs+reward) {args.task} {args.num_envs} envs (side run)",

@@ -1,8 +1,10 @@
 #!/bin/bash
-# instruction-cache counters: current vs old library
+# instruction-cache and issue counters of the fused env-step kernel (Humanoid bench), one PMC
+# pass per block: SQC (I-cache), SQ (wave-cycle split, instruction fetch)
 source "$(dirname "$0")/gpu_lib.sh"
-B="python3 bench.py --steps 30 --warmup 5 --no-cpu-baseline --fuse-envs 0 --no-side"
-for v in libmi_sim libmi_sim_old libmi_sim_v6; do
-  run ${v}_ic 300 env MI_SIM_LIB=omniisaacgymenvs_amd/$v.so rocprofv3 --pmc SQC_ICACHE_HITS SQC_ICACHE_MISSES SQ_IFETCH SQ_WAIT_INST_ANY SQ_WAVE_CYCLES --kernel-trace -d gpurun_out/${v}_ic -o run -- $B
-done
+B="python3 bench.py --steps 30 --warmup 5 --no-cpu-baseline --fuse-envs 0 --no-side ${BARGS:-}"
+RP="rocprofv3 --output-format csv --kernel-trace"
+T=${TAG:-cur}
+run ic1_$T 90 timeout -s KILL 80 $RP --pmc SQC_ICACHE_HITS SQC_ICACHE_MISSES SQC_ICACHE_MISSES_DUPLICATE -d gpurun_out/ic1_$T -o run -- $B
+run ic2_$T 90 timeout -s KILL 80 $RP --pmc SQ_IFETCH SQ_WAIT_INST_ANY SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_ACTIVE_INST_ANY SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU -d gpurun_out/ic2_$T -o run -- $B
 echo ALL_DONE
