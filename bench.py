@@ -51,6 +51,8 @@ def parse(argv=None):
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-side", action="store_true", help="skip the Cartpole / Ant side runs")
     ap.add_argument("--modular", action="store_true", help="method-by-method path, not fused")
+    ap.add_argument("--events-apart", action="store_true",
+                    help="diagnostic: time the window without kernel events, events in a second window")
     ap.add_argument("--fuse-envs", type=int, default=1048576,
                     help="envs of the obs/reward-fuse HBM roofline side measurement (0: skip)")
     return ap.parse_args(argv)
@@ -83,9 +85,12 @@ class ShardLoop:
         self.H = horizon if rollout is None else min(horizon, rollout.H)
         self.h = 0          # next row of the current horizon
         self.gathering = True
+        self.ev = None      # (starts, ends, every, k0): kernel events on steps k0, k0 + every, ...
 
     def step(self, k: int):
         a = self.actions[k % len(self.actions)]
+        if self.ev is not None:
+            self.env.kernel_events = self.ev[:2] if (k - self.ev[3]) % self.ev[2] == 0 else None
         r = self.rollout
         if r is None:
             return self.env.step(a)[0]
@@ -225,6 +230,22 @@ def kernel_name(view, task) -> str:
     return "k_env_step"
 
 
+TIME_EVERY = 4   # every 4th fused launch of a timed window carries the kernel-timing events
+
+
+def launch_times_ms(view, cap: int):
+    """Mean duration (ms) of the fused launches timed since mi_sim_time_launches (dispatch-carried
+    HIP events), then timing off; None when no launch was timed."""
+    import ctypes as C
+    from omniisaacgymenvs_amd import native as NL
+    buf = (C.c_float * cap)()
+    n = C.c_int32(0)
+    NL.check(NL.lib().mi_sim_launch_times(view.handle, buf, cap, C.byref(n)), "mi_sim_launch_times")
+    NL.check(NL.lib().mi_sim_time_launches(view.handle, 0, 0), "mi_sim_time_launches")
+    k = min(n.value, cap)
+    return sum(buf[:k]) / k if k else None
+
+
 def read_traffic(task_name: str):
     """HBM bytes per launch from the committed PMC passes (profiles/traffic_<task>.json), if any:
     (instruction fetch at face value + data reads x2 + WRITE_SIZE, per the calibration of
@@ -264,17 +285,15 @@ def side_run(task_name: str, n: int, steps: int = 200, warmup: int = 30) -> dict
     env.reset()
     for k in range(warmup):
         env.step(actions[k % len(actions)])
-    starts = [torch.cuda.Event(enable_timing=True) for _ in range(steps)]
-    ends = [torch.cuda.Event(enable_timing=True) for _ in range(steps)]
-    env.kernel_events = (starts, ends)
+    from omniisaacgymenvs_amd import native as NL
+    NL.check(NL.lib().mi_sim_time_launches(view.handle, TIME_EVERY, steps), "mi_sim_time_launches")
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     for k in range(steps):
         env.step(actions[k % len(actions)])
     torch.cuda.synchronize()
     el = time.perf_counter() - t0
-    env.kernel_events = None
-    kms = sum(s.elapsed_time(e) for s, e in zip(starts, ends)) / steps
+    kms = launch_times_ms(view, steps)
     ach = ALGO_BYTES[task_name] * n / (kms * 1e-3) / 1e9
     # the same steps replayed from a captured HIP graph (as the PPO rollout runs them,
     # rlg/a2c_continuous.py graph_rollout): no per-step Python / launch overhead
@@ -347,15 +366,45 @@ def main():
 
     for k in range(args.warmup):
         loop.step(k)
-    # kernel events around every fused launch inside the timed region (same stream)
-    starts = [torch.cuda.Event(enable_timing=True) for _ in range(args.steps)]
-    ends = [torch.cuda.Event(enable_timing=True) for _ in range(args.steps)]
-    env.kernel_events = (starts, ends)
-    env._ev_i = 0
-    win = loop.window(args.warmup, args.steps, sync, barrier)
-    env.kernel_events = None
+    # kernel time, live, over the timed region: HIP start / stop events carried by the dispatch of
+    # every TIME_EVERY-th fused launch (hipExtLaunchKernelGGL inside libmi_sim,
+    # mi_sim_time_launches), on the launch stream. Torch event records around every launch slowed
+    # the window by 2.5 % (Humanoid) / 6.9 % (Ant), dispatch events on every launch by 1.7 % /
+    # 4.3 % (`--events-apart`); on every 4th launch the window is within noise.
+    from omniisaacgymenvs_amd import native as NL
+    if args.events_apart:
+        # diagnostic: the same window plain, with torch events around every launch, and with
+        # the dispatch-carried events
+        win = loop.window(args.warmup, args.steps, sync, barrier)
+        s_all = [torch.cuda.Event(enable_timing=True) for _ in range(args.steps)]
+        e_all = [torch.cuda.Event(enable_timing=True) for _ in range(args.steps)]
+        env._ev_i = 0
+        loop.ev = (s_all, e_all, 1, args.warmup + args.steps)
+        win_ev = loop.window(args.warmup + args.steps, args.steps, sync, barrier)
+        loop.ev = None
+        env.kernel_events = None
+        torch_ms = sum(a.elapsed_time(b) for a, b in zip(s_all, e_all)) / args.steps
+        k0 = args.warmup + 2 * args.steps
+        NL.check(NL.lib().mi_sim_time_launches(view.handle, 1, args.steps), "mi_sim_time_launches")
+        win_x = loop.window(k0, args.steps, sync, barrier)
+        ext_ms = launch_times_ms(view, args.steps)
+        NL.check(NL.lib().mi_sim_time_launches(view.handle, TIME_EVERY, args.steps), "mi_sim_time_launches")
+        win_s = loop.window(k0 + args.steps, args.steps, sync, barrier)
+        s_ms = launch_times_ms(view, args.steps)
+        print(json.dumps({"events_apart": {
+            f"ms_per_step_dispatch_events_every_{TIME_EVERY}": round(win_s["elapsed"] / args.steps * 1e3, 4),
+            f"kernel_ms_dispatch_events_every_{TIME_EVERY}": round(s_ms, 4) if s_ms else None,
+            "ms_per_step_plain": round(win["elapsed"] / args.steps * 1e3, 4),
+            "ms_per_step_torch_events": round(win_ev["elapsed"] / args.steps * 1e3, 4),
+            "kernel_ms_torch_events": round(torch_ms, 4),
+            "ms_per_step_dispatch_events": round(win_x["elapsed"] / args.steps * 1e3, 4),
+            "kernel_ms_dispatch_events": round(ext_ms, 4) if ext_ms else None}}))
+    else:
+        if env.fused:
+            NL.check(NL.lib().mi_sim_time_launches(view.handle, TIME_EVERY, args.steps), "mi_sim_time_launches")
+        win = loop.window(args.warmup, args.steps, sync, barrier)
     elapsed = win["elapsed"]
-    kernel_ms = sum(s.elapsed_time(e) for s, e in zip(starts, ends)) / args.steps if env.fused else None
+    kernel_ms = launch_times_ms(view, args.steps) if env.fused else None
     gather_info = None
     if distributed:
         t = torch.tensor([elapsed], device=device, dtype=torch.float64)

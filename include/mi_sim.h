@@ -218,6 +218,15 @@ int mi_env_step(mi_sim* sim, const float* actions /*[N,A]*/, int32_t substeps,
                 float* rew_out /*[N]|NULL*/, int64_t* reset_out /*[N]|NULL*/, void* stream);
 /* rew_out / reset_out: the fresh copies VecEnvRLGames._process_data returns
  * (vec_env_rlgames.py:41-46), written by the same launch instead of two clone kernels. */
+/* Launch timing (measurement only, no reference counterpart; bench.py's roofline): from now on
+ * every `every`-th mi_env_step / mi_task_post_step launch (up to `capacity` of them) carries a HIP start / stop event
+ * pair on its own dispatch (hipExtLaunchKernelGGL), so the recorded interval is the kernel alone
+ * and no marker packets are queued between launches. every <= 0 turns it off. Launches made while
+ * the stream captures a graph are not timed. */
+int mi_sim_time_launches(mi_sim* sim, int32_t every, int32_t capacity);
+/* Durations (ms) of the launches timed since mi_sim_time_launches, in launch order: waits for
+ * each one's stop event, writes min(recorded, max_out) values, *n_out = number recorded. */
+int mi_sim_launch_times(mi_sim* sim, float* ms_out, int32_t max_out, int32_t* n_out);
 
 /* --- observation / action noise DR (utils/domain_randomization/randomize.py:176-306) ------
  * The `domain_randomization.randomization_params.{observations,actions}` block of a task YAML.

@@ -5,6 +5,7 @@
 // action clamp + efforts, controlFrequencyInv physics substeps, obs / reward / done and the
 // VecEnv obs clamp, with the per-env solver workspace resident in L2 / MALL between phases.
 #include <hip/hip_runtime.h>
+#include <hip/hip_ext.h>
 
 #include <cmath>
 #include <cstdarg>
@@ -72,7 +73,14 @@ struct mi_sim {
     int post_kernel = -1, post_grid = 0;   // last mi_task_post_step launch (mi_task_post_kernel)
     std::vector<float> lower, upper;  // host copy for mi_sim_info
     std::vector<void*> allocs;
+    // launch timing (mi_sim_time_launches): every tev_every-th mi_env_step launch carries a
+    // start / stop event pair on its own dispatch (hipExtLaunchKernelGGL), no marker packets
+    std::vector<hipEvent_t> tev;      // [2 * capacity]: start, stop of recorded launch k
+    int tev_every = 0;
+    long long tev_seen = 0;
+    int tev_rec = 0;
 };
+static hipError_t timed_launch(mi_sim* s, void* stream, hipEvent_t* ev0, hipEvent_t* ev1);
 
 static int dev_alloc(mi_sim* s, void** p, size_t bytes) {
     if (bytes == 0) bytes = 16;
@@ -1261,6 +1269,7 @@ int mi_sim_create(const mi_model_desc* md, const mi_sim_params* prm, int32_t N, 
 int mi_sim_destroy(mi_sim* s) {
     if (!s) return MI_OK;
     (void)hipSetDevice(s->device);
+    for (hipEvent_t e : s->tev) (void)hipEventDestroy(e);
     for (void* p : s->allocs) (void)hipFree(p);
     delete s;
     return MI_OK;
@@ -1466,8 +1475,12 @@ int mi_task_post_step(mi_sim* s, const float* actions, float* obs, float* rew, i
             const char* pm = getenv("MI_POST_PIPE_MIN");   // tiles per workgroup (tuning)
             if (!g && ntiles < (pm ? atoi(pm) : 2) * grid) goto one_tile;
             const KParams* kp = (const KParams*)s->kp_dev;
-#define POST_PIPE(R) hipLaunchKernelGGL(k_loco_post_pipe<R>, dim3(grid), dim3(64), tile, STREAM(stream), kp, \
-            actions, obs, rew, reset_buf, progress_buf, potentials, prev_potentials)
+            hipEvent_t ev0 = nullptr, ev1 = nullptr;
+            HIP_TRY(timed_launch(s, stream, &ev0, &ev1));
+#define POST_PIPE(R) do { if (ev0) hipExtLaunchKernelGGL(k_loco_post_pipe<R>, dim3(grid), dim3(64), (uint32_t)tile, \
+            STREAM(stream), ev0, ev1, 0, kp, actions, obs, rew, reset_buf, progress_buf, potentials, prev_potentials); \
+            else hipLaunchKernelGGL(k_loco_post_pipe<R>, dim3(grid), dim3(64), tile, STREAM(stream), kp, \
+            actions, obs, rew, reset_buf, progress_buf, potentials, prev_potentials); } while (0)
             switch (es) {
                 case 32: POST_PIPE(4); break;
                 case 64: POST_PIPE(8); break;
@@ -1487,8 +1500,13 @@ int mi_task_post_step(mi_sim* s, const float* actions, float* obs, float* rew, i
     const size_t tile = post_tile_lds(te, stage, s->ds.es, s->tp.A, s->tp.O, s->dm.D, s->dm.S);
     if (s->tp.kind != MI_TASK_CARTPOLE && s->ds.fs == 1 && tile <= 64 * 1024) {
         const dim3 g((s->N + te - 1) / te);
-#define POST_TILED(TE, ST) hipLaunchKernelGGL((k_loco_post_tiled<TE, ST>), g, dim3(64), tile, STREAM(stream), \
-            s->dm, s->ds, s->tp, actions, obs, rew, reset_buf, progress_buf, potentials, prev_potentials)
+        hipEvent_t ev0 = nullptr, ev1 = nullptr;
+        HIP_TRY(timed_launch(s, stream, &ev0, &ev1));
+#define POST_TILED(TE, ST) do { if (ev0) hipExtLaunchKernelGGL((k_loco_post_tiled<TE, ST>), g, dim3(64), (uint32_t)tile, \
+            STREAM(stream), ev0, ev1, 0, s->dm, s->ds, s->tp, actions, obs, rew, reset_buf, progress_buf, potentials, \
+            prev_potentials); \
+            else hipLaunchKernelGGL((k_loco_post_tiled<TE, ST>), g, dim3(64), tile, STREAM(stream), \
+            s->dm, s->ds, s->tp, actions, obs, rew, reset_buf, progress_buf, potentials, prev_potentials); } while (0)
         switch (var) {
             case 0: POST_TILED(64, true); break;
             case 1: POST_TILED(64, false); break;
@@ -1546,6 +1564,23 @@ int mi_task_is_done(mi_sim* s, const float* obs, int64_t* reset_buf, const int64
     return MI_OK;
 }
 
+// Timed launch (mi_sim_time_launches): the event pair of this launch, or nulls. The events ride on
+// the kernel's own dispatch (hipExtLaunchKernelGGL); launches into a capturing stream are not timed.
+static hipError_t timed_launch(mi_sim* s, void* stream, hipEvent_t* ev0, hipEvent_t* ev1) {
+    *ev0 = *ev1 = nullptr;
+    if (s->tev_every > 0 && s->tev_rec < (int)s->tev.size() / 2 && (s->tev_seen++ % s->tev_every) == 0) {
+        hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
+        const hipError_t e = hipStreamIsCapturing(STREAM(stream), &cs);
+        if (e != hipSuccess) return e;
+        if (cs == hipStreamCaptureStatusNone) {
+            *ev0 = s->tev[2 * s->tev_rec];
+            *ev1 = s->tev[2 * s->tev_rec + 1];
+            ++s->tev_rec;
+        }
+    }
+    return hipSuccess;
+}
+
 int mi_env_step(mi_sim* s, const float* actions, int32_t substeps, float* obs_out, float* obs_task,
                 float* rew, int64_t* reset_buf, int64_t* progress_buf, float* potentials,
                 float* prev_potentials, float* actions_out, float* rew_out, int64_t* reset_out,
@@ -1556,18 +1591,66 @@ int mi_env_step(mi_sim* s, const float* actions, int32_t substeps, float* obs_ou
         return fail(MI_E_NULL, "mi_env_step: action DR needs actions_out (task.actions)");
     if (substeps < 0 || substeps > 64) return fail(MI_E_ARG, "substeps %d out of range", substeps);
     HIP_TRY(hipSetDevice(s->device));
+    hipEvent_t ev0 = nullptr, ev1 = nullptr;
+    HIP_TRY(timed_launch(s, stream, &ev0, &ev1));
     if (s->wave && s->tp.kind != MI_TASK_CARTPOLE)
         with_topo(s->topo, [&](auto T) {
-            hipLaunchKernelGGL(k_env_step_wave<decltype(T)>, wave_grid(s), wave_block(s), s->lds_bytes,
-                               STREAM(stream), (const KParams*)s->kp_dev, actions, substeps,
-                               obs_out, obs_task, rew, reset_buf, progress_buf, potentials,
-                               prev_potentials, actions_out, rew_out, reset_out);
+            if (ev0)
+                hipExtLaunchKernelGGL(k_env_step_wave<decltype(T)>, wave_grid(s), wave_block(s),
+                                      (uint32_t)s->lds_bytes, STREAM(stream), ev0, ev1, 0,
+                                      (const KParams*)s->kp_dev, actions, substeps, obs_out, obs_task,
+                                      rew, reset_buf, progress_buf, potentials, prev_potentials,
+                                      actions_out, rew_out, reset_out);
+            else
+                hipLaunchKernelGGL(k_env_step_wave<decltype(T)>, wave_grid(s), wave_block(s), s->lds_bytes,
+                                   STREAM(stream), (const KParams*)s->kp_dev, actions, substeps,
+                                   obs_out, obs_task, rew, reset_buf, progress_buf, potentials,
+                                   prev_potentials, actions_out, rew_out, reset_out);
         });
+    else if (ev0)
+        hipExtLaunchKernelGGL(k_env_step, grid_for(s, s->N), dim3(s->block), 0u, STREAM(stream), ev0, ev1, 0,
+                              s->dm, s->ds, s->sp, s->tp, actions, substeps, obs_out, obs_task, rew,
+                              reset_buf, progress_buf, potentials, prev_potentials, actions_out, rew_out,
+                              reset_out);
     else
         hipLaunchKernelGGL(k_env_step, grid_for(s, s->N), dim3(s->block), 0, STREAM(stream), s->dm,
                            s->ds, s->sp, s->tp, actions, substeps, obs_out, obs_task, rew, reset_buf,
                            progress_buf, potentials, prev_potentials, actions_out, rew_out, reset_out);
     LAUNCH_CHECK();
+    return MI_OK;
+}
+
+int mi_sim_time_launches(mi_sim* s, int32_t every, int32_t capacity) {
+    NEED(s);
+    if (every > 0 && (capacity < 1 || capacity > (1 << 20)))
+        return fail(MI_E_ARG, "mi_sim_time_launches: capacity %d out of range", capacity);
+    HIP_TRY(hipSetDevice(s->device));
+    s->tev_every = every > 0 ? every : 0;
+    s->tev_seen = 0;
+    s->tev_rec = 0;
+    const size_t want = every > 0 ? 2 * (size_t)capacity : 0;
+    while (s->tev.size() < want) {
+        hipEvent_t e = nullptr;
+        HIP_TRY(hipEventCreate(&e));
+        s->tev.push_back(e);
+    }
+    while (s->tev.size() > want) {
+        (void)hipEventDestroy(s->tev.back());
+        s->tev.pop_back();
+    }
+    return MI_OK;
+}
+
+int mi_sim_launch_times(mi_sim* s, float* ms_out, int32_t max_out, int32_t* n_out) {
+    NEED(s); NEED(n_out);
+    if (max_out > 0) NEED(ms_out);
+    HIP_TRY(hipSetDevice(s->device));
+    const int n = std::min(s->tev_rec, std::max(0, (int)max_out));
+    for (int k = 0; k < n; ++k) {
+        HIP_TRY(hipEventSynchronize(s->tev[2 * k + 1]));
+        HIP_TRY(hipEventElapsedTime(&ms_out[k], s->tev[2 * k], s->tev[2 * k + 1]));
+    }
+    *n_out = s->tev_rec;
     return MI_OK;
 }
 

@@ -117,6 +117,8 @@ _SIGS = {
     "mi_task_metrics": (C.c_int, [C.c_void_p] + [C.c_void_p] * 6),
     "mi_task_is_done": (C.c_int, [C.c_void_p] + [C.c_void_p] * 4),
     "mi_env_step": (C.c_int, [C.c_void_p, C.c_void_p, C.c_int32] + [C.c_void_p] * 11),
+    "mi_sim_time_launches": (C.c_int, [C.c_void_p, C.c_int32, C.c_int32]),
+    "mi_sim_launch_times": (C.c_int, [C.c_void_p, C.c_void_p, C.c_int32, _i32p]),
     "mi_task_set_dr": (C.c_int, [C.c_void_p, C.POINTER(MiDrParams)]),
     "mi_dr_apply_actions": (C.c_int, [C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p]),
     "mi_dr_apply_observations": (C.c_int, [C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p]),
