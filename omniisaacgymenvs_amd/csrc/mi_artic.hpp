@@ -383,8 +383,8 @@ MI_D void artic_substep(const DevModel& m, const DevState& st, const SimP& p, in
         m3_tvec(R, T, Tl);
 #pragma unroll
         for (int q = 0; q < 3; ++q) {
-            st.sens[sx(st, 6 * si + q, i)] = Fl[q];
-            st.sens[sx(st, 6 * si + 3 + q, i)] = Tl[q];
+            st.sens[ssx(st, 6 * si + q, i)] = Fl[q];
+            st.sens[ssx(st, 6 * si + 3 + q, i)] = Tl[q];
         }
     }
     // ---------------- integrate ----------------

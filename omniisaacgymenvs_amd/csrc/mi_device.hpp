@@ -61,9 +61,14 @@ struct DevModel {
 //     32 floats = whole 128-B lines); the wave reads / writes its env's state with one
 //     coalesced access per field group;
 //   field-major SoA (one-lane-per-env kernels): fs = N, es = 1; lane-consecutive envs.
+// The sensor wrenches have strides of their own (sfs, ses): with records they are NOT in the
+// record but in a [N][6S] array next to it (sfs = 1, ses = 6S), so the state the obs/reward fuse
+// reads fits whole lines (Humanoid: pos, quat, vel, q, qd = 55 floats, 2 of the record's 3 lines,
+// + 48 contiguous sensor bytes, instead of all 3 lines); field-major: sfs = N, ses = 1.
 struct DevState {
     int N;
     int fs, es;           // field stride, env stride (floats)
+    int sfs, ses;         // sensor field / env stride (floats)
     int64_t off;          // global id of env 0 (multi-GPU shard offset)
     uint64_t seed;
     const float* origins; // [3][N]
@@ -83,6 +88,10 @@ struct DevState {
 
 MI_D size_t sx(const DevState& st, int k, int i) {
     return (size_t)k * (size_t)st.fs + (size_t)i * (size_t)st.es;
+}
+// sensor element k of env i (st.sens)
+MI_D size_t ssx(const DevState& st, int k, int i) {
+    return (size_t)k * (size_t)st.sfs + (size_t)i * (size_t)st.ses;
 }
 
 struct DevTask {

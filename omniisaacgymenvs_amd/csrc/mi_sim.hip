@@ -207,25 +207,29 @@ __global__ __launch_bounds__(64) void k_loco_post_tiled(DevModel m, DevState st,
     const int n = min(TE, st.N - e0);
     const int O = tp.O, A = tp.A;
     if (TE == 32 && STAGE) {
-        // compact tile: each record's used fields only (root 13, q, qd, sensors: the efforts
-        // and the line padding are dropped on the way into LDS), actions read in place
+        // compact tile: each record's used fields only (root 13, q, qd: the float4s up to the end
+        // of qd, so the efforts line is never fetched) and the env's sensor wrenches from their
+        // own array; actions read in place
         const int D = m.D, S = m.S;
-        const int k0 = 13 + 2 * D, s0 = 13 + 3 * D, ns = 6 * S, PC = (k0 + ns) | 1;   // odd row stride: no LDS bank aliasing across envs
+        const int k0 = 13 + 2 * D, ne4 = (k0 + 3) >> 2, ns = 6 * S, PC = (k0 + ns) | 1;   // odd row stride: no LDS bank aliasing across envs
         float* srec = sm;
         float* sobs = sm + TE * PC;
         float* sterm = sobs + TE * O;                          // [TE][3] sums
         {
             const float4* s4 = (const float4*)(st.root_pos + (size_t)e0 * st.es);
-            for (int k = lane; k < n * st.es / 4; k += 64) {   // es % 4 == 0 (whole lines)
-                const float4 v4 = s4[k];
+            for (int k = lane; k < n * ne4; k += 64) {         // es % 4 == 0 (whole lines)
+                const int e = k / ne4, c4 = k - e * ne4;
+                const float4 v4 = s4[e * (st.es >> 2) + c4];
                 const float vv[4] = {v4.x, v4.y, v4.z, v4.w};
-                const int f0 = 4 * k, e = f0 / st.es, c0 = f0 - e * st.es;
 #pragma unroll
                 for (int q = 0; q < 4; ++q) {
-                    const int c = c0 + q;
+                    const int c = 4 * c4 + q;
                     if (c < k0) srec[e * PC + c] = vv[q];
-                    else if (c >= s0 && c < s0 + ns) srec[e * PC + k0 + (c - s0)] = vv[q];
                 }
+            }
+            for (int k = lane; k < n * ns; k += 64) {
+                const int e = k / ns, c = k - e * ns;
+                srec[e * PC + k0 + c] = st.sens[ssx(st, c, e0 + e)];
             }
         }
         __syncthreads();
@@ -233,6 +237,7 @@ __global__ __launch_bounds__(64) void k_loco_post_tiled(DevModel m, DevState st,
         v.fs = 1; v.es = PC;
         v.root_pos = srec; v.root_quat = srec + 3; v.root_vel = srec + 7;
         v.q = srec + 13; v.qd = srec + 13 + D; v.sens = srec + k0;
+        v.sfs = 1; v.ses = PC;
         // split by lane halves: lanes 0..31 the root-frame block of env `lane`, lanes 32..63 the
         // per-DOF / sensor block and the reward's DOF-order sums of env `lane - 32`
         const int e = lane & 31;
@@ -278,7 +283,7 @@ __global__ __launch_bounds__(64) void k_loco_post_tiled(DevModel m, DevState st,
     v.root_pos = srec; v.root_quat = srec + (st.root_quat - st.root_pos);
     v.root_vel = srec + (st.root_vel - st.root_pos);
     v.q = srec + (st.q - st.root_pos); v.qd = srec + (st.qd - st.root_pos);
-    v.sens = srec + (st.sens - st.root_pos);
+    v.sens = st.sens + ssx(st, 0, e0);      // sensor wrenches read in place (their own array)
     if (lane < n) {
         const int i = e0 + lane;
         float* R = STAGE ? sobs + (size_t)lane * O : obs + (size_t)i * O;
@@ -482,18 +487,20 @@ __device__ __forceinline__ float* wave_env_lds(const WaveTabs& t, float* smem) {
 // rows, per-env scalars). Same arithmetic and write order per env as k_loco_post_tiled<32, true>
 // (bit-identical outputs).
 // Data movement is whole float4s with wave-uniform trip counts and no per-element guards:
-//  - record tile in LDS: each record's float4s as they sit in HBM, minus the float4s that hold
-//    efforts only (the task never reads them), at an odd float4 stride P4 so one field of 32
-//    envs spreads over the banks; a dropped float4 lands in the record's spare slot P4 - 1;
+//  - record tile in LDS: per env the record's first ne4 float4s (root, q, qd: the whole lines the
+//    task reads; the efforts line is never fetched) and the env's ns4 float4s of sensor wrenches
+//    from their own [N][6S] array, at an odd float4 stride P4 so one field of 32 envs spreads
+//    over the banks; loads past the tile land in a spare float4 after the tile;
 //  - loads clamp their index to the tile (a ragged last tile re-reads its last element into
 //    slots nobody reads) instead of branching;
 //  - the parameter block is read through the laundered KParams pointer once per tile (scalar
 //    loads), so no loop-invariant parameter occupies an SGPR across the tile loop.
-// NR4 = float4 per lane per tile (32 records x es floats / 4 / 64 = es / 8), a template
-// constant: the loads of a tile are one straight-line block, every register defined on every
-// path (a guarded block made the compiler stage the tile through scratch). Action rows: always
-// MI_PIPE_A loads per lane, the index clamped to the tile, the overhang written to a spare float.
-// Host-checked: records (fs = 1) of es = 8 NR4 floats; 1 <= A <= 32; D, 6S <= 64.
+// NR4 = record float4s per lane per tile (>= 32 ne4 / 64) and NS4 = sensor float4s per lane per
+// tile (>= 32 ns4 / 64), template constants: the loads of a tile are one straight-line block,
+// every register defined on every path (a guarded block made the compiler stage the tile through
+// scratch). Action rows: always MI_PIPE_A loads per lane, the index clamped to the tile, the
+// overhang written to a spare float. Host-checked: records (fs = 1), sensors (sfs = 1,
+// ses = 6S, 6S % 4 == 0); 1 <= A <= 32; D, 6S <= 64.
 constexpr int MI_PIPE_A = 16;   // 32 envs x <= 32 actions / 64 lanes
 // floor(x / d) for 0 <= x < 4096, 1 <= d <= 128: (x * ceil(2^20 / d)) >> 20 (exact there)
 MI_D int div_small(int x, unsigned magic) { return (int)(((unsigned)x * magic) >> 20); }
@@ -501,27 +508,28 @@ MI_D int div_small(int x, unsigned magic) { return (int)(((unsigned)x * magic) >
 typedef float v4f __attribute__((ext_vector_type(4)));   // native 16-B vector (no struct copies)
 
 struct PipeGeo {   // record-tile geometry of k_loco_post_pipe (floats unless noted)
-    int es4, ef0, ef1, nd, P4, P, s0;
+    int es4, ne4, ns4, P4, P, s0;
 };
-__host__ __device__ inline PipeGeo pipe_geo(int es, int D) {
+__host__ __device__ inline PipeGeo pipe_geo(int es, int D, int S) {
     PipeGeo g;
     g.es4 = es >> 2;
-    g.ef0 = (13 + 2 * D + 3) >> 2;                        // first float4 past qd
-    g.ef1 = (13 + 3 * D) >> 2;                            // float4 holding the first sensor value
-    if (g.ef1 < g.ef0) g.ef1 = g.ef0;
-    g.nd = g.ef1 - g.ef0;                                 // float4s of efforts only: dropped
-    g.P4 = ((g.es4 - g.nd) + 1) | 1;                      // odd, with a spare slot P4 - 1
+    g.ne4 = (13 + 2 * D + 3) >> 2;                        // record float4s up to the end of qd
+    g.ns4 = (6 * S) >> 2;                                 // sensor float4s (6S % 4 == 0)
+    g.P4 = (g.ne4 + g.ns4) | 1;                           // odd float4 stride
     g.P = 4 * g.P4;
-    g.s0 = 13 + 3 * D - 4 * g.nd;                         // sensors in the LDS record
+    g.s0 = 4 * g.ne4;                                     // sensors in the LDS record
     return g;
 }
-static size_t post_pipe_lds(int es, int A, int O, int D) {
-    const PipeGeo g = pipe_geo(es, D);
-    // records [32][P], obs tile [32][O], reward sums [32][3], potentials in / out, spare float
-    return sizeof(float) * (size_t)(32 * g.P + 32 * O + 3 * 32 + 2 * 32 + 4);
+constexpr int pipe_nr4(int ne4) { return (32 * ne4 + 63) / 64; }
+constexpr int pipe_ns4(int ns4) { return (32 * ns4 + 63) / 64; }
+static size_t post_pipe_lds(int es, int A, int O, int D, int S) {
+    const PipeGeo g = pipe_geo(es, D, S);
+    // records [32][P] + a spare float4, obs tile [32][O], reward sums [32][3], potentials in /
+    // out, spare float
+    return sizeof(float) * (size_t)(32 * g.P + 4 + 32 * O + 3 * 32 + 2 * 32 + 4);
 }
 
-template <int NR4>
+template <int NR4, int NS4>
 __global__ __launch_bounds__(64) void k_loco_post_pipe(const KParams* __restrict__ kp_arg,
                                                       const float* __restrict__ actions,
                                                       float* obs, float* rew, int64_t* reset_buf,
@@ -533,17 +541,19 @@ __global__ __launch_bounds__(64) void k_loco_post_pipe(const KParams* __restrict
     const KParams* kp = opaque_kp(kp_arg);
     const int O = kp->tp.O, A = kp->tp.A, D = kp->m.D, S = kp->m.S, es = kp->st.es, N = kp->st.N;
     const int ntiles = (N + TE - 1) / TE;
-    const PipeGeo g = pipe_geo(es, D);
+    const PipeGeo g = pipe_geo(es, D, S);
     const int ns = 6 * S, ka = 12 + 2 * D + ns;            // obs column of actions[0]
-    const unsigned mag_es = ((1u << 20) + g.es4 - 1) / g.es4, mag_a = ((1u << 20) + A - 1) / A;
+    const unsigned mag_ne = ((1u << 20) + g.ne4 - 1) / g.ne4, mag_a = ((1u << 20) + A - 1) / A;
+    const unsigned mag_ns = ((1u << 20) + g.ns4 - 1) / g.ns4;
     v4f* srec4 = reinterpret_cast<v4f*>(sm);
     float* srec = sm;
-    float* sobs = sm + TE * g.P;
+    const int spare4 = TE * g.P4;                          // float4 slot past the record tile
+    float* sobs = sm + TE * g.P + 4;
     float* sterm = sobs + TE * O;                          // [TE][3] sums
     float* spot = sterm + 3 * TE;                          // [TE] potentials (in / out)
     float* sprev = spot + TE;                              // [TE] prev_potentials (out)
-    const int trash = TE * g.P + TE * O + 5 * TE;          // spare float (action overhang)
-    v4f rr[NR4];
+    const int trash = TE * g.P + 4 + TE * O + 5 * TE;      // spare float (action overhang)
+    v4f rr[NR4], rsn[NS4];
     float ra[MI_PIPE_A];
     int64_t pg = 0, rs = 0;
     int nf = 0;
@@ -553,10 +563,15 @@ __global__ __launch_bounds__(64) void k_loco_post_pipe(const KParams* __restrict
 #define MI_PIPE_ISSUE(K, T)                                                                     \
     do {                                                                                        \
         const int e0_ = (T) * TE, n_ = min(TE, N - e0_);                                        \
-        const int c4_ = n_ * g.es4, ca_ = n_ * A;                                               \
+        const int c4_ = n_ * g.ne4, cs_ = n_ * g.ns4, ca_ = n_ * A;                              \
         const v4f* s4_ = reinterpret_cast<const v4f*>((K)->st.root_pos + (size_t)e0_ * es);       \
+        const v4f* ss_ = reinterpret_cast<const v4f*>((K)->st.sens + (size_t)e0_ * ns);           \
         const float* ga_ = actions + (size_t)e0_ * A;                                           \
-        _Pragma("unroll") for (int r = 0; r < NR4; ++r) rr[r] = s4_[min(lane + 64 * r, c4_ - 1)]; \
+        _Pragma("unroll") for (int r = 0; r < NR4; ++r) {                                       \
+            const int k_ = min(lane + 64 * r, c4_ - 1), e_ = div_small(k_, mag_ne);              \
+            rr[r] = s4_[e_ * g.es4 + (k_ - e_ * g.ne4)];                                         \
+        }                                                                                       \
+        _Pragma("unroll") for (int r = 0; r < NS4; ++r) rsn[r] = ss_[min(lane + 64 * r, cs_ - 1)]; \
         _Pragma("unroll") for (int r = 0; r < MI_PIPE_A; ++r) ra[r] = ga_[min(lane + 64 * r, ca_ - 1)]; \
         const int i_ = e0_ + min(lane, n_ - 1);                                                 \
         pg = progress_buf[i_];                                                                  \
@@ -579,9 +594,13 @@ __global__ __launch_bounds__(64) void k_loco_post_pipe(const KParams* __restrict
         // registers -> LDS: records (float4 slots), actions into the obs rows' action columns
 #pragma unroll
         for (int r = 0; r < NR4; ++r) {
-            const int kk = lane + 64 * r, e = div_small(kk, mag_es), k4 = kk - e * g.es4;
-            const int slot = k4 < g.ef0 ? k4 : (k4 < g.ef1 ? g.P4 - 1 : k4 - g.nd);
-            srec4[e * g.P4 + slot] = rr[r];
+            const int kk = lane + 64 * r, e = div_small(kk, mag_ne);
+            srec4[kk < TE * g.ne4 ? e * g.P4 + (kk - e * g.ne4) : spare4] = rr[r];
+        }
+#pragma unroll
+        for (int r = 0; r < NS4; ++r) {
+            const int kk = lane + 64 * r, e = div_small(kk, mag_ns);
+            srec4[kk < TE * g.ns4 ? e * g.P4 + g.ne4 + (kk - e * g.ns4) : spare4] = rsn[r];
         }
 #pragma unroll
         for (int r = 0; r < MI_PIPE_A; ++r) {
@@ -1205,20 +1224,24 @@ int mi_sim_create(const mi_model_desc* md, const mi_sim_params* prm, int32_t N, 
     void* p = nullptr;
 #define AL(field, T, cnt) if ((rc = dev_alloc(s, &p, sizeof(T) * (size_t)(cnt)))) return cleanup(rc); st.field = (T*)p
     if (s->wave) {
-        // one record per env: pos 3, quat 4, vel 6, q D, qd D, eff D, sensors 6S, padded to
-        // whole 128-B lines (the wave touches only its own lines, each access coalesced)
-        const int rec = (13 + 3 * D + 6 * S + 31) & ~31;
+        // one record per env: pos 3, quat 4, vel 6, q D, qd D, eff D, padded to whole 128-B
+        // lines (the wave touches only its own lines, each access coalesced); the sensor
+        // wrenches in a [N][6S] array of their own (DevState::sfs / ses)
+        const int rec = (13 + 3 * D + 31) & ~31;
         float* r = nullptr;
         if ((rc = dev_alloc(s, &p, sizeof(float) * (size_t)rec * N))) return cleanup(rc);
         r = (float*)p;
         st.fs = 1; st.es = rec;
         st.root_pos = r; st.root_quat = r + 3; st.root_vel = r + 7; st.q = r + 13;
-        st.qd = r + 13 + D; st.eff = r + 13 + 2 * D; st.sens = r + 13 + 3 * D;
+        st.qd = r + 13 + D; st.eff = r + 13 + 2 * D;
+        AL(sens, float, (size_t)6 * S * N);
+        st.sfs = 1; st.ses = 6 * S;
     } else {
         st.fs = N; st.es = 1;
         AL(root_pos, float, 3 * N); AL(root_quat, float, 4 * N); AL(root_vel, float, 6 * N);
         AL(q, float, (size_t)D * N); AL(qd, float, (size_t)D * N); AL(eff, float, (size_t)D * N);
         AL(sens, float, (size_t)6 * S * N);
+        st.sfs = N; st.ses = 1;
     }
     AL(reset_count, uint32_t, N); AL(nan_flag, int32_t, N); AL(dr_state, uint32_t, (size_t)6 * N);
     AL(nan_total, unsigned long long, 1);
@@ -1319,7 +1342,7 @@ int mi_get_sensor_wrench(mi_sim* s, float* out, void* stream) {
     HIP_TRY(hipSetDevice(s->device));
     if (s->dm.S == 0) return MI_OK;
     hipLaunchKernelGGL(k_soa_to_rows, gather_grid(s->N), dim3(256), 0, STREAM(stream),
-                       s->ds.sens, s->N, 6 * s->dm.S, s->ds.fs, s->ds.es, out);
+                       s->ds.sens, s->N, 6 * s->dm.S, s->ds.sfs, s->ds.ses, out);
     LAUNCH_CHECK();
     return MI_OK;
 }
@@ -1452,18 +1475,21 @@ int mi_task_post_step(mi_sim* s, const float* actions, float* obs, float* rew, i
     HIP_TRY(hipSetDevice(s->device));
     int var = post_tile_variant();
     if (var == 4) {   // 32p: several tiles per resident workgroup, next tile's loads in flight
-        const int es = s->ds.es;
-        const size_t tile = post_pipe_lds(es, s->tp.A, s->tp.O, s->dm.D);
+        const int es = s->ds.es, ns = 6 * s->dm.S;
+        const size_t tile = post_pipe_lds(es, s->tp.A, s->tp.O, s->dm.D, s->dm.S);
+        const PipeGeo pg = pipe_geo(es, s->dm.D, s->dm.S);
+        // shipped (NR4, NS4) instantiations: Humanoid (7, 2), Ant (4, 3); other models take the
+        // one-tile kernel
+        const int nr4 = pipe_nr4(pg.ne4), ns4 = pipe_ns4(pg.ns4);
+        const int combo = (nr4 == 7 && ns4 == 2) ? 1 : (nr4 == 4 && ns4 == 3) ? 2 : 0;
         if (s->tp.kind != MI_TASK_CARTPOLE && s->wave && s->kp_dev && s->ds.fs == 1 && es % 32 == 0 &&
-            es >= 32 && es <= 128 && s->tp.A >= 1 && s->tp.A <= 32 && s->dm.D >= 1 && s->dm.D <= 64 &&
-            6 * s->dm.S <= 64 && tile <= 64 * 1024) {
+            s->ds.sfs == 1 && s->ds.ses == ns && ns % 4 == 0 && combo &&
+            s->tp.A >= 1 && s->tp.A <= 32 && s->dm.D >= 1 && s->dm.D <= 64 &&
+            ns <= 64 && tile <= 64 * 1024) {
             if (s->num_cu <= 0)
                 HIP_TRY(hipDeviceGetAttribute(&s->num_cu, hipDeviceAttributeMultiprocessorCount, s->device));
             const int ntiles = (s->N + 31) / 32;
-            const void* fn = es == 32 ? (const void*)k_loco_post_pipe<4>
-                           : es == 64 ? (const void*)k_loco_post_pipe<8>
-                           : es == 96 ? (const void*)k_loco_post_pipe<12>
-                                      : (const void*)k_loco_post_pipe<16>;
+            const void* fn = combo == 1 ? (const void*)k_loco_post_pipe<7, 2> : (const void*)k_loco_post_pipe<4, 3>;
             // one resident round: workgroups per CU as registers and LDS allow together
             int per_cu = 0;
             HIP_TRY(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, fn, 64, tile));
@@ -1477,15 +1503,13 @@ int mi_task_post_step(mi_sim* s, const float* actions, float* obs, float* rew, i
             const KParams* kp = (const KParams*)s->kp_dev;
             hipEvent_t ev0 = nullptr, ev1 = nullptr;
             HIP_TRY(timed_launch(s, stream, &ev0, &ev1));
-#define POST_PIPE(R) do { if (ev0) hipExtLaunchKernelGGL(k_loco_post_pipe<R>, dim3(grid), dim3(64), (uint32_t)tile, \
+#define POST_PIPE(R, Q) do { if (ev0) hipExtLaunchKernelGGL((k_loco_post_pipe<R, Q>), dim3(grid), dim3(64), (uint32_t)tile, \
             STREAM(stream), ev0, ev1, 0, kp, actions, obs, rew, reset_buf, progress_buf, potentials, prev_potentials); \
-            else hipLaunchKernelGGL(k_loco_post_pipe<R>, dim3(grid), dim3(64), tile, STREAM(stream), kp, \
+            else hipLaunchKernelGGL((k_loco_post_pipe<R, Q>), dim3(grid), dim3(64), tile, STREAM(stream), kp, \
             actions, obs, rew, reset_buf, progress_buf, potentials, prev_potentials); } while (0)
-            switch (es) {
-                case 32: POST_PIPE(4); break;
-                case 64: POST_PIPE(8); break;
-                case 96: POST_PIPE(12); break;
-                default: POST_PIPE(16); break;
+            switch (combo) {
+                case 1: POST_PIPE(7, 2); break;
+                default: POST_PIPE(4, 3); break;
             }
 #undef POST_PIPE
             LAUNCH_CHECK();

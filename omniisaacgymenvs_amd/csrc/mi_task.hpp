@@ -277,7 +277,7 @@ MI_D void loco_obs_dof(const DevModel& m, const DevState& st, const DevTask& tp,
         orow[12 + 2 * D + 6 * S + j] = clampf(act[j], -act_clip, act_clip);
     }
     for (int k = 0; k < 6 * S; ++k)
-        orow[12 + 2 * D + k] = st.sens[sx(st, k, i)] * tp.contact_force_scale;
+        orow[12 + 2 * D + k] = st.sens[ssx(st, k, i)] * tp.contact_force_scale;
 }
 
 // ---------------------------------------------------------------------------------------

@@ -1439,7 +1439,7 @@ MI_D void wave_artic_substep(const DevModel& m, const WaveTabs& t, const DevStat
         sm[t.s_q + lane] = qn;                       // final state stays in LDS (post-step)
         finite = isfinite(v) && isfinite(qn);
     }
-    if (store_state && lane < 6 * m.S) st.sens[sx(st, lane, i)] = sm[t.s_rb + lane];
+    if (store_state && lane < 6 * m.S) st.sens[ssx(st, lane, i)] = sm[t.s_rb + lane];
     if (nr && lane == 0) {
         float u6[6], rp[3], rq[4];
 #pragma unroll
