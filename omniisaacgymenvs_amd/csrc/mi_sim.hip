@@ -524,9 +524,9 @@ constexpr int pipe_nr4(int ne4) { return (32 * ne4 + 63) / 64; }
 constexpr int pipe_ns4(int ns4) { return (32 * ns4 + 63) / 64; }
 static size_t post_pipe_lds(int es, int A, int O, int D, int S) {
     const PipeGeo g = pipe_geo(es, D, S);
-    // records [32][P] + a spare float4, obs tile [32][O], reward sums [32][3], potentials in /
-    // out, spare float
-    return sizeof(float) * (size_t)(32 * g.P + 4 + 32 * O + 3 * 32 + 2 * 32 + 4);
+    // records [32][P] + a spare float4, obs tile [32][O], potentials in / out, spare float (the
+    // reward sums stay in registers: lane pairs). Humanoid 20 128 B: 8 workgroups per CU.
+    return sizeof(float) * (size_t)(32 * g.P + 4 + 32 * O + 2 * 32 + 4);
 }
 
 template <int NR4, int NS4>
@@ -549,10 +549,9 @@ __global__ __launch_bounds__(64) void k_loco_post_pipe(const KParams* __restrict
     float* srec = sm;
     const int spare4 = TE * g.P4;                          // float4 slot past the record tile
     float* sobs = sm + TE * g.P + 4;
-    float* sterm = sobs + TE * O;                          // [TE][3] sums
-    float* spot = sterm + 3 * TE;                          // [TE] potentials (in / out)
+    float* spot = sobs + TE * O;                           // [TE] potentials (in / out)
     float* sprev = spot + TE;                              // [TE] prev_potentials (out)
-    const int trash = TE * g.P + 4 + TE * O + 5 * TE;      // spare float (action overhang)
+    const int trash_o = TE * O + 2 * TE;                   // spare float past sprev (action overhang), from sobs
     v4f rr[NR4], rsn[NS4];
     float ra[MI_PIPE_A];
     int64_t pg = 0, rs = 0;
@@ -605,7 +604,7 @@ __global__ __launch_bounds__(64) void k_loco_post_pipe(const KParams* __restrict
 #pragma unroll
         for (int r = 0; r < MI_PIPE_A; ++r) {
             const int kk = lane + 64 * r, e = div_small(kk, mag_a);
-            sobs[kk < TE * A ? e * O + ka + (kk - e * A) : trash - TE * g.P] = ra[r];
+            sobs[kk < TE * A ? e * O + ka + (kk - e * A) : trash_o] = ra[r];
         }
         const int64_t progress = pg + 1, rb = rs;          // rl_task.py:242
         const int nflag = nf;
