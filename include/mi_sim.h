@@ -264,6 +264,10 @@ int mi_fill_uniform(mi_sim* sim, float* out /*[N,cols]*/, int32_t cols, uint64_t
                     uint64_t step, float lo, float hi, void* stream);
 /* Per-env reset counters (the Philox counter of the reset noise stream) -> host [N]. */
 int mi_get_reset_count(mi_sim* sim, uint32_t* out /*[N] host*/);
+/* Host [N] -> the per-env reset counters (restores a recorded state, e.g. a golden fixture's,
+ * so the next reset draws the same Philox noise; no reference counterpart: torch's global
+ * generator state plays this role there, locomotion.py:120-124). Blocks the host. */
+int mi_set_reset_count(mi_sim* sim, const uint32_t* in /*[N] host*/);
 /* Number of env-steps whose physics produced a non-finite state and were forced to reset. */
 int mi_sim_nan_count(mi_sim* sim, int64_t* count);
 /* Diagnostics: which physics kernel runs. path: 0 one-lane-per-env, 1 wavefront-per-env;

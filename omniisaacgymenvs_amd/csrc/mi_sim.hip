@@ -1756,6 +1756,14 @@ int mi_get_reset_count(mi_sim* s, uint32_t* out) {
     return MI_OK;
 }
 
+int mi_set_reset_count(mi_sim* s, const uint32_t* in) {
+    NEED(s); NEED(in);
+    HIP_TRY(hipSetDevice(s->device));
+    HIP_TRY(hipDeviceSynchronize());
+    HIP_TRY(hipMemcpy(s->ds.reset_count, in, sizeof(uint32_t) * s->N, hipMemcpyHostToDevice));
+    return MI_OK;
+}
+
 int mi_sim_nan_count(mi_sim* s, int64_t* count) {
     NEED(s); NEED(count);
     HIP_TRY(hipSetDevice(s->device));

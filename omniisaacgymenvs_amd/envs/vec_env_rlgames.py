@@ -80,6 +80,7 @@ class VecEnvRLGames:
             # the fused launch may have bound task.obs_buf to a returned obs tensor (clip_obs =
             # inf, single write); the method-by-method path writes obs_buf in place
             self._task.obs_buf = self._task.obs_buf.clone()
+            self._task._obs_aliased = False
 
     # ------------------------------------------------------------------ RL API
     def _process_data(self) -> None:

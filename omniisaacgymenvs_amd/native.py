@@ -126,6 +126,7 @@ _SIGS = {
     "mi_fill_uniform": (C.c_int, [C.c_void_p, C.c_void_p, C.c_int32, C.c_uint64, C.c_uint64,
                                   C.c_float, C.c_float, C.c_void_p]),
     "mi_get_reset_count": (C.c_int, [C.c_void_p, C.c_void_p]),
+    "mi_set_reset_count": (C.c_int, [C.c_void_p, C.c_void_p]),
     "mi_sim_nan_count": (C.c_int, [C.c_void_p, _i64p]),
     "mi_sim_kernel_path": (C.c_int, [C.c_void_p, _i32p, _i32p, _i32p]),
     "mi_abi_version": (C.c_int, []),

@@ -153,9 +153,12 @@ class A2CAgent:
         # ranks' actors and broadcasts the weights back. (rl_games' multi_gpu runs a learner per
         # rank and averages gradients instead; here each rollout crosses xGMI once and there is
         # one optimizer.) num_actors stays the per-rank count, batch_size is the learner's.
-        self.world = (dist.get_world_size() if bool(cfg.get("multi_gpu", False)) and dist.is_available()
-                      and dist.is_initialized() else 1)
-        self.rank = dist.get_rank() if self.world > 1 else 0
+        # `distributed` also holds at world size 1 under an initialised process group (the
+        # single-GPU rehearsal of config 5's gather / broadcast path, tests/test_gpu_nccl.py)
+        self.distributed = (bool(cfg.get("multi_gpu", False)) and dist.is_available()
+                            and dist.is_initialized())
+        self.world = dist.get_world_size() if self.distributed else 1
+        self.rank = dist.get_rank() if self.distributed else 0
         self.is_learner = self.rank == 0
         self.batch_size = self.horizon * self.num_actors * self.world
         self.minibatch_size = int(cfg["minibatch_size"])
@@ -221,12 +224,12 @@ class A2CAgent:
         H, N, O, A = self.horizon, self.num_actors, self.num_obs, self.num_actions
         dev, f32 = self.device, torch.float32
         self.rollout = None
-        if self.world > 1:
+        if self.distributed:
             # the rollout buffers ARE the gather slab's fields (zero copy; one slab, so the
             # captured rollout graph keeps writing the same addresses)
             from ..utils.distributed import RolloutGather
             self.rollout = RolloutGather(H, N, O, dev, self.world, buffers=1, mode="gather", dst=0,
-                                         extra=self._SLAB_EXTRA(A))
+                                         extra=self._SLAB_EXTRA(A), with_done=False)
             v = self.rollout.slabs[0].views
             self.buf = {"obses": v["obs"], "rewards": v["rew"], "dones": v["dones_f"],
                         "actions": v["actions"].view(H, N, A), "neglogpacs": v["neglogpacs"],
@@ -262,7 +265,7 @@ class A2CAgent:
         self._mb_stats = torch.zeros((self.mini_epochs, self.num_minibatches, 5), device=dev, dtype=f32)
         self.epoch_num = 0
         self.frame = 0
-        if self.world > 1:
+        if self.distributed:
             self._broadcast_weights()   # every replica starts from the learner's initial weights
         self.last_mean_rewards = -100500.0
         self.stats: Dict[str, float] = {}
@@ -373,7 +376,7 @@ class A2CAgent:
                 self.graph.replay()
             else:
                 self._rollout_body()
-        self._global = self._gather_horizon() if self.world > 1 else None
+        self._global = self._gather_horizon() if self.distributed else None
         ep = self.episode_sums.cpu().numpy()           # the rollout's one host sync
         for cnt, rsum, lsum in ep:
             if cnt > 0:
@@ -397,7 +400,7 @@ class A2CAgent:
     # ------------------------------------------------------------------ training
     def prepare_dataset(self) -> Dict[str, torch.Tensor]:
         b, last_values, dones = self.buf, self.last_values, self.dones
-        if self.world > 1:             # the learner: every rank's actors, gathered
+        if self.distributed:             # the learner: every rank's actors, gathered
             b, last_values, dones = self._global
         adv, ret = ops.gae(b["rewards"], b["values"], b["dones"], last_values, dones,
                            self.gamma, self.tau)
@@ -584,7 +587,7 @@ class A2CAgent:
             a_loss_m, c_loss_m = torch.stack(a_l).mean().item(), torch.stack(c_l).mean().item()
             b_loss_m, ent_m = torch.stack(b_l).mean().item(), torch.stack(ents).mean().item()
             kl_m = torch.stack(kls).mean().item()
-        if self.world > 1:
+        if self.distributed:
             self._broadcast_weights()
         update_time = time.perf_counter() - t0
         self.frame += self.batch_size

@@ -51,7 +51,13 @@ class RLTask:
         self.cleanup()
 
     def cleanup(self) -> None:
-        """Torch buffers for RL data collection (rl_task.py:98-107)."""
+        """Torch buffers for RL data collection (rl_task.py:98-107).
+
+        ``obs_buf`` on the fused locomotion step (clip_obs = inf) is rebound to the fresh obs
+        tensor that step returns (one HBM write instead of two; LocomotionTask.fused_step): the
+        env never writes that tensor again, but an in-place change of the returned obs is visible
+        through ``obs_buf`` until the next step. With caller-provided output buffers it stays a
+        buffer of its own."""
         self.obs_buf = torch.zeros((self._num_envs, self.num_observations), device=self._device, dtype=torch.float)
         self.states_buf = torch.zeros((self._num_envs, self.num_states), device=self._device, dtype=torch.float)
         self.rew_buf = torch.zeros(self._num_envs, device=self._device, dtype=torch.float)

@@ -165,9 +165,18 @@ class LocomotionTask(RLTask):
         the copies _process_data hands back (vec_env_rlgames.py:41-46)."""
         a = actions.to(self._device, dtype=torch.float32).contiguous()
         obs_out, rew_out, reset_out = self._step_outputs(out)
-        # clip_obs = inf (locomotion default, rl_task.py:69): the clamped copy equals obs_buf, so
-        # the launch writes the row once and obs_buf becomes that tensor (no second HBM write)
-        single = math.isinf(self.clip_obs)
+        # clip_obs = inf (locomotion default, rl_task.py:69): the clamped copy equals obs_buf. With
+        # fresh output tensors (out is None) the launch writes the row once and obs_buf becomes
+        # that tensor: the env never writes it again (the next step returns another fresh
+        # tensor), so it behaves as the reference's returned .clone() (vec_env_rlgames.py:43) as
+        # long as the caller does not modify the returned obs in place and then read
+        # task.obs_buf. With caller buffers (a rollout slab row, a graph-pool tensor) obs_buf
+        # stays a persistent buffer of its own and the launch writes both
+        # (tests/test_gpu_parity.py::test_returned_obs_contract).
+        single = math.isinf(self.clip_obs) and out is None
+        if not single and getattr(self, "_obs_aliased", False):
+            self.obs_buf = torch.empty_like(self.obs_buf)   # never write a tensor handed out
+            self._obs_aliased = False
         N.check(N.lib().mi_env_step(self._h(), a.data_ptr(), int(self.control_frequency_inv),
                                     obs_out.data_ptr(), 0 if single else self.obs_buf.data_ptr(),
                                     self.rew_buf.data_ptr(),
@@ -177,5 +186,6 @@ class LocomotionTask(RLTask):
                                     self._stream()), "mi_env_step")
         if single:
             self.obs_buf = obs_out
+            self._obs_aliased = True
         return obs_out, rew_out, reset_out
 

@@ -45,11 +45,14 @@ def shard_range(rank: int, world: int, envs_per_rank: int) -> Tuple[int, int]:
     return rank * envs_per_rank, world * envs_per_rank
 
 
-def slab_fields(num_obs: int, extra: Sequence[Tuple[str, int, torch.dtype]] = ()):
+def slab_fields(num_obs: int, extra: Sequence[Tuple[str, int, torch.dtype]] = (),
+                with_done: bool = True):
     """Per-env fields of one slab row, 8-byte fields first: done i64, rew f32, obs f32 [O] — the
     dtypes VecEnvRLGames.step returns (vec_env_rlgames.py:41-46) — then any learner fields
-    (name, width, dtype)."""
-    f = [("done", 1, torch.int64), ("rew", 1, torch.float32), ("obs", num_obs, torch.float32)]
+    (name, width, dtype). ``with_done=False`` drops the i64 done field for a caller that keeps its
+    own done field (the learner's f32 ``dones_f``), so no unread bytes cross xGMI."""
+    f = [("done", 1, torch.int64)] if with_done else []
+    f += [("rew", 1, torch.float32), ("obs", num_obs, torch.float32)]
     f += [(n, w, d) for n, w, d in extra]
     return f
 
@@ -99,12 +102,13 @@ class RolloutGather:
 
     def __init__(self, horizon: int, n: int, num_obs: int, device, world: int, buffers: int = 2,
                  mode: str = "gather", dst: int = 0, rank: Optional[int] = None,
-                 extra: Sequence[Tuple[str, int, torch.dtype]] = ()):
+                 extra: Sequence[Tuple[str, int, torch.dtype]] = (), with_done: bool = True):
         if mode not in ("gather", "all_gather"):
             raise ValueError(f"mode must be 'gather' or 'all_gather' (got {mode!r})")
         self.H, self.n, self.O, self.world, self.mode, self.dst = horizon, n, num_obs, world, mode, dst
         self.rank = (dist.get_rank() if dist.is_initialized() else 0) if rank is None else rank
-        fields = slab_fields(num_obs, extra)
+        fields = slab_fields(num_obs, extra, with_done)
+        self.with_done = with_done
         self.slabs = [_Slab(horizon, n, fields, device) for _ in range(buffers)]
         # the learner (gather) or every rank (all_gather) holds [world, H, step_bytes]
         self.holds_output = mode == "all_gather" or self.rank == dst
@@ -129,7 +133,7 @@ class RolloutGather:
 
     def slot(self, h: int):
         s = self.slabs[self.active]
-        return s.obs[h], s.rew[h], s.done[h]
+        return s.obs[h], s.rew[h], (s.done[h] if self.with_done else None)
 
     def field(self, name: str, h: int) -> torch.Tensor:
         return self.slabs[self.active].views[name][h]

@@ -113,3 +113,34 @@ def task_params_from_cfg(task_name: str):
     tp._keep = (gears, ratio, init)
     tp.joint_gears, tp.motor_effort_ratio, tp.init_dof_pos = N.fptr(gears), N.fptr(ratio), N.fptr(init)
     return tp, m, (gears, ratio, init)
+
+
+def oracle_sensitivity(env, seed, actions, substeps, bufs_before, groups, rel=2.0 ** -22, rng_seed=0):
+    """Oracle-side estimate of how much this step amplifies rounding-level differences, per env
+    and observation group: an oracle twin of the device's CURRENT state (call before the device
+    steps) with root pose / velocity, q and qd each scaled by (1 + rel * u), u ~ U(-1, 1) (2 ulp
+    of float32), stepped with the same actions; returns ({group: [N] max |obs_pert - obs_ref|},
+    [N] |rew_pert - rew_ref|, the unperturbed twin's buffers). Contact / PGS conditioning
+    (stacked contacts, near-singular Delassus blocks) shows up here as a large value, so a
+    device-vs-oracle difference can be judged against the step's own conditioning rather than
+    against the device's measured error."""
+    import copy
+
+    rng = np.random.default_rng(rng_seed)
+    ref = oracle_twin(env, seed)
+    pert = oracle_twin(env, seed)
+    p, q, v = pert.root_state()
+    jq, jqd = pert.dof_state()
+    f = lambda a: (a * (1.0 + rel * rng.uniform(-1, 1, a.shape))).astype(np.float32)
+    if env.task.model.root_free:
+        pert.set_root_state(f(p), q, f(v))
+    pert.set_dof_state(f(jq), f(jqd))
+    b_ref, b_pert = copy.deepcopy(bufs_before), copy.deepcopy(bufs_before)
+    ref.env_step(actions, substeps, b_ref)
+    pert.env_step(actions, substeps, b_pert)
+    d = np.abs(b_pert["obs"] - b_ref["obs"])
+    out = {g: d[:, sl].max(axis=1) for g, sl in groups.items()}
+    rew = np.abs(b_pert["rew"] - b_ref["rew"])
+    ref.close()
+    pert.close()
+    return out, rew, b_ref

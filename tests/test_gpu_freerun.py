@@ -5,10 +5,19 @@ makes per-env comparison meaningless over long horizons, so this test compares t
 distributions a policy would see after `STEPS` free-running steps from the identical
 post-reset state with identical Philox actions (tools/free_run.py): per-step reward samples
 (two-sample KS statistic and the mean), completed-episode lengths (KS, count, mean) and the
-per-step reset rate (locomotion.py:257-321, cartpole.py:143-162). Bounds are ~5-10x the
-measured values: Humanoid reward KS 2e-4, episode-length KS 6e-4; Ant reward KS
-1.5e-3 (Ant rarely falls in 200 random steps, so its episode statistics are count-only);
-Cartpole identical.
+per-step reset rate (locomotion.py:257-321, cartpole.py:143-162).
+
+Bounds are ~10x the values measured at round-2 HEAD (profiles/r02/free_run_{h,a,c}.log), per
+task:
+
+  task      reward KS   reward-mean rel.diff   reset-rate max diff   episodes (dev / orc)   ep-len KS   ep-len mean rel.diff
+  Humanoid  2.05e-4     9.6e-6                 1.2e-4                28078 / 28093          6.3e-4      4.7e-5
+  Ant       1.46e-3     3.5e-3                 6.1e-5                29 / 32                (29 episodes: count only)
+  Cartpole  3.3e-6      8e-8                   0                     80969 / 80969          0           0
+
+Ant rarely falls in 200 random steps, so its episode statistics are a count check only. The
+two runs share actions and every reset's Philox noise, so they stay strongly correlated: these
+bounds sit below the sampling noise of two independent runs and would catch a biased device.
 """
 import pytest
 
@@ -16,17 +25,26 @@ from tools.free_run import free_run
 
 pytestmark = pytest.mark.gpu
 
+BOUNDS = {
+    #            reward_ks  reward_mean_rel  reset_rate  episodes_abs  ep_len_ks  ep_len_mean_rel
+    "Humanoid": (2e-3, 1e-3, 1.2e-3, 150, 6e-3, 5e-4),
+    "Ant": (1.5e-2, 3.5e-2, 6e-4, 8, None, None),
+    "Cartpole": (1e-4, 1e-5, 1e-4, 8, 1e-3, 1e-4),
+}
+
 
 @pytest.mark.parametrize("name,steps", [("Humanoid", 200), ("Ant", 200), ("Cartpole", 300)])
 def test_free_running_distributions_match_oracle(gpu, name, steps):
+    ks, mean_rel, rate, ep_abs, len_ks, len_rel = BOUNDS[name]
     r = free_run(name, 4096, steps)
-    assert r["reward_ks"] <= 0.01, r
+    assert r["reward_ks"] <= ks, r
     dm, om = r["reward_mean"]
-    assert abs(dm - om) <= 0.01 * max(abs(om), 0.1), r
-    assert r["reset_rate_window_maxdiff"] <= 0.005, r
+    assert abs(dm - om) <= mean_rel * max(abs(om), 0.1), r
+    assert r["reset_rate_window_maxdiff"] <= rate, r
     nd, no = r["episodes"]
-    assert abs(nd - no) <= max(8, 0.03 * no), r
-    if no >= 1000:
-        assert r["episode_len_ks"] <= 0.02, r
+    assert abs(nd - no) <= ep_abs, r
+    if len_ks is not None:
+        assert no >= 1000, r
+        assert r["episode_len_ks"] <= len_ks, r
         ld, lo = r["episode_len_mean"]
-        assert abs(ld - lo) <= 0.02 * lo, r
+        assert abs(ld - lo) <= len_rel * lo, r

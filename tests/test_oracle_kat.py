@@ -164,3 +164,155 @@ def test_kat8_reset_timing():
     orc.env_step(np.zeros((n, 21), np.float32), 2, b)                     # t+1 re-inits env 0
     assert b["progress"][0] == 1 and b["reset"][0] == 0
     assert b["obs"][0, 0] > 1.0
+
+
+# --------------------------------------------------------------------------------------------
+# Multi-formula KATs, each derived by hand from the reference text:
+#   get_observations  tasks/shared/locomotion.py:219-252 (to_target z zeroed, potentials =
+#                     -|to_target|/dt, compute_heading_and_up / compute_rot, unscale, the obs cat)
+#   calculate_metrics tasks/shared/locomotion.py:290-320; Humanoid limit cost tasks/humanoid.py:120-127
+# with dt = 1/60 (locomotion.py:163) and the wxyz quaternion convention. Expected values are
+# computed here in float64 from closed forms (rotations by hand), not by calling the oracle.
+
+def _pose(task, pos, quat, vel=None, q=None, qd=None, sens=None, act=None, prev=None):
+    tp, m, (gears, ratio, _) = task_params_from_cfg(task)
+    D, S = m.num_dof, m.num_sensors
+    lim = m.dof_limits()
+    mid = (0.5 * (lim[:, 0] + lim[:, 1]))[None, :]
+    pos = np.asarray(pos, np.float32)[None, :]
+    # the potential at this position as the reference's float32 tensors compute it:
+    # -norm(to_target) / dt with dt = 1/60 a float32 (locomotion.py:163, :223)
+    tx, ty = np.float32(1000.0) - pos[0, 0], np.float32(0.0) - pos[0, 1]
+    pot_here = -np.sqrt(tx * tx + ty * ty) / np.float32(1 / 60)
+    out = loco_post_math(tp, pos, np.asarray(quat, np.float32)[None, :],
+                         np.zeros((1, 6), np.float32) if vel is None else np.asarray(vel, np.float32)[None, :],
+                         mid.astype(np.float32) if q is None else q,
+                         np.zeros((1, D), np.float32) if qd is None else qd,
+                         np.zeros((1, S, 6), np.float32) if sens is None else sens,
+                         np.zeros((1, D), np.float32) if act is None else act,
+                         lim[:, 0], lim[:, 1], np.zeros(1), np.zeros(1),
+                         np.full(1, pot_here if prev is None else prev, np.float32),
+                         np.full(1, pot_here if prev is None else prev, np.float32))
+    return tp, m, ratio, out
+
+
+def _yaw_quat(deg):
+    h = math.radians(deg) / 2
+    return [math.cos(h), 0.0, 0.0, math.sin(h)]
+
+
+def _wrap(a):
+    return math.atan2(math.sin(a), math.cos(a))   # normalize_angle, locomotion.py:190-192
+
+
+@pytest.mark.parametrize("task", ["Humanoid", "Ant"])
+@pytest.mark.parametrize("yaw_deg", [90.0, 45.0, 200.0])
+def test_kat9_yawed_torso(task, yaw_deg):
+    """Torso yawed about z by psi at (x, y, z): heading_vec = (cos psi, sin psi, 0), up_vec = e_z
+    (compute_heading_and_up), so obs7 = wrap(psi) (get_euler_xyz yaw mod 2 pi, then
+    normalize_angle), obs8 = 0, obs10 = 1, obs11 = heading_vec . (1000 - x, -y)/|.|, and obs9 =
+    wrap(atan2(0 - z, 1000 - x) - psi) (compute_rot's atan2(z, x) target angle)."""
+    x, y, z = 4.0, -3.0, 1.1
+    psi = math.radians(yaw_deg)
+    tp, m, ratio, r = _pose(task, (x, y, z), _yaw_quat(yaw_deg))
+    o = r["obs"][0]
+    tx, ty = 1000.0 - x, -y
+    L = math.hypot(tx, ty)
+    np.testing.assert_allclose(o[7], _wrap(psi), atol=2e-6)
+    np.testing.assert_allclose(o[8], 0.0, atol=1e-6)
+    np.testing.assert_allclose(o[9], _wrap(math.atan2(-z, tx) - psi), atol=2e-6)
+    np.testing.assert_allclose(o[10], 1.0, atol=1e-6)
+    np.testing.assert_allclose(o[11], (math.cos(psi) * tx + math.sin(psi) * ty) / L, atol=2e-6)
+    # reward: heading term switches to hw * obs11 / 0.8 below 0.8 (locomotion.py:290-293)
+    h = (math.cos(psi) * tx + math.sin(psi) * ty) / L
+    heading = tp.heading_weight if h > 0.8 else tp.heading_weight * h / 0.8
+    expect = tp.alive_reward_scale + tp.up_weight + heading     # progress 0, mid-range joints
+    np.testing.assert_allclose(r["rew"][0], expect, atol=2e-6)
+
+
+@pytest.mark.parametrize("task", ["Humanoid", "Ant"])
+def test_kat10_moving_tilted_torso_local_frame(task):
+    """Torso yawed +90 deg: quat_rotate_inverse maps world (vx, vy, vz) to (vy, -vx, vz) (a
+    rotation by -90 deg about z); obs1-3 = that, obs4-6 = the same map of the angular velocity
+    times angularVelocityScale (locomotion.py:239-240). A +30 deg roll about x instead: up_vec =
+    (0, -sin 30, cos 30) -> obs10 = cos 30 < 0.93 -> no up reward (locomotion.py:296-297), obs8 =
+    pi/6, and obs1-3 = (vx, vy cos30 + vz sin30, -vy sin30 + vz cos30)."""
+    v, w = (1.0, 2.0, 3.0), (0.1, -0.2, 0.3)
+    tp, m, ratio, r = _pose(task, (0.0, 0.0, 1.3), _yaw_quat(90.0), vel=[*v, *w])
+    o = r["obs"][0]
+    s = tp.angular_velocity_scale
+    np.testing.assert_allclose(o[1:4], [v[1], -v[0], v[2]], atol=1e-5)
+    np.testing.assert_allclose(o[4:7], [s * w[1], -s * w[0], s * w[2]], atol=1e-6)
+    np.testing.assert_allclose(o[0], 1.3, atol=0)
+    c, sn = math.cos(math.radians(30)), math.sin(math.radians(30))
+    roll_q = [math.cos(math.radians(15)), math.sin(math.radians(15)), 0.0, 0.0]
+    tp, m, ratio, r = _pose(task, (0.0, 0.0, 1.3), roll_q, vel=[*v, *w])
+    o = r["obs"][0]
+    np.testing.assert_allclose(o[1:4], [v[0], v[1] * c + v[2] * sn, -v[1] * sn + v[2] * c], atol=1e-5)
+    np.testing.assert_allclose(o[4:7], [s * w[0], s * (w[1] * c + w[2] * sn), s * (-w[1] * sn + w[2] * c)],
+                               atol=1e-6)
+    np.testing.assert_allclose(o[8], math.pi / 6, atol=2e-6)
+    np.testing.assert_allclose(o[7], 0.0, atol=1e-6)
+    np.testing.assert_allclose(o[10], c, atol=1e-6)
+    np.testing.assert_allclose(o[11], 1.0, atol=1e-6)        # heading_vec stays e_x
+    expect = tp.alive_reward_scale + 0.0 + tp.heading_weight   # up_proj 0.866 < 0.93
+    np.testing.assert_allclose(r["rew"][0], expect, atol=2e-6)
+
+
+@pytest.mark.parametrize("task", ["Humanoid", "Ant"])
+def test_kat11_dof_and_sensor_scaling(task):
+    """obs[12+D:12+2D] = qd * dofVelocityScale, obs[12+2D:12+2D+6S] = sensors (row-major [S, 6])
+    * contactForceScale, obs[12+2D+6S:] = actions (locomotion.py:246-249)."""
+    tp0, m, _, _ = _pose(task, (0.0, 0.0, 1.3), [1, 0, 0, 0])
+    D, S = m.num_dof, m.num_sensors
+    qd = np.linspace(-3.0, 4.0, D, dtype=np.float32)[None, :]
+    sens = np.arange(S * 6, dtype=np.float32).reshape(1, S, 6) * 7.5 - 40.0
+    act = np.linspace(-1.0, 1.0, D, dtype=np.float32)[None, :]
+    tp, m, ratio, r = _pose(task, (0.0, 0.0, 1.3), [1, 0, 0, 0], qd=qd, sens=sens, act=act)
+    o = r["obs"][0]
+    np.testing.assert_allclose(o[12 + D:12 + 2 * D], qd[0].astype(np.float64) * tp.dof_vel_scale, rtol=1e-6)
+    np.testing.assert_allclose(o[12 + 2 * D:12 + 2 * D + 6 * S],
+                               sens.reshape(-1).astype(np.float64) * tp.contact_force_scale, rtol=1e-6, atol=1e-7)
+    np.testing.assert_array_equal(o[12 + 2 * D + 6 * S:], act[0])
+    assert o.shape[0] == 12 + 3 * D + 6 * S == tp.num_obs
+
+
+@pytest.mark.parametrize("task", ["Humanoid", "Ant"])
+def test_kat12_full_reward_moving_actions_velocities(task):
+    """Every reward term at once (locomotion.py:290-320): torso yawed 45 deg (heading below 0.8:
+    hw * cos45 / 0.8), moved 0.1 m toward the target since the previous potential (progress =
+    (|to_target_prev| - |to_target|) / dt = 6), non-zero actions and DOF velocities (action cost
+    ac * sum a^2, electricity ec * sum |a * qd * dofVelocityScale| * ratio), one joint at 0.995 of
+    its range (Humanoid: 0.25 * (0.995 - 0.98) / 0.02 * ratio_j, humanoid.py:120-127; Ant: counts
+    unscaled > 0.99, ant.py:92-95)."""
+    tp0, m, ratio, _ = _pose(task, (0.0, 0.0, 1.3), [1, 0, 0, 0])
+    D = m.num_dof
+    lim = m.dof_limits().astype(np.float64)
+    lo, hi = lim[:, 0], lim[:, 1]
+    q = 0.5 * (lo + hi)
+    j = 2
+    q[j] = 0.5 * (0.995 * (hi[j] - lo[j]) + hi[j] + lo[j])  # unscale -> 0.995
+    act = np.array([(-1) ** k * (0.1 + 0.8 * k / D) for k in range(D)], np.float32)[None, :]
+    qd = np.array([0.5 + 0.3 * k for k in range(D)], np.float32)[None, :] * np.where(np.arange(D) % 3 == 0, -1, 1)
+    prev = -np.float32(1000.0) / np.float32(1 / 60)            # potential at x = 0, y = 0
+    tp, m, ratio, r = _pose(task, (0.1, 0.0, 1.3), _yaw_quat(45.0), q=q[None, :].astype(np.float32),
+                            qd=qd.astype(np.float32), act=act, prev=prev)
+    a64, qd64 = act[0].astype(np.float64), qd[0].astype(np.float64)
+    progress = (1000.0 - 999.9) * 60.0
+    heading = tp.heading_weight * math.cos(math.radians(45.0)) / 0.8
+    act_cost = float(np.sum(a64 ** 2))
+    elec = float(np.sum(np.abs(a64 * qd64 * tp.dof_vel_scale) * np.asarray(ratio, np.float64)))
+    if task == "Humanoid":
+        limit = tp.joints_at_limit_cost * (0.995 - 0.98) / 0.02 * float(ratio[j])
+    else:
+        limit = 1.0
+    expect = (progress + tp.alive_reward_scale + tp.up_weight + heading
+              - tp.actions_cost * act_cost - tp.energy_cost * elec - limit)
+    # float32 potentials are ~6e4 in magnitude (ulp 3.9e-3): the progress term carries that error
+    np.testing.assert_allclose(r["rew"][0], expect, atol=1.2e-2)
+    # the same step without the progress term pins every other term to float32 rounding
+    tp, m, ratio, r0 = _pose(task, (0.1, 0.0, 1.3), _yaw_quat(45.0), q=q[None, :].astype(np.float32),
+                             qd=qd.astype(np.float32), act=act)
+    np.testing.assert_allclose(r0["rew"][0], expect - progress, atol=2e-5)
+    np.testing.assert_allclose(r["pot"][0] - prev, progress, atol=1.2e-2)
+    assert r["prev"][0] == prev

@@ -1,6 +1,6 @@
 #!/usr/bin/env python3
 """Correction factors of FETCH_SIZE / WRITE_SIZE per access width, from the rocprofv3 passes of
-tools/fetch_calib (tools/gpu_calib.sh).
+tools/fetch_calib (tools/gpu.sh calib).
 
     python tools/calib_summary.py gpurun_out [--out profiles/r02/fetch_calib.json]
 

@@ -1,5 +1,5 @@
 #!/usr/bin/env python3
-"""Copy the judged summaries of a tools/gpu_profile.sh run from gpurun_out/ into profiles/<round>/:
+"""Copy the judged summaries of a tools/gpu.sh run from gpurun_out/ into profiles/<round>/:
 rocprofv3 kernel stats per task, PMC traffic (also profiles/traffic_<task>.json, read by
 bench.py), SQ issue/wait counters, phase-stamp breakdowns and the default bench line.
 

@@ -5,11 +5,15 @@ The reference has no tests and no vectors, and importing it is denied (DESIGN.md
 fixtures come from the build's own oracle. Each fixture records the model/config hashes and
 the seed, so a change to the assets or the oracle is visible as a diff.
 
-For each task: 32 envs of the composed task config, seed 42, GridCloner origins. Step 0 is
-VecEnvRLGames.reset (reset_buf = 1, zero actions); steps 1..3 use U(-1, 1) actions drawn from
-numpy's PCG64(seed). Task creation's post_reset (one reset_idx of every env) runs first.
-Per step: the clamped obs, reward, reset / progress masks, the physics
-state and the oracle's contact-decision margins.
+For each task: 256 envs of the composed task config, seed 42, GridCloner origins. Step 0 is
+VecEnvRLGames.reset (reset_buf = 1, zero actions); steps 1..23 use U(-1, 1) actions drawn from
+numpy's PCG64(seed) (Humanoids start to fall at step 17 under these actions, so the last steps
+carry terminations and the re-initialisation of the reset envs). Task creation's post_reset (one reset_idx of every env) runs first.
+Per step: the clamped obs, reward, reset / progress masks, potentials, the physics state, the
+per-env reset counters (the Philox counter of the reset noise), the oracle's contact-decision
+margins and, for a self-colliding model, the smallest self-pair surface gap (< contact_offset:
+a self contact is active). Everything a device needs to restart from step k's state is stored,
+so the GPU test can check every step from the fixture's own state (tests/test_golden.py).
 
     python tools/make_golden.py            # (re)write tests/golden/*.npz + manifest.json
 """
@@ -24,7 +28,7 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
 GOLDEN = os.path.join(ROOT, "tests", "golden")
 TASKS = ("Cartpole", "Ant", "Humanoid")
-N_ENVS, SEED, STEPS = 32, 42, 3
+N_ENVS, SEED, STEPS = 256, 42, 23
 ASSETS = {"Cartpole": "cartpole.xml", "Ant": "ant.xml", "Humanoid": "humanoid.xml"}
 
 
@@ -55,22 +59,27 @@ def run(task: str):
     orc.reset_idx(np.arange(N_ENVS), b)
     b["reset"][:] = 1                                        # VecEnv.reset (rl_task.py:218-221)
     rng = np.random.Generator(np.random.PCG64(SEED))
-    rec = {k: [] for k in ("actions", "obs", "rew", "reset", "progress", "root_pos", "root_quat",
-                           "root_vel", "q", "qd", "margin")}
+    rec = {k: [] for k in ("actions", "obs", "rew", "reset", "progress", "pot", "prev", "root_pos",
+                           "root_quat", "root_vel", "q", "qd", "reset_count", "margin", "self_gap")}
     for step in range(STEPS + 1):
         a = np.zeros((N_ENVS, tp.num_actions), np.float32) if step == 0 else \
             rng.uniform(-1.0, 1.0, (N_ENVS, tp.num_actions)).astype(np.float32)
         orc.env_step(a, 2, b)
         p, qt, v = orc.root_state()
         q, qd = orc.dof_state()
+        gap = np.array([orc.self_min_gap(i) for i in range(N_ENVS)], np.float32) \
+            if sp.enable_self_collisions else np.full(N_ENVS, np.inf, np.float32)
         for k, x in (("actions", a), ("obs", b["obs"]), ("rew", b["rew"]), ("reset", b["reset"]),
-                     ("progress", b["progress"]), ("root_pos", p), ("root_quat", qt),
-                     ("root_vel", v), ("q", q), ("qd", qd), ("margin", orc.decision_margin())):
+                     ("progress", b["progress"]), ("pot", b["pot"]), ("prev", b["prev"]),
+                     ("root_pos", p), ("root_quat", qt), ("root_vel", v), ("q", q), ("qd", qd),
+                     ("reset_count", orc.reset_count()), ("margin", orc.decision_margin()),
+                     ("self_gap", gap)):
             rec[k].append(np.array(x, copy=True))
     arrays = {k: np.stack(v) for k, v in rec.items()}
     arrays["origins"] = origins
     meta = {"task": task, "num_envs": N_ENVS, "seed": SEED, "steps": STEPS + 1, "substeps": 2,
             "enable_self_collisions": int(sp.enable_self_collisions),
+            "contact_offset": float(sp.contact_offset),
             "model_sha256": sha256(os.path.join(ROOT, "omniisaacgymenvs_amd", "robots", "assets",
                                                 ASSETS[task])),
             "task_cfg_sha256": sha256(os.path.join(ROOT, "omniisaacgymenvs_amd", "cfg", "task",

@@ -21,7 +21,7 @@ def main():
     from omniisaacgymenvs_amd import native as N
     from omniisaacgymenvs_amd.utils.task_util import make_env
     from oracle.oracle import lib as orc_lib
-    from tests.helpers import oracle_twin, sync_oracle, task_buffers
+    from tests.helpers import oracle_sensitivity, oracle_twin, sync_oracle, task_buffers
 
     task_name = sys.argv[1] if len(sys.argv) > 1 else "Humanoid"
     n = int(sys.argv[2]) if len(sys.argv) > 2 else 4096
@@ -50,10 +50,17 @@ def main():
         groups = {"root": slice(0, 12), "dof_pos": slice(12, 12 + D), "dof_vel": slice(12 + D, 12 + 2 * D),
                   "sensors": slice(12 + 2 * D, 12 + 2 * D + 6 * S), "actions": slice(12 + 2 * D + 6 * S, None)}
     gerr = {g: [] for g in list(groups) + ["rew"]}
-    errs, margins = [], []
+    gsens = {g: [] for g in list(groups) + ["rew"]}
+    errs, margins, senss = [], [], []
     for k in range(3, 3 + steps):
         b = task_buffers(env)
         a = acts(k)
+        # oracle-side conditioning of this step (tests/helpers.py oracle_sensitivity)
+        sg, sr, _ = oracle_sensitivity(env, 3, a.cpu().numpy(), task.control_frequency_inv, b, groups)
+        for g in groups:
+            gsens[g].append(sg[g])
+        gsens["rew"].append(sr)
+        senss.append(np.maximum(np.max(np.stack(list(sg.values())), axis=0), sr))
         o, r, d, _ = env.step(a)
         torch.cuda.synchronize()
         orc.env_step(a.cpu().numpy(), task.control_frequency_inv, b)
@@ -68,15 +75,24 @@ def main():
         sync_oracle(env, orc)
     e = np.concatenate(errs)
     m = np.concatenate(margins)
+    sens = np.concatenate(senss)
     q = {f"q{p}": float(np.quantile(e, p / 100)) for p in (50, 90, 99, 99.9)}
     far = m >= 1e-4
     worst = np.argsort(-np.where(far, e, 0))[:8]
     out = {"task": task_name, "envs": n, "steps": steps, **q, "max": float(e.max()),
            "max_far_from_threshold": float(e[far].max()) if far.any() else None,
            "frac_gt_2e-3_far": float((e[far] > 2e-3).mean()) if far.any() else None,
-           "worst_far": [(int(i % n), int(i // n), float(e[i]), float(m[i])) for i in worst],
+           "worst_far": [(int(i % n), int(i // n), float(e[i]), float(m[i]), float(sens[i])) for i in worst],
+           # far envs: error vs the oracle's own rounding sensitivity (2-ulp input perturbation)
+           "sens_quantiles": {f"q{p}": float(np.quantile(sens, p / 100)) for p in (50, 99, 99.9)},
+           "ratio_err_over_sens_far": {f"q{p}": float(np.quantile(e[far] / np.maximum(sens[far], 1e-7), p / 100))
+                                       for p in (50, 99, 99.9, 100)},
+           "max_far_err_where_sens_lt_2e-4": float(e[far & (sens < 2e-4)].max()) if (far & (sens < 2e-4)).any() else None,
+           "frac_far_sens_ge_2e-4": float((sens[far] >= 2e-4).mean()) if far.any() else None,
            "groups": {g: {f"q{p}": float(np.quantile(np.concatenate(v), p / 100)) for p in (50, 99)} |
-                      {"max_far": float(np.concatenate(v)[far].max()) if far.any() else None}
+                      {"max_far": float(np.concatenate(v)[far].max()) if far.any() else None,
+                       "max_far_ratio_to_sens": float((np.concatenate(v)[far] / np.maximum(
+                           np.concatenate(gsens[g])[far], 1e-6)).max()) if far.any() else None}
                       for g, v in gerr.items()}}
     print(json.dumps(out), flush=True)
     orc.close()

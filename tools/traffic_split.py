@@ -1,6 +1,6 @@
 #!/usr/bin/env python3
 """Per-launch HBM traffic of the fused env-step kernel, split into instruction fetch, per-env
-reads and per-env writes, from the env-count sweep of tools/gpu_traffic_sweep.sh.
+reads and per-env writes, from the env-count sweep of tools/gpu.sh traffic.
 
     python tools/traffic_split.py <Task> <sweep_dir> [--n 4096] [--out profiles/traffic_<task>.json]
 
