@@ -139,18 +139,7 @@ class ShardLoop:
                 "bytes": (r.bytes_sent - b0) if r is not None else 0}
 
 
-def cpu_baseline(task_name: str, env, seconds: float) -> dict:
-    """Time the CPU oracle's fused env step on a bounded sample of the same workload: per thread
-    count, warm-up steps then the median of 3 timed runs (contract: ~10-30 s of CPU work in all,
-    instead of BASELINE.md's 200 / 2000 / median-of-5, which would take minutes per leg)."""
-    import numpy as np
-    from oracle.oracle import OracleSim, lib as orc_lib, make_buffers
-
-    task = env.task
-    n = min(task.num_envs, 256 if task_name != "Cartpole" else 4096)
-    origins = task.env_pos_cpu[:n]
-    view = task.get_robot()
-    results = {}
+def _cpu_share() -> int:
     ncpu = os.cpu_count() or 1
     try:
         ncpu = len(os.sched_getaffinity(0))
@@ -158,65 +147,114 @@ def cpu_baseline(task_name: str, env, seconds: float) -> dict:
         pass
     # the GPU box exposes the whole machine's CPUs but grants this job a share
     # (OMP_NUM_THREADS=16 there); never oversubscribe that share
-    ncpu = min(ncpu, int(os.environ.get("OMP_NUM_THREADS", ncpu)))
+    return min(ncpu, int(os.environ.get("OMP_NUM_THREADS", ncpu)))
+
+
+WARM, TIMED, RUNS = 200, 2000, 5   # BASELINE.md / SURVEY §8(d) protocol
+
+
+def cpu_baseline(task_name: str, env, seconds: float) -> dict:
+    """The CPU baselines, each on BASELINE.md's protocol (200 warm-up env-steps, then the median
+    of 5 runs of 2000 timed env-steps), on a bounded sample so the whole leg stays within
+    `seconds`:
+      * the C oracle's fused step of the metric's task (oracle/oracle.c, the build's CPU
+        restatement: the reference's PhysX-CPU path is closed and absent) at 1, 4 and all granted
+        threads, with the env count scaled per thread count to the time budget;
+      * config 1 (Cartpole, 16 envs): the reference's Cartpole task as torch ops on CPU tensors
+        (oracle/torch_cartpole.py, CPU torch as the reference's pipeline=cpu runs it) and the C
+        oracle, 1 thread each."""
+    import numpy as np
+    from oracle.oracle import OracleSim, lib as orc_lib, make_buffers
+
+    task = env.task
+    view = task.get_robot()
+    ncpu = _cpu_share()
     sweep = sorted({1, min(4, ncpu), ncpu})
     rng = np.random.default_rng(0)
-    warm = 20
+    per_leg = 0.8 * seconds / len(sweep)
+
+    def protocol(step_fn, n):
+        for k in range(WARM):
+            step_fn(k)
+        runs = []
+        for _ in range(RUNS):
+            t0 = time.perf_counter()
+            for k in range(TIMED):
+                step_fn(k)
+            runs.append(n * TIMED / (time.perf_counter() - t0))
+        return statistics.median(runs)
+
+    results = {}
     for threads in sweep:
         orc_lib().orc_set_threads(threads)
-        orc = OracleSim(task.model, view.sim_params, n, origins, seed=42)
-        orc.configure(task.task_params(), keep=task)
-        b = make_buffers(n, task.num_observations, task.num_actions)
-        acts = rng.uniform(-1, 1, (8, n, task.num_actions)).astype(np.float32)
+
+        def make(n):
+            orc = OracleSim(task.model, view.sim_params, n, task.env_pos_cpu[:n], seed=42)
+            orc.configure(task.task_params(), keep=task)
+            return orc, make_buffers(n, task.num_observations, task.num_actions)
+        # calibrate: cost of one env-step per env at this thread count, then size the sample
+        orc, b = make(threads)
+        acts = rng.uniform(-1, 1, (8, threads, task.num_actions)).astype(np.float32)
         t0 = time.perf_counter()
-        for k in range(warm):   # warm-up (first resets, caches)
+        for k in range(20):
             orc.env_step(acts[k % 8], task.control_frequency_inv, b)
-        per_step = (time.perf_counter() - t0) / warm
-        budget = seconds / len(sweep) / 3
-        steps = max(3, int(budget / per_step))
-        runs = []
-        for _ in range(3):
-            t0 = time.perf_counter()
-            for k in range(steps):
-                orc.env_step(acts[k % 8], task.control_frequency_inv, b)
-            runs.append(n * steps / (time.perf_counter() - t0))
-        results[threads] = (statistics.median(runs), steps)
+        per_env_step = (time.perf_counter() - t0) / (20 * threads)
         orc.close()
-    v1, steps1 = results[1]
-    # BASELINE config 1 (Cartpole, 16 envs, CPU): small enough for BASELINE.md's full protocol
-    # (200 warm-up, 2000 timed env-steps, median of 5), 1 thread
+        total = WARM + RUNS * TIMED
+        n = int(per_leg / (total * per_env_step)) // threads * threads
+        n = max(threads, min(n, 256, task.num_envs))
+        orc, b = make(n)
+        acts = rng.uniform(-1, 1, (8, n, task.num_actions)).astype(np.float32)
+        v = protocol(lambda k: orc.env_step(acts[k % 8], task.control_frequency_inv, b), n)
+        orc.close()
+        results[threads] = (v, n)
+    v1, n1 = results[1]
     orc_lib().orc_set_threads(1)
-    c1 = None
+    c1 = c1t = None
     try:
+        import torch
         from omniisaacgymenvs_amd.robots.articulations import GridCloner
+        from oracle.torch_cartpole import CpuTorchCartpole
         from tests.helpers import sim_params, task_params_from_cfg
         tp1, m1, _ = task_params_from_cfg("Cartpole")
-        orc = OracleSim(m1, sim_params(rest_offset=0.001), 16, GridCloner(4.0).get_clone_positions(16), seed=42)
+        sp1 = sim_params(rest_offset=0.001)
+        orc = OracleSim(m1, sp1, 16, GridCloner(4.0).get_clone_positions(16), seed=42)
         orc.configure(tp1)
         b1 = make_buffers(16, tp1.num_obs, tp1.num_actions)
         a1 = rng.uniform(-1, 1, (8, 16, tp1.num_actions)).astype(np.float32)
-        for k in range(200):
-            orc.env_step(a1[k % 8], 2, b1)
-        runs = []
-        for _ in range(5):
-            t0 = time.perf_counter()
-            for k in range(2000):
-                orc.env_step(a1[k % 8], 2, b1)
-            runs.append(16 * 2000 / (time.perf_counter() - t0))
+        c1 = {"value": round(protocol(lambda k: orc.env_step(a1[k % 8], 2, b1), 16), 1),
+              "unit": "env-steps/s", "cores": 1, "kind": "port",
+              "sample": "Cartpole 16 envs, 200 warm-up + median of 5 x 2000 env-steps (BASELINE.md "
+                        "protocol), C oracle fused step (2 substeps)"}
         orc.close()
-        c1 = {"value": round(statistics.median(runs), 1), "unit": "env-steps/s", "cores": 1,
-              "sample": "Cartpole 16 envs, 200 warm-up + median of 5 x 2000 env-steps (BASELINE.md protocol), "
-                        "oracle fused step (2 substeps)"}
+        threads0 = torch.get_num_threads()
+        torch.set_num_threads(1)
+        try:
+            torch.manual_seed(42)
+            ct = CpuTorchCartpole(m1, sp1, tp1, 16, seed=42, noise="torch")
+            ct.reset()
+            at = [torch.from_numpy(a1[k]) for k in range(8)]
+            c1t = {"value": round(protocol(lambda k: ct.step(at[k % 8]), 16), 1), "unit": "env-steps/s",
+                   "cores": 1, "kind": "port",
+                   "sample": "Cartpole 16 envs on CPU torch (oracle/torch_cartpole.py: the reference's "
+                             "cartpole.py:80-162 task ops + VecEnvRLGames.step sequence, analytic "
+                             "dynamics, torch.rand resets), 200 warm-up + median of 5 x 2000 env-steps, "
+                             "1 torch thread"}
+        finally:
+            torch.set_num_threads(threads0)
     except Exception as e:   # noqa: BLE001 - the side leg must not sink the bench line
-        c1 = {"error": str(e)}
+        c1 = c1 or {"error": str(e)}
+        c1t = c1t or {"error": str(e)}
     return {
         "value": round(v1, 1), "unit": "env-steps/s", "cores": 1, "kind": "port",
-        "sample": f"{task_name} {n} envs, {warm} warm-up + median of 3 x {steps1} env-steps, 1 thread; "
-                  f"oracle/oracle.c fused step (2 substeps). Algorithm: the oracle's dense CRBA + "
-                  f"Cholesky articulated step (device: tree LTDL), same contacts / limits / PGS and task "
-                  f"math. Protocol: bounded sample, not BASELINE.md's 200 / 2000 / median-of-5",
+        "sample": f"{task_name} {n1} envs (sample sized to the time budget), {WARM} warm-up + median of "
+                  f"{RUNS} x {TIMED} env-steps (BASELINE.md protocol), 1 thread; oracle/oracle.c fused step "
+                  f"(2 substeps). Algorithm: the oracle's dense CRBA + Cholesky articulated step (device: "
+                  f"tree LTDL), same contacts / limits / PGS and task math",
         "threads_sweep": {str(t): round(v[0], 1) for t, v in results.items()},
+        "threads_sweep_envs": {str(t): v[1] for t, v in results.items()},
         "config1_cartpole16": c1,
+        "config1_cpu_torch": c1t,
     }
 
 

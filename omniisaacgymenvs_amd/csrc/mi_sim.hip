@@ -673,8 +673,10 @@ __global__ __launch_bounds__(64) void k_loco_post_pipe(const KParams* __restrict
 #undef MI_PIPE_ISSUE
 }
 
+// register budget of the wave kernels: TopoCT::kWaves waves per SIMD
+#define MI_WAVE_OCC __attribute__((amdgpu_waves_per_eu(T::kWaves, T::kWaves)))
 template <class T>
-__global__ __launch_bounds__(256) void k_sim_step_wave(const KParams* __restrict__ kp, int substeps) {
+__global__ __launch_bounds__(256) MI_WAVE_OCC void k_sim_step_wave(const KParams* __restrict__ kp, int substeps) {
     extern __shared__ __attribute__((aligned(16))) float smem[];
     const WaveTabs& t = kp->t;
     const int i = wave_env();
@@ -689,7 +691,7 @@ __global__ __launch_bounds__(256) void k_sim_step_wave(const KParams* __restrict
 }
 
 template <class T>
-__global__ __launch_bounds__(256) void k_env_step_wave(const KParams* __restrict__ kp,
+__global__ __launch_bounds__(256) MI_WAVE_OCC void k_env_step_wave(const KParams* __restrict__ kp,
                                                       const float* actions, int substeps,
                                                       float* obs_out, float* obs_task, float* rew,
                                                       int64_t* reset_buf, int64_t* progress_buf,
@@ -774,6 +776,9 @@ __global__ __launch_bounds__(256) void k_soa_to_rows(const float* __restrict__ s
         out[t] = tile[c * (MI_GATHER_TILE + 1) + e];
     }
 }
+// Scatter: one lane per (row, column). With duplicate ids each column of the env takes its
+// value from one of the duplicate rows, unspecified which (torch index_put_ and PhysX's indexed
+// setters leave duplicates undefined as well; tests/test_gpu_view.py).
 template <typename IDX>
 __global__ __launch_bounds__(256) void k_rows_to_soa(const float* __restrict__ src, int n, int C,
                                                     const IDX* __restrict__ idx, int N, int fs, int es,
@@ -1146,9 +1151,20 @@ int mi_sim_create(const mi_model_desc* md, const mi_sim_params* prm, int32_t N, 
             for (int k = 0; k < m.nv; ++k) lr += (anc_start[k + 1] - anc_start[k] + 3) & ~3;
             t.s_L = take(ct ? lr + m.nv : 4);
         }
-        // CT path: J rows of up to 64 constraint rows for the PGS (LDS is not the occupancy
-        // limit here: registers cap the wave path at 2 waves/SIMD = 8 envs/CU = 20 KB each)
-        t.j_rows_lds = ct ? std::min(48, m.max_rows) : 0;
+        // Residency: the kernels' register budget allows TopoCT::kWaves waves per SIMD, i.e.
+        // envs_cu = 4 kWaves resident envs per CU (Humanoid 8, Ant 16: all 4096 envs of a launch
+        // in one round). E envs per workgroup share one copy of the constant block; each env's
+        // region [s_R, s_total) gets the floats that leave envs_cu envs inside the CU's 160 KB.
+        int waves = 2, lam_rows = 0;
+        with_topo(s->topo, [&](auto T) { waves = decltype(T)::kWaves; lam_rows = decltype(T)::kLamRows; });
+        const int envs_cu = 4 * std::max(1, waves);
+        t.envs_per_wg = ct && waves >= 4 ? 4 : 1;
+        if (const char* e = getenv("MI_WAVE_ENVS")) t.envs_per_wg = std::max(1, std::min(4, atoi(e)));
+        const int E = t.envs_per_wg;
+        const int env_budget = ((163840 / (int)sizeof(float)) / std::max(1, envs_cu / E) - al4(t.mc_len)) / E;
+        // CT path: J rows of the first constraint rows for the PGS; a 16-envs/CU budget keeps
+        // the rows the Delassus-space sweeps use (kLamRows), the 8-envs/CU one up to 48
+        t.j_rows_lds = ct ? std::min(waves >= 4 ? lam_rows : 48, m.max_rows) : 0;
         t.s_J = take(ct ? t.j_rows_lds * m.nv : 4);
         // CT path: W rows for the P9 -> P10 hand-over. First choice: the rest of the dead
         // span; when that holds fewer rows than a one-bank PGS can use and the LDS budget of
@@ -1162,10 +1178,12 @@ int mi_sim_create(const mi_model_desc* md, const mi_sim_params* prm, int32_t N, 
         t.s_W2 = 0;
         {
             const int want = std::min(64, m.max_rows);
-            const int lds_budget_floats = (160 * 1024 / 8) / (int)sizeof(float);
-            if (ct && t.w_rows_lds < want && so + al4(want * m.nv) <= lds_budget_floats) {
-                t.s_W = take(want * m.nv);
-                t.w_rows_lds = t.w_rows_a = want;
+            const int lds_budget_floats = t.s_R + env_budget;   // end of this env's share
+            int fit = want;   // the most W rows a dedicated region can hold within the share
+            while (fit > 0 && so + al4(fit * m.nv) > lds_budget_floats) --fit;
+            if (ct && t.w_rows_lds < fit && (fit == want || !self_on)) {
+                t.s_W = take(fit * m.nv);
+                t.w_rows_lds = t.w_rows_a = fit;
             } else if (ct && self_on && t.w_rows_lds < want) {   // (w_row<kSelf> on device)
                 const int extra = std::min(want - t.w_rows_lds, (lds_budget_floats - so - 3) / m.nv);
                 if (extra > 0) {
@@ -1179,8 +1197,6 @@ int mi_sim_create(const mi_model_desc* md, const mi_sim_params* prm, int32_t N, 
         // by w * env_stride
         t.s_env = t.s_R;
         t.env_stride = so - t.s_env;
-        t.envs_per_wg = 1;
-        if (const char* e = getenv("MI_WAVE_ENVS")) t.envs_per_wg = std::max(1, std::min(4, atoi(e)));
         {   // the sequential regions strictly increase; the row data sits inside the dead
             // span (overlay) or between s_rp and s_xs
             const int offs[] = {t.s_mc, t.s_R, t.s_o, t.s_S, t.s_F, t.s_Ic, t.s_M, t.s_X,
@@ -1265,17 +1281,6 @@ int mi_sim_create(const mi_model_desc* md, const mi_sim_params* prm, int32_t N, 
     hipError_t e = hipDeviceSynchronize();
     if (e != hipSuccess) return cleanup(fail(MI_E_HIP, "init: %s", hipGetErrorString(e)));
     if ((rc = sync_kparams(s))) return cleanup(rc);
-    if (s->wave && s->lds_bytes > 64 * 1024) {   // above the default dynamic-LDS limit
-        hipError_t e1 = hipSuccess, e2 = hipSuccess;
-        with_topo(s->topo, [&](auto T) {
-            e1 = hipFuncSetAttribute((const void*)k_env_step_wave<decltype(T)>,
-                                     hipFuncAttributeMaxDynamicSharedMemorySize, (int)s->lds_bytes);
-            e2 = hipFuncSetAttribute((const void*)k_sim_step_wave<decltype(T)>,
-                                     hipFuncAttributeMaxDynamicSharedMemorySize, (int)s->lds_bytes);
-        });
-        if (e1 != hipSuccess || e2 != hipSuccess)
-            return cleanup(fail(MI_E_HIP, "wave kernels: %zu B of LDS per workgroup refused", s->lds_bytes));
-    }
     if (s->wave && s->lds_bytes > 64 * 1024) {   // above the default dynamic-LDS limit
         hipError_t e1 = hipSuccess, e2 = hipSuccess;
         with_topo(s->topo, [&](auto T) {

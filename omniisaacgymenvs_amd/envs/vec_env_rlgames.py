@@ -19,6 +19,7 @@ from typing import Optional
 import numpy as np
 import torch
 
+from ..utils.roctx import trace_range
 from .world import Scene, World
 
 
@@ -107,7 +108,7 @@ class VecEnvRLGames:
                 obs, rew, resets = t.fused_step(actions, out)
                 ev[1][k].record()
                 self._ev_i += 1
-            else:
+            else:   # one launch: no per-phase ranges (the kernel trace names it)
                 obs, rew, resets = t.fused_step(actions, out)
             self.sim_frame_count += t.control_frequency_inv
             # fresh tensors written by the launch itself (= _process_data's clones)
@@ -126,11 +127,14 @@ class VecEnvRLGames:
         actions = torch.clamp(actions, -t.clip_actions, t.clip_actions).to(t.device).clone()
         if t.randomize_actions:
             actions = t._dr_randomizer.apply_actions_randomization(actions=actions, reset_buf=t.reset_buf)
-        t.pre_physics_step(actions)
-        for _ in range(t.control_frequency_inv):
-            self._world.step(render=self._render)
-            self.sim_frame_count += 1
-        self._obs, self._rew, self._resets, self._extras = t.post_physics_step()
+        with trace_range("pre_physics_step"):
+            t.pre_physics_step(actions)
+        with trace_range("physics (controlFrequencyInv x World.step)"):
+            for _ in range(t.control_frequency_inv):
+                self._world.step(render=self._render)
+                self.sim_frame_count += 1
+        with trace_range("post_physics_step"):
+            self._obs, self._rew, self._resets, self._extras = t.post_physics_step()
         if t.randomize_observations:
             self._obs = t._dr_randomizer.apply_observations_randomization(observations=self._obs,
                                                                           reset_buf=t.reset_buf)

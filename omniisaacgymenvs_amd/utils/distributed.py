@@ -210,4 +210,5 @@ class RolloutGather:
         self.wait()
         v = o.views[name][:, : self.last_rows]
         v = v.transpose(0, 1)
-        return v.reshape((self.last_rows, self.world * self.n) + tuple(v.shape[3:]))
+        # contiguous (at world 1 the reshape alone would be a strided view of the slab)
+        return v.reshape((self.last_rows, self.world * self.n) + tuple(v.shape[3:])).contiguous()

@@ -19,7 +19,7 @@ from omniisaacgymenvs_amd import native as N
 from omniisaacgymenvs_amd.utils.task_util import make_env
 from oracle.oracle import lib as orc_lib
 from tests.helpers import oracle_twin, sync_oracle, task_buffers
-from tests.test_gpu_parity import check_pair
+from tests.test_gpu_parity import check_pair, oracle_sens, pot_mag
 
 pytestmark = pytest.mark.gpu
 
@@ -48,12 +48,13 @@ def test_full_size_step_matches_oracle(gpu, name):
     for k in range(3, 5):
         b = task_buffers(env)
         acts = _actions(env, k)
+        sens = oracle_sens(env, 3, acts.cpu().numpy(), b)
         obs_dict, rew, resets, _ = env.step(acts)
         torch.cuda.synchronize()
         orc.env_step(acts.cpu().numpy(), task.control_frequency_inv, b)
         tol = 1e-4 if name == "Cartpole" else 2e-3
         check_pair(name, task, obs_dict["obs"].cpu().numpy(), rew.cpu().numpy(), b["obs"], b["rew"],
-                   tol, orc.decision_margin())
+                   tol, orc.decision_margin(), sens=sens, pot=pot_mag(b))
         assert np.array_equal(resets.cpu().numpy(), b["reset"])
         assert np.array_equal(task.progress_buf.cpu().numpy(), b["progress"])
         sync_oracle(env, orc)

@@ -2,9 +2,10 @@
 
 Tolerances (fp32): task math from identical state rtol=atol=1e-4
 (transcendentals: device ocml vs glibc differ by a few ulp); one fused env step incl.
-physics per observation field group (GROUP_TOL: median / 99th percentile / max bounds at ~5x the
-measured device-oracle error; CRBA+LTDL on the device vs dense J^T I J + Cholesky in the oracle,
-4 PGS sweeps amplify rounding); reset / done masks and progress are compared BIT-EXACT.
+physics: every obs entry and the reward within 2e-3 for envs away from a contact / limit
+threshold, widened only by the oracle's own rounding sensitivity of that env's step and the
+float32 quantisation of the potentials (check_pair); median / 99th-percentile regression bounds
+per field group (GROUP_TOL); reset / done masks and progress are compared BIT-EXACT.
 """
 import numpy as np
 import pytest
@@ -14,7 +15,7 @@ from omniisaacgymenvs_amd import native as N
 from omniisaacgymenvs_amd.utils.task_util import make_env
 from oracle import oracle as oracle_mod
 from oracle.oracle import lib as orc_lib
-from tests.helpers import oracle_twin, rand_actions, sync_oracle, task_buffers
+from tests.helpers import oracle_sensitivity, oracle_twin, rand_actions, sync_oracle, task_buffers
 
 pytestmark = pytest.mark.gpu
 TASKS = ["Cartpole", "Ant", "Humanoid"]
@@ -126,18 +127,23 @@ def _sensor_cols(task):
 # may go either way under a different float summation order (contact model discontinuity).
 DECISION_EPS = 1e-4
 
-# Device-vs-oracle bounds per observation field group after ONE fused env step from identical
-# state: (median, 99th percentile, max over envs away from a decision threshold) of the per-env
-# max |device - oracle| in the group, each ~5x what tools/parity_stats.py measured over
-# 4 steps x 4096 envs (DESIGN.md §4 lists the measured values). The force-sensor columns carry
-# the PGS contact impulses (4 sweeps, ill-conditioned stacks), hence their wider tail.
+# Per-env bound after ONE fused env step from identical state, for envs away from a decision
+# threshold: every obs entry and the reward within FAR_ABS (the round-1 one-step bar), unless the
+# step's own conditioning, measured on the ORACLE side, allows more:
+#  * sens: the oracle's response to a 2-ulp perturbation of its input state (tests/helpers.py
+#    oracle_sensitivity, max over the env's obs entries and reward) — stacked contacts and
+#    near-singular Delassus blocks amplify rounding; such an env may differ by SENS_K x that;
+#  * the reward carries potentials - prev_potentials with |potentials| ~ 6e4 in float32
+#    (locomotion.py:223, dt = 1/60): 2 ulp of the potentials is the reward's own quantisation.
+# The median / 99th-percentile bounds per field group (GROUP_TOL, ~5x the measured device-oracle
+# error over 4 steps x 4096 envs, tools/parity_stats.py) stay as regression detectors.
+FAR_ABS = 2e-3
+SENS_K = 4.0
 GROUP_TOL = {
-    "Humanoid": {"root": (2e-5, 1e-4, 1e-3), "dof_pos": (1e-5, 5e-5, 4e-4),
-                 "dof_vel": (5e-5, 4e-4, 3e-3), "sensors": (5e-5, 3e-3, 3e-2),
-                 "actions": (0.0, 0.0, 0.0), "rew": (2e-6, 5e-5, 2e-2)},
-    "Ant": {"root": (5e-6, 4e-5, 1e-4), "dof_pos": (1e-6, 3e-6, 1e-5),
-            "dof_vel": (3e-6, 4e-5, 2e-4), "sensors": (1e-5, 1.5e-4, 5e-4),
-            "actions": (0.0, 0.0, 0.0), "rew": (1e-6, 2e-6, 1e-5)},
+    "Humanoid": {"root": (2e-5, 1e-4), "dof_pos": (1e-5, 5e-5), "dof_vel": (5e-5, 4e-4),
+                 "sensors": (5e-5, 3e-3), "actions": (0.0, 0.0), "rew": (2e-6, 5e-5)},
+    "Ant": {"root": (5e-6, 4e-5), "dof_pos": (1e-6, 3e-6), "dof_vel": (3e-6, 4e-5),
+            "sensors": (1e-5, 1.5e-4), "actions": (0.0, 0.0), "rew": (1e-6, 2e-6)},
 }
 GROUP_TOL["AntSelf"] = GROUP_TOL["Humanoid"]   # Ant with self-collision pairs (runtime tables)
 
@@ -148,33 +154,58 @@ def obs_groups(task):
             "sensors": slice(12 + 2 * D, 12 + 2 * D + 6 * S), "actions": slice(12 + 2 * D + 6 * S, None)}
 
 
-def check_pair(name, task, obs, rew, obs_ref, rew_ref, tol, margin):
+def oracle_sens(env, seed, actions, bufs):
+    """Per-env oracle-side rounding sensitivity of the coming step (call BEFORE the device steps;
+    None for Cartpole, whose analytic step has no ill-conditioned solve)."""
+    if env.task.model.dyn_kind != 0:
+        return None
+    sg, sr, _ = oracle_sensitivity(env, seed, np.asarray(actions, np.float32),
+                                   env.task.control_frequency_inv, bufs, obs_groups(env.task))
+    return np.maximum(np.max(np.stack(list(sg.values())), axis=0), sr)
+
+
+def pot_mag(b):
+    return np.maximum(np.abs(b["pot"]), np.abs(b["prev"]))
+
+
+def check_pair(name, task, obs, rew, obs_ref, rew_ref, tol, margin, sens=None, pot=None,
+               quantiles=True):
     """Per-env parity after one fused step from identical state.
 
-    Cartpole: every env within `tol` (1e-4). Locomotion: per field group the median / 99th
-    percentile / max (over envs whose oracle `margin` — closest contact or limit activation
-    decision to its threshold during the step, OracleSim.decision_margin — is >= DECISION_EPS)
-    of the per-env max abs error stay within GROUP_TOL; envs at a threshold may take the other
-    discrete branch but must stay rare (< 2 %). `tol` is unused for locomotion (kept for the
-    call sites' signature)."""
+    Cartpole: every env within `tol` (1e-4). Locomotion: envs whose oracle `margin` (closest
+    contact or limit activation decision to its threshold during the step,
+    OracleSim.decision_margin) is >= DECISION_EPS: every obs entry within max(FAR_ABS,
+    SENS_K * sens) and the reward within that or 2 ulp of the potentials (`pot` = max |potential|
+    of the step); envs at a threshold may take the other discrete branch but must stay rare
+    (< 2 %). With `quantiles`, the median / 99th percentile of each group's per-env max error
+    stay within GROUP_TOL."""
     if name == "Cartpole":
         bad = ~np.all(np.isclose(obs, obs_ref, rtol=tol, atol=tol), axis=1)
         bad |= ~np.isclose(rew, rew_ref, rtol=tol, atol=tol)
         assert not bad.any(), f"{name}: envs {np.nonzero(bad)[0]}"
         return
     near = margin < DECISION_EPS
+    allow = np.full(len(rew), FAR_ABS)
+    if sens is not None:
+        allow = np.maximum(allow, SENS_K * sens)
+    allow_rew = allow.copy()
+    if pot is not None:
+        allow_rew = np.maximum(allow_rew, 2.0 * np.spacing(np.asarray(pot, np.float32)).astype(np.float64))
     err = {g: np.abs(obs[:, sl] - obs_ref[:, sl]).max(axis=1) for g, sl in obs_groups(task).items()}
     err["rew"] = np.abs(rew - rew_ref)
-    over_near = np.zeros(len(rew), bool)
+    over = np.zeros(len(rew), bool)
     for g, e in err.items():
-        q50, q99, emax = GROUP_TOL[name][g]
-        far = e[~near]
-        assert np.quantile(e, 0.5) <= q50, f"{name} {g}: median error {np.quantile(e, 0.5):.3g} > {q50}"
-        assert np.quantile(e, 0.99) <= q99, f"{name} {g}: q99 error {np.quantile(e, 0.99):.3g} > {q99}"
-        assert far.size == 0 or far.max() <= emax, (
-            f"{name} {g}: env {np.nonzero(~near)[0][far.argmax()]} error {far.max():.3g} > {emax}")
-        over_near |= near & (e > emax)
-    assert over_near.mean() < 0.02, f"{name}: {over_near.sum()} envs at a threshold differ"
+        if quantiles:
+            q50, q99 = GROUP_TOL[name][g]
+            assert np.quantile(e, 0.5) <= q50, f"{name} {g}: median error {np.quantile(e, 0.5):.3g} > {q50}"
+            assert np.quantile(e, 0.99) <= q99, f"{name} {g}: q99 error {np.quantile(e, 0.99):.3g} > {q99}"
+        lim = allow_rew if g == "rew" else allow
+        bad = (e > lim) & ~near
+        assert not bad.any(), (
+            f"{name} {g}: env {np.nonzero(bad)[0][0]} error {e[bad][0]:.3g} > {lim[bad][0]:.3g} "
+            f"(sensitivity {None if sens is None else sens[bad][0]:.3g})")
+        over |= near & (e > lim)
+    assert over.mean() < 0.02, f"{name}: {over.sum()} envs at a threshold differ"
 
 
 def check_device_pair(name, obs_a, rew_a, obs_b, rew_b, tol, margin):
@@ -200,12 +231,13 @@ def test_fused_env_step_matches_oracle(env_pair):
     for step in range(3):
         b = task_buffers(env)
         acts = rand_actions(n, A, 100 + step)
+        sens = oracle_sens(env, 11, acts.numpy(), b)
         obs_dict, rew, resets, _ = env.step(acts.to("cuda:0"))
         torch.cuda.synchronize()
         orc.env_step(acts.numpy(), task.control_frequency_inv, b)
         tol = 1e-4 if name == "Cartpole" else 2e-3
         check_pair(name, task, obs_dict["obs"].cpu().numpy(), rew.cpu().numpy(), b["obs"], b["rew"],
-                   tol, orc.decision_margin())
+                   tol, orc.decision_margin(), sens=sens, pot=pot_mag(b))
         assert np.array_equal(resets.cpu().numpy(), b["reset"])
         assert np.array_equal(task.progress_buf.cpu().numpy(), b["progress"])
         sync_oracle(env, orc)   # re-align (chaotic contact dynamics)
@@ -301,11 +333,12 @@ def test_self_collision_on_uncompiled_model_uses_runtime_tables(gpu, monkeypatch
         sync_oracle(env, orc)
         b = task_buffers(env)
         acts = rand_actions(64, env.num_actions, 90 + step)
+        sens = oracle_sens(env, 9, acts.numpy(), b)
         o, r, d, _ = env.step(acts.to("cuda:0"))
         torch.cuda.synchronize()
         orc.env_step(acts.numpy(), env.task.control_frequency_inv, b)
         check_pair("AntSelf", env.task, o["obs"].cpu().numpy(), r.cpu().numpy(), b["obs"], b["rew"],
-                   2e-3, orc.decision_margin())
+                   2e-3, orc.decision_margin(), sens=sens, pot=pot_mag(b))
     env.close()
 
 
@@ -330,11 +363,12 @@ def test_self_collision_active_on_device(gpu):
     for step in range(12):
         b = task_buffers(env)
         acts = rand_actions(256, task.num_actions, 300 + step)
+        sens = oracle_sens(env, 5, acts.numpy(), b)
         obs_dict, rew, resets, _ = env.step(acts.to("cuda:0"))
         torch.cuda.synchronize()
         orc.env_step(acts.numpy(), task.control_frequency_inv, b)
         check_pair("Humanoid", task, obs_dict["obs"].cpu().numpy(), rew.cpu().numpy(), b["obs"],
-                   b["rew"], 2e-3, orc.decision_margin())
+                   b["rew"], 2e-3, orc.decision_margin(), sens=sens, pot=pot_mag(b))
         assert np.array_equal(resets.cpu().numpy(), b["reset"])
         sync_oracle(env, orc)
         touching += sum(orc.self_min_gap(e) < 0.02 for e in range(0, 256, 8))
@@ -429,4 +463,31 @@ def test_post_step_nan_guard(gpu, monkeypatch, var):
                                       t.prev_potentials.data_ptr(), view.stream()), "mi_task_post_step")
     torch.cuda.synchronize()
     assert view.nan_count() - n0 == len(bad)
+    env.close()
+
+
+def test_modular_step_roctx_ranges(gpu, monkeypatch):
+    """the method-by-method step brackets pre_physics_step / the physics substeps /
+    post_physics_step in roctx ranges (utils/roctx.py), in the reference's order."""
+    from omniisaacgymenvs_amd.utils import roctx
+
+    calls = []
+
+    class Rec:
+        def roctxRangePushA(self, name):
+            calls.append(("push", name.decode()))
+            return 0
+
+        def roctxRangePop(self):
+            calls.append(("pop",))
+            return 0
+
+    monkeypatch.setattr(roctx, "_LIB", Rec())
+    monkeypatch.setattr(roctx, "_TRIED", True)
+    env = make_env("Ant", num_envs=64, device="cuda:0", seed=2)
+    env.use_fused(False)
+    env.step(torch.zeros((64, env.num_actions), device="cuda:0"))
+    names = [c[1] for c in calls if c[0] == "push"]
+    assert names == ["pre_physics_step", "physics (controlFrequencyInv x World.step)", "post_physics_step"]
+    assert sum(c[0] == "pop" for c in calls) == 3
     env.close()

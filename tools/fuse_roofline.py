@@ -68,9 +68,21 @@ def measure(task_name: str, n: int, launches: int = 30, env=None) -> dict:
     label = t.get_robot().post_kernel()[0] or kernel_label(n)   # what mi_task_post_step launched
     if own:
         env.close()
-    return {"kernel": label, "task": task_name, "num_envs": n, "kernel_ms": round(ms, 4),
-            "algo_bytes_per_env": B, "achieved": round(gbs, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-            "frac": round(gbs / HBM_PEAK_GBS, 4)}
+    rec = {"kernel": label, "task": task_name, "num_envs": n, "kernel_ms": round(ms, 4),
+           "algo_bytes_per_env": B, "achieved": round(gbs, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+           "frac": round(gbs / HBM_PEAK_GBS, 4)}
+    # measured HBM bytes per launch (rocprofv3 FETCH_SIZE / WRITE_SIZE passes of this kernel at
+    # this env count, gfx950 read correction: tools/pmc_traffic.py), when committed
+    tf = os.path.join(ROOT, "profiles", f"traffic_fuse_{task_name}.json")
+    if os.path.exists(tf):
+        with open(tf) as f:
+            d = json.load(f)
+        if int(d.get("num_envs", -1)) == n:
+            rec["traffic"] = d["bytes_per_launch"]
+            rec["traffic_per_env"] = round(d["bytes_per_launch"] / n, 1)
+            rec["traffic_over_algo"] = round(d["bytes_per_launch"] / (B * n), 3)
+            rec["traffic_source"] = f"profiles/traffic_fuse_{task_name}.json"
+    return rec
 
 
 def main():

@@ -21,6 +21,7 @@
 #   patha        INTEGRATION path (A): reference call sequence over ArticulationView -> path_a_humanoid.json
 #   train        PPO frames/s (tools/bench_train.py)                       -> bench_train_*.log
 #   sizes        env-count sweep of the fused step (tools/bw_sweep.py)     -> bw_sweep_*.json
+#   ab           bench A/B: default library vs LIB_B (alternating passes)  -> DESIGN perf log
 # Environment knobs: TASK (Humanoid), NS (env counts), BARGS (extra bench.py args), TAG (log suffix).
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 export TMPDIR=/tmp
@@ -43,7 +44,7 @@ run() {  # run <name> <timeout> <cmd...>; exit codes 0/1 (test failures) continu
 recipe() {
   case "$1" in
   tests)
-    run pytest_gpu 900 python -u -m pytest tests -m gpu -q -x --timeout 200 --timeout-method thread ${PYTEST_K:+-k "$PYTEST_K"}
+    run pytest_gpu 900 python -u -m pytest tests -m gpu -q ${PYTEST_X--x} --timeout 200 --timeout-method thread ${PYTEST_K:+-k "$PYTEST_K"}
     grep -E "^FAILED|^E  .*Error|passed|failed" gpurun_out/pytest_gpu.log | head -30 ;;
   smoke)
     run smoke 300 python -u -c "import __graft_entry__ as g; g.smoke()" ;;
@@ -90,6 +91,12 @@ recipe() {
     for T in ${TASKS:-Humanoid}; do run train_${T}_$TAG 600 python -u tools/bench_train.py --task $T; done ;;
   sizes)
     run sizes_${TASK}_$TAG 300 python -u tools/bw_sweep.py $TASK ${NS// /,} ;;
+  ab)   # A/B of the default library against LIB_B (another build of libmi_sim.so), alternating
+    for k in 1 2 3; do
+      run ab_a_${TASK}_$k 200 python -u bench.py --task $TASK --steps 300 --warmup 30 --no-cpu-baseline --no-side --fuse-envs 0 ${BARGS:-}
+      run ab_b_${TASK}_$k 200 env MI_SIM_LIB=$LIB_B python -u bench.py --task $TASK --steps 300 --warmup 30 --no-cpu-baseline --no-side --fuse-envs 0 ${BARGS:-}
+    done
+    for f in gpurun_out/ab_[ab]_${TASK}_*.log; do echo "$f $(grep -o '"kernel_ms": [0-9.]*\|"ms_per_step": [0-9.]*\|"lds_bytes_per_env": [0-9]*' $f | head -3 | tr '\n' ' ')"; done ;;
   *)
     echo "unknown recipe $1"; exit 2 ;;
   esac

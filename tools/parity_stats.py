@@ -52,6 +52,9 @@ def main():
     gerr = {g: [] for g in list(groups) + ["rew"]}
     gsens = {g: [] for g in list(groups) + ["rew"]}
     errs, margins, senss = [], [], []
+    grel = {g: [] for g in groups}
+    gmag = {g: [] for g in groups}
+    potmag = []
     for k in range(3, 3 + steps):
         b = task_buffers(env)
         a = acts(k)
@@ -68,6 +71,10 @@ def main():
         rd = np.abs(r.cpu().numpy() - b["rew"])
         for g, sl in groups.items():
             gerr[g].append(od[:, sl].max(axis=1))
+            # mixed abs / rel error per entry: |d| / max(1, |oracle value|)
+            grel[g].append((od[:, sl] / np.maximum(1.0, np.abs(b["obs"][:, sl]))).max(axis=1))
+            gmag[g].append(np.abs(b["obs"][:, sl]).max(axis=1))
+        potmag.append(np.maximum(np.abs(b["pot"]), np.abs(b["prev"])))
         gerr["rew"].append(rd)
         e = np.maximum(od.max(axis=1), rd)
         errs.append(e)
@@ -94,6 +101,19 @@ def main():
                        "max_far_ratio_to_sens": float((np.concatenate(v)[far] / np.maximum(
                            np.concatenate(gsens[g])[far], 1e-6)).max()) if far.any() else None}
                       for g, v in gerr.items()}}
+    # reward: float32 potentials are ~6e4 (ulp 3.9e-3); the step's reward carries pot - prev
+    pm = np.concatenate(potmag) if potmag else None
+    if pm is not None and task_name != "Cartpole":
+        r_all = np.concatenate(gerr["rew"])
+        ulp = np.spacing(pm.astype(np.float32)).astype(np.float64)
+        out["rew_err_over_pot_ulp_far"] = float((r_all[far] / ulp[far]).max())
+    for g in groups:
+        rel = np.concatenate(grel[g])
+        mag = np.concatenate(gmag[g])
+        ab = np.concatenate(gerr[g])
+        w = int(np.argmax(np.where(far, ab, -1)))
+        out["groups"][g]["max_far_mixed_rel"] = float(rel[far].max()) if far.any() else None
+        out["groups"][g]["worst_far_abs_with_mag"] = [float(ab[w]), float(mag[w])]
     print(json.dumps(out), flush=True)
     orc.close()
     env.close()

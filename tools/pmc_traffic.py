@@ -44,10 +44,12 @@ def main():
     if "--out" in sys.argv:
         out = sys.argv[sys.argv.index("--out") + 1]
     kern = sys.argv[sys.argv.index("--kernel") + 1] if "--kernel" in sys.argv else "k_env_step"
+    n_envs = int(sys.argv[sys.argv.index("--num-envs") + 1]) if "--num-envs" in sys.argv else None
     fkb, nf = per_launch(fdir, "FETCH_SIZE", kern)
     wkb, nw = per_launch(wdir, "WRITE_SIZE", kern)
     rec = {
-        "task": task, "kernel": kern + ("* (fused env step)" if kern == "k_env_step" else "*"), "launches": {"fetch": nf, "write": nw},
+        "task": task, "kernel": kern + ("* (fused env step)" if kern == "k_env_step" else "*"),
+        "num_envs": n_envs, "launches": {"fetch": nf, "write": nw},
         "fetch_kib_raw": round(fkb, 1), "write_kib_raw": round(wkb, 1),
         "read_bytes_corrected": round(2 * fkb * 1024), "write_bytes": round(wkb * 1024),
         "bytes_per_launch": round(2 * fkb * 1024 + wkb * 1024),
