@@ -542,6 +542,13 @@ def main():
             sys.path.insert(0, os.path.join(ROOT, "tools"))
             from fuse_roofline import measure
             out["obs_reward_fuse"] = measure(args.task, args.fuse_envs, 30)
+        if world == 1 and not args.no_side and args.task != "Cartpole":
+            # INTEGRATION.md path (A): the reference's own task code over the ArticulationView
+            # tensor API (indexed reset scatters, set_joint_efforts, controlFrequencyInv x
+            # World.step, the five getters) on the same task and env count
+            sys.path.insert(0, os.path.join(ROOT, "tools"))
+            from path_a_timing import measure as path_a
+            out["path_a"] = path_a(args.task, n_local, 100)
         if world == 1 and not args.no_cpu_baseline:
             out["cpu_baseline"] = cpu_baseline(args.task, env, args.cpu_seconds)
         print(json.dumps(out), flush=True)

@@ -173,7 +173,14 @@ int mi_set_root_state(mi_sim* sim, const float* pos /*[n,3]|NULL*/, const float*
                       void* stream);
 
 /* --- physics step: World.step x controlFrequencyInv (envs/vec_env_rlgames.py:64-66) --- */
+/* Substeps are deferred and coalesced: consecutive mi_sim_step calls on one stream with no
+ * other call touching the state in between (the reference's controlFrequencyInv x World.step
+ * loop) run as ONE launch, issued by the next entry point that reads or writes the state (or by
+ * mi_sim_flush); results are identical to separate launches. Inside a stream capture, and with
+ * the environment variable MI_SIM_DEFER=0, every call launches at once. */
 int mi_sim_step(mi_sim* sim, int32_t substeps, void* stream);
+/* Issue any deferred substeps now (stream-ordered; no host sync). */
+int mi_sim_flush(mi_sim* sim, void* stream);
 
 /* --- fused task kernels ---------------------------------------------------------------- */
 int mi_task_configure(mi_sim* sim, const mi_task_params* tp);

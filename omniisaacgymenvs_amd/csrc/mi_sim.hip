@@ -71,6 +71,13 @@ struct mi_sim {
     void* kp_dev = nullptr;  // device copy of KParams (wave path)
     int num_cu = 0;          // compute units of the device (queried on first use)
     int post_kernel = -1, post_grid = 0;   // last mi_task_post_step launch (mi_task_post_kernel)
+    // deferred physics substeps (mi_sim_step): World.step() twice in a row (the reference's
+    // controlFrequencyInv loop, vec_env_rlgames.py:64-66) becomes ONE launch of two substeps,
+    // issued by the next entry point that touches the state (flush_pending)
+    bool defer = true;
+    int pending = 0;
+    hipStream_t pending_stream = nullptr;
+    hipEvent_t pending_ev = nullptr;
     std::vector<float> lower, upper;  // host copy for mi_sim_info
     std::vector<void*> allocs;
     // launch timing (mi_sim_time_launches): every tev_every-th mi_env_step launch carries a
@@ -754,22 +761,26 @@ __global__ void k_reset_idx(DevModel m, DevState st, DevTask tp, const int64_t* 
 // The field-major layout of the one-lane-per-env path (es = 1) gathers through an LDS tile:
 // field-major reads in, row-major writes out, both coalesced.
 constexpr int MI_GATHER_TILE = 256, MI_GATHER_MAXC = 32;
-__global__ __launch_bounds__(256) void k_soa_to_rows(const float* __restrict__ src, int N, int C,
-                                                    int fs, int es, float* __restrict__ dst) {
+// Several fields of one ArticulationView call (get_world_poses: pos + quat; set_world_poses;
+// get / set_velocities, ...) in ONE launch: blockIdx.y picks the field.
+struct GField { const float* src; float* dst; int C; };
+struct GFields { GField f[3]; };
+__global__ __launch_bounds__(256) void k_soa_to_rows_multi(GFields fs3, int N, int fs, int es) {
+    const GField g = fs3.f[blockIdx.y];
     const int64_t e0 = (int64_t)blockIdx.x * MI_GATHER_TILE;
     const int ne = (int)min((int64_t)MI_GATHER_TILE, (int64_t)N - e0);
-    const int tot = ne * C;
-    float* out = dst + e0 * C;
+    const int C = g.C, tot = ne * C;
+    float* out = g.dst + e0 * C;
     if (es != 1 || C > MI_GATHER_MAXC) {           // records (or too wide for the tile)
         for (int t = threadIdx.x; t < tot; t += blockDim.x) {
             const int e = t / C, c = t - e * C;
-            out[t] = src[(size_t)c * fs + (size_t)(e0 + e) * es];
+            out[t] = g.src[(size_t)c * fs + (size_t)(e0 + e) * es];
         }
         return;
     }
     __shared__ float tile[MI_GATHER_MAXC * (MI_GATHER_TILE + 1)];   // [c][e], odd stride
     for (int c = 0; c < C; ++c)
-        if ((int)threadIdx.x < ne) tile[c * (MI_GATHER_TILE + 1) + threadIdx.x] = src[(size_t)c * fs + e0 + threadIdx.x];
+        if ((int)threadIdx.x < ne) tile[c * (MI_GATHER_TILE + 1) + threadIdx.x] = g.src[(size_t)c * fs + e0 + threadIdx.x];
     __syncthreads();
     for (int t = threadIdx.x; t < tot; t += blockDim.x) {
         const int e = t / C, c = t - e * C;
@@ -780,15 +791,15 @@ __global__ __launch_bounds__(256) void k_soa_to_rows(const float* __restrict__ s
 // value from one of the duplicate rows, unspecified which (torch index_put_ and PhysX's indexed
 // setters leave duplicates undefined as well; tests/test_gpu_view.py).
 template <typename IDX>
-__global__ __launch_bounds__(256) void k_rows_to_soa(const float* __restrict__ src, int n, int C,
-                                                    const IDX* __restrict__ idx, int N, int fs, int es,
-                                                    float* __restrict__ dst) {
+__global__ __launch_bounds__(256) void k_rows_to_soa_multi(GFields fs3, int n, const IDX* __restrict__ idx,
+                                                          int N, int fs, int es) {
+    const GField g = fs3.f[blockIdx.y];
     const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (t >= (int64_t)n * C) return;
-    const int r = (int)(t / C), c = (int)(t - (int64_t)r * C);
+    if (t >= (int64_t)n * g.C) return;
+    const int r = (int)(t / g.C), c = (int)(t - (int64_t)r * g.C);
     const int64_t i = idx ? (int64_t)idx[r] : r;
     if (i < 0 || i >= N) return;                   // out-of-range ids are ignored
-    dst[(size_t)c * fs + (size_t)i * es] = src[t];
+    const_cast<float*>(g.dst)[(size_t)c * fs + (size_t)i * es] = g.src[t];
 }
 static inline dim3 gather_grid(int N) { return dim3((N + MI_GATHER_TILE - 1) / MI_GATHER_TILE); }
 static inline dim3 scatter_grid(int n, int C) { return dim3((unsigned)(((int64_t)n * C + 255) / 256)); }
@@ -879,6 +890,7 @@ int mi_sim_create(const mi_model_desc* md, const mi_sim_params* prm, int32_t N, 
     mi_sim* s = new mi_sim();
     s->device = device_id;
     s->N = N;
+    if (const char* d = getenv("MI_SIM_DEFER")) s->defer = atoi(d) != 0;
     if (const char* b = getenv("MI_SIM_BLOCK")) {
         int v = atoi(b);
         if (v >= 1 && v <= 1024) s->block = v;
@@ -1300,6 +1312,7 @@ int mi_sim_destroy(mi_sim* s) {
     if (!s) return MI_OK;
     (void)hipSetDevice(s->device);
     for (hipEvent_t e : s->tev) (void)hipEventDestroy(e);
+    if (s->pending_ev) (void)hipEventDestroy(s->pending_ev);
     for (void* p : s->allocs) (void)hipFree(p);
     delete s;
     return MI_OK;
@@ -1323,46 +1336,110 @@ int mi_sim_info(const mi_sim* s, int32_t* num_envs, int32_t* num_dof, int32_t* n
 #define STREAM(x) ((hipStream_t)(x))
 #define NEED(p) if (!(p)) return fail(MI_E_NULL, "%s: null %s", __func__, #p)
 
+static int launch_sim(mi_sim* s, int substeps, hipStream_t stream) {
+    if (s->wave)
+        with_topo(s->topo, [&](auto T) {
+            hipLaunchKernelGGL(k_sim_step_wave<decltype(T)>, wave_grid(s), wave_block(s), s->lds_bytes,
+                               stream, (const KParams*)s->kp_dev, substeps);
+        });
+    else
+        hipLaunchKernelGGL(k_sim_step, grid_for(s, s->N), dim3(s->block), 0, stream, s->dm, s->ds,
+                           s->sp, substeps);
+    LAUNCH_CHECK();
+    return MI_OK;
+}
+
+static bool capturing(hipStream_t st) {
+    hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
+    return hipStreamIsCapturing(st, &cs) == hipSuccess && cs != hipStreamCaptureStatusNone;
+}
+
+// Issue the substeps mi_sim_step deferred, on the stream they were requested on; a caller on
+// another stream waits for them. Substeps requested before a stream capture began cannot be
+// issued into it: that is refused loudly (call the step inside the capture, or synchronise).
+static int flush_pending(mi_sim* s, void* stream) {
+    if (s->pending == 0) return MI_OK;
+    const int k = s->pending;
+    hipStream_t ps = s->pending_stream;
+    if (capturing(ps) || (stream && capturing(STREAM(stream))))
+        return fail(MI_E_STATE, "%d physics substep(s) requested before a stream capture began are "
+                                "still pending: synchronise before capturing", k);
+    s->pending = 0;
+    HIP_TRY(hipSetDevice(s->device));
+    int rc = launch_sim(s, k, ps);
+    if (rc) return rc;
+    if (STREAM(stream) != ps) {
+        if (!s->pending_ev) HIP_TRY(hipEventCreateWithFlags(&s->pending_ev, hipEventDisableTiming));
+        HIP_TRY(hipEventRecord(s->pending_ev, ps));
+        HIP_TRY(hipStreamWaitEvent(STREAM(stream), s->pending_ev, 0));
+    }
+    return MI_OK;
+}
+#define FLUSH(s, stream) do { int rc_ = flush_pending((s), (stream)); if (rc_) return rc_; } while (0)
+
+static int gather_fields(mi_sim* s, GFields f, int nf, int fs, int es, void* stream) {
+    if (nf == 0) return MI_OK;
+    dim3 g = gather_grid(s->N);
+    g.y = (unsigned)nf;
+    hipLaunchKernelGGL(k_soa_to_rows_multi, g, dim3(256), 0, STREAM(stream), f, s->N, fs, es);
+    LAUNCH_CHECK();
+    return MI_OK;
+}
+
+extern "C++" template <typename IDX>
+static int scatter_fields(mi_sim* s, GFields f, int nf, int n, const IDX* idx, void* stream) {
+    if (nf == 0 || n == 0) return MI_OK;
+    int cmax = 0;
+    for (int k = 0; k < nf; ++k) cmax = std::max(cmax, f.f[k].C);
+    dim3 g = scatter_grid(n, cmax);
+    g.y = (unsigned)nf;
+    hipLaunchKernelGGL(k_rows_to_soa_multi<IDX>, g, dim3(256), 0, STREAM(stream), f, n, idx, s->N,
+                       s->ds.fs, s->ds.es);
+    LAUNCH_CHECK();
+    return MI_OK;
+}
+
 int mi_get_root_state(mi_sim* s, float* pos, float* quat, float* vel, void* stream) {
     NEED(s);
     HIP_TRY(hipSetDevice(s->device));
-    const dim3 g = gather_grid(s->N), b(256);
-    if (pos) hipLaunchKernelGGL(k_soa_to_rows, g, b, 0, STREAM(stream), s->ds.root_pos, s->N, 3, s->ds.fs, s->ds.es, pos);
-    if (quat) hipLaunchKernelGGL(k_soa_to_rows, g, b, 0, STREAM(stream), s->ds.root_quat, s->N, 4, s->ds.fs, s->ds.es, quat);
-    if (vel) hipLaunchKernelGGL(k_soa_to_rows, g, b, 0, STREAM(stream), s->ds.root_vel, s->N, 6, s->ds.fs, s->ds.es, vel);
-    LAUNCH_CHECK();
-    return MI_OK;
+    FLUSH(s, stream);
+    GFields f{};
+    int nf = 0;
+    if (pos) f.f[nf++] = {s->ds.root_pos, pos, 3};
+    if (quat) f.f[nf++] = {s->ds.root_quat, quat, 4};
+    if (vel) f.f[nf++] = {s->ds.root_vel, vel, 6};
+    return gather_fields(s, f, nf, s->ds.fs, s->ds.es, stream);
 }
 
 int mi_get_dof_state(mi_sim* s, float* q, float* qd, void* stream) {
     NEED(s);
     HIP_TRY(hipSetDevice(s->device));
-    const dim3 g = gather_grid(s->N), b(256);
-    if (q) hipLaunchKernelGGL(k_soa_to_rows, g, b, 0, STREAM(stream), s->ds.q, s->N, s->dm.D, s->ds.fs, s->ds.es, q);
-    if (qd) hipLaunchKernelGGL(k_soa_to_rows, g, b, 0, STREAM(stream), s->ds.qd, s->N, s->dm.D, s->ds.fs, s->ds.es, qd);
-    LAUNCH_CHECK();
-    return MI_OK;
+    FLUSH(s, stream);
+    GFields f{};
+    int nf = 0;
+    if (q) f.f[nf++] = {s->ds.q, q, s->dm.D};
+    if (qd) f.f[nf++] = {s->ds.qd, qd, s->dm.D};
+    return gather_fields(s, f, nf, s->ds.fs, s->ds.es, stream);
 }
 
 int mi_get_sensor_wrench(mi_sim* s, float* out, void* stream) {
     NEED(s); NEED(out);
     HIP_TRY(hipSetDevice(s->device));
+    FLUSH(s, stream);
     if (s->dm.S == 0) return MI_OK;
-    hipLaunchKernelGGL(k_soa_to_rows, gather_grid(s->N), dim3(256), 0, STREAM(stream),
-                       s->ds.sens, s->N, 6 * s->dm.S, s->ds.sfs, s->ds.ses, out);
-    LAUNCH_CHECK();
-    return MI_OK;
+    GFields f{};
+    f.f[0] = {s->ds.sens, out, 6 * s->dm.S};
+    return gather_fields(s, f, 1, s->ds.sfs, s->ds.ses, stream);
 }
 
 int mi_set_dof_efforts(mi_sim* s, const float* eff, const int32_t* idx, int32_t n, void* stream) {
     NEED(s); NEED(eff);
     if (n < 0 || n > s->N || (!idx && n != s->N)) return fail(MI_E_SHAPE, "mi_set_dof_efforts: bad n=%d", n);
     HIP_TRY(hipSetDevice(s->device));
-    if (n == 0) return MI_OK;
-    hipLaunchKernelGGL(k_rows_to_soa<int32_t>, scatter_grid(n, s->dm.D), dim3(256), 0, STREAM(stream),
-                       eff, n, s->dm.D, idx, s->N, s->ds.fs, s->ds.es, s->ds.eff);
-    LAUNCH_CHECK();
-    return MI_OK;
+    FLUSH(s, stream);
+    GFields f{};
+    f.f[0] = {eff, s->ds.eff, s->dm.D};
+    return scatter_fields<int32_t>(s, f, 1, n, idx, stream);
 }
 
 int mi_set_dof_state(mi_sim* s, const float* q, const float* qd, const int64_t* idx, int32_t n,
@@ -1370,12 +1447,12 @@ int mi_set_dof_state(mi_sim* s, const float* q, const float* qd, const int64_t* 
     NEED(s);
     if (n < 0 || n > s->N || (!idx && n != s->N)) return fail(MI_E_SHAPE, "mi_set_dof_state: bad n=%d", n);
     HIP_TRY(hipSetDevice(s->device));
-    if (n == 0) return MI_OK;
-    const dim3 g = scatter_grid(n, s->dm.D), b(256);
-    if (q) hipLaunchKernelGGL(k_rows_to_soa<int64_t>, g, b, 0, STREAM(stream), q, n, s->dm.D, idx, s->N, s->ds.fs, s->ds.es, s->ds.q);
-    if (qd) hipLaunchKernelGGL(k_rows_to_soa<int64_t>, g, b, 0, STREAM(stream), qd, n, s->dm.D, idx, s->N, s->ds.fs, s->ds.es, s->ds.qd);
-    LAUNCH_CHECK();
-    return MI_OK;
+    FLUSH(s, stream);
+    GFields f{};
+    int nf = 0;
+    if (q) f.f[nf++] = {q, s->ds.q, s->dm.D};
+    if (qd) f.f[nf++] = {qd, s->ds.qd, s->dm.D};
+    return scatter_fields<int64_t>(s, f, nf, n, idx, stream);
 }
 
 int mi_set_root_state(mi_sim* s, const float* pos, const float* quat, const float* vel,
@@ -1383,28 +1460,38 @@ int mi_set_root_state(mi_sim* s, const float* pos, const float* quat, const floa
     NEED(s);
     if (n < 0 || n > s->N || (!idx && n != s->N)) return fail(MI_E_SHAPE, "mi_set_root_state: bad n=%d", n);
     HIP_TRY(hipSetDevice(s->device));
-    if (n == 0) return MI_OK;
-    const dim3 b(256);
-    if (pos) hipLaunchKernelGGL(k_rows_to_soa<int64_t>, scatter_grid(n, 3), b, 0, STREAM(stream), pos, n, 3, idx, s->N, s->ds.fs, s->ds.es, s->ds.root_pos);
-    if (quat) hipLaunchKernelGGL(k_rows_to_soa<int64_t>, scatter_grid(n, 4), b, 0, STREAM(stream), quat, n, 4, idx, s->N, s->ds.fs, s->ds.es, s->ds.root_quat);
-    if (vel) hipLaunchKernelGGL(k_rows_to_soa<int64_t>, scatter_grid(n, 6), b, 0, STREAM(stream), vel, n, 6, idx, s->N, s->ds.fs, s->ds.es, s->ds.root_vel);
-    LAUNCH_CHECK();
-    return MI_OK;
+    FLUSH(s, stream);
+    GFields f{};
+    int nf = 0;
+    if (pos) f.f[nf++] = {pos, s->ds.root_pos, 3};
+    if (quat) f.f[nf++] = {quat, s->ds.root_quat, 4};
+    if (vel) f.f[nf++] = {vel, s->ds.root_vel, 6};
+    return scatter_fields<int64_t>(s, f, nf, n, idx, stream);
 }
 
 int mi_sim_step(mi_sim* s, int32_t substeps, void* stream) {
     NEED(s);
     if (substeps < 0 || substeps > 64) return fail(MI_E_ARG, "substeps %d out of range", substeps);
+    if (substeps == 0) return MI_OK;
     HIP_TRY(hipSetDevice(s->device));
-    if (s->wave)
-        with_topo(s->topo, [&](auto T) {
-            hipLaunchKernelGGL(k_sim_step_wave<decltype(T)>, wave_grid(s), wave_block(s), s->lds_bytes,
-                               STREAM(stream), (const KParams*)s->kp_dev, substeps);
-        });
-    else
-        hipLaunchKernelGGL(k_sim_step, grid_for(s, s->N), dim3(s->block), 0, STREAM(stream), s->dm,
-                           s->ds, s->sp, substeps);
-    LAUNCH_CHECK();
+    // deferred: consecutive steps on one stream with nothing reading or writing the state in
+    // between are issued as one launch (identical results: later substeps of a launch continue
+    // from the LDS copy of exactly the state a separate launch would reload); inside a stream
+    // capture, and with MI_SIM_DEFER=0, every call launches at once
+    if (!s->defer || capturing(STREAM(stream))) {
+        FLUSH(s, stream);
+        return launch_sim(s, substeps, STREAM(stream));
+    }
+    if (s->pending && s->pending_stream != STREAM(stream)) FLUSH(s, stream);
+    s->pending += substeps;
+    s->pending_stream = STREAM(stream);
+    if (s->pending >= 64) FLUSH(s, stream);
+    return MI_OK;
+}
+
+int mi_sim_flush(mi_sim* s, void* stream) {
+    NEED(s);
+    FLUSH(s, stream);
     return MI_OK;
 }
 
@@ -1456,6 +1543,7 @@ int mi_task_pre_step(mi_sim* s, const float* actions, int64_t* reset_buf, int64_
     NEED(s); NEED_TASK(s); NEED(actions); NEED(reset_buf); NEED(progress_buf);
     if (s->tp.kind != MI_TASK_CARTPOLE) { NEED(potentials); NEED(prev_potentials); }
     HIP_TRY(hipSetDevice(s->device));
+    FLUSH(s, stream);
     hipLaunchKernelGGL(k_pre_step, grid_for(s, s->N), dim3(s->block), 0, STREAM(stream), s->dm,
                        s->ds, s->tp, actions, reset_buf, progress_buf, potentials, prev_potentials,
                        actions_out);
@@ -1468,6 +1556,7 @@ int mi_task_reset_idx(mi_sim* s, const int64_t* env_ids, int32_t n, int64_t* res
     NEED(s); NEED_TASK(s);
     if (n < 0 || n > s->N || (!env_ids && n != s->N)) return fail(MI_E_SHAPE, "mi_task_reset_idx: bad n=%d", n);
     HIP_TRY(hipSetDevice(s->device));
+    FLUSH(s, stream);
     if (n == 0) return MI_OK;
     hipLaunchKernelGGL(k_reset_idx, grid_for(s, n), dim3(s->block), 0, STREAM(stream), s->dm, s->ds,
                        s->tp, env_ids, n, reset_buf, progress_buf, potentials, prev_potentials);
@@ -1480,6 +1569,7 @@ int mi_task_post_step(mi_sim* s, const float* actions, float* obs, float* rew, i
     NEED(s); NEED_TASK(s); NEED(obs); NEED(rew); NEED(reset_buf); NEED(progress_buf);
     if (s->tp.kind != MI_TASK_CARTPOLE) { NEED(actions); NEED(potentials); NEED(prev_potentials); }
     HIP_TRY(hipSetDevice(s->device));
+    FLUSH(s, stream);
     int var = post_tile_variant();
     if (var == 4) {   // 32p: several tiles per resident workgroup, next tile's loads in flight
         const int es = s->ds.es, ns = 6 * s->dm.S;
@@ -1568,6 +1658,7 @@ int mi_task_observations(mi_sim* s, const float* actions, float* obs, float* pot
     NEED(s); NEED_TASK(s); NEED(obs);
     if (s->tp.kind != MI_TASK_CARTPOLE) { NEED(actions); NEED(potentials); NEED(prev_potentials); }
     HIP_TRY(hipSetDevice(s->device));
+    FLUSH(s, stream);
     hipLaunchKernelGGL(k_observations, grid_for(s, s->N), dim3(s->block), 0, STREAM(stream), s->dm,
                        s->ds, s->tp, actions, obs, potentials, prev_potentials);
     LAUNCH_CHECK();
@@ -1579,6 +1670,7 @@ int mi_task_metrics(mi_sim* s, const float* actions, const float* obs, float* re
     NEED(s); NEED_TASK(s); NEED(obs); NEED(rew);
     if (s->tp.kind != MI_TASK_CARTPOLE) { NEED(actions); NEED(potentials); NEED(prev_potentials); }
     HIP_TRY(hipSetDevice(s->device));
+    FLUSH(s, stream);
     hipLaunchKernelGGL(k_metrics, grid_for(s, s->N), dim3(s->block), 0, STREAM(stream), s->dm,
                        s->ds, s->tp, actions, obs, rew, potentials, prev_potentials);
     LAUNCH_CHECK();
@@ -1589,6 +1681,7 @@ int mi_task_is_done(mi_sim* s, const float* obs, int64_t* reset_buf, const int64
                     void* stream) {
     NEED(s); NEED_TASK(s); NEED(obs); NEED(reset_buf); NEED(progress_buf);
     HIP_TRY(hipSetDevice(s->device));
+    FLUSH(s, stream);
     hipLaunchKernelGGL(k_is_done, grid_for(s, s->N), dim3(s->block), 0, STREAM(stream), s->ds,
                        s->tp, obs, reset_buf, progress_buf);
     LAUNCH_CHECK();
@@ -1622,6 +1715,7 @@ int mi_env_step(mi_sim* s, const float* actions, int32_t substeps, float* obs_ou
         return fail(MI_E_NULL, "mi_env_step: action DR needs actions_out (task.actions)");
     if (substeps < 0 || substeps > 64) return fail(MI_E_ARG, "substeps %d out of range", substeps);
     HIP_TRY(hipSetDevice(s->device));
+    FLUSH(s, stream);
     hipEvent_t ev0 = nullptr, ev1 = nullptr;
     HIP_TRY(timed_launch(s, stream, &ev0, &ev1));
     if (s->wave && s->tp.kind != MI_TASK_CARTPOLE)
@@ -1756,6 +1850,7 @@ int mi_fill_uniform(mi_sim* s, float* out, int32_t cols, uint64_t seed, uint64_t
 int mi_get_reset_count(mi_sim* s, uint32_t* out) {
     NEED(s); NEED(out);
     HIP_TRY(hipSetDevice(s->device));
+    FLUSH(s, s->pending_stream);
     HIP_TRY(hipDeviceSynchronize());
     HIP_TRY(hipMemcpy(out, s->ds.reset_count, sizeof(uint32_t) * s->N, hipMemcpyDeviceToHost));
     return MI_OK;
@@ -1764,6 +1859,7 @@ int mi_get_reset_count(mi_sim* s, uint32_t* out) {
 int mi_set_reset_count(mi_sim* s, const uint32_t* in) {
     NEED(s); NEED(in);
     HIP_TRY(hipSetDevice(s->device));
+    FLUSH(s, s->pending_stream);
     HIP_TRY(hipDeviceSynchronize());
     HIP_TRY(hipMemcpy(s->ds.reset_count, in, sizeof(uint32_t) * s->N, hipMemcpyHostToDevice));
     return MI_OK;

@@ -108,6 +108,7 @@ _SIGS = {
     "mi_set_root_state": (C.c_int, [C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p,
                                     C.c_int32, C.c_void_p]),
     "mi_sim_step": (C.c_int, [C.c_void_p, C.c_int32, C.c_void_p]),
+    "mi_sim_flush": (C.c_int, [C.c_void_p, C.c_void_p]),
     "mi_task_configure": (C.c_int, [C.c_void_p, C.POINTER(MiTaskParams)]),
     "mi_task_pre_step": (C.c_int, [C.c_void_p] + [C.c_void_p] * 7),
     "mi_task_reset_idx": (C.c_int, [C.c_void_p, C.c_void_p, C.c_int32] + [C.c_void_p] * 5),

@@ -131,3 +131,34 @@ def test_indexed_efforts_through_a_substep(gpu, name):
         np.testing.assert_allclose(got["pos"], p, rtol=tol, atol=tol)
     orc.close()
     env.close()
+
+
+@pytest.mark.parametrize("name", ["Humanoid", "Ant", "Cartpole"])
+def test_deferred_substeps_equal_immediate_launches(gpu, name, monkeypatch):
+    """World.step() twice (vec_env_rlgames.py:64-66) is one launch of two substeps, issued by the
+    next call that touches the state (include/mi_sim.h mi_sim_step): bit-identical to one launch
+    per World.step (MI_SIM_DEFER=0) through the method-by-method step and the getters."""
+    ea = make_env(name, num_envs=NENV, device="cuda:0", seed=4)
+    monkeypatch.setenv("MI_SIM_DEFER", "0")
+    eb = make_env(name, num_envs=NENV, device="cuda:0", seed=4)
+    monkeypatch.delenv("MI_SIM_DEFER")
+    for e in (ea, eb):
+        e.use_fused(False)
+        e.reset()
+    g = torch.Generator().manual_seed(8)
+    for k in range(4):
+        acts = (torch.rand((NENV, ea.num_actions), generator=g) * 2 - 1).cuda()
+        oa, ra, da, _ = ea.step(acts)
+        ob, rb, db, _ = eb.step(acts)
+        assert torch.equal(oa["obs"], ob["obs"]) and torch.equal(ra, rb) and torch.equal(da, db), k
+    # the reference's path (A) order: efforts, two World.step, then the getters
+    for e in (ea, eb):
+        v = e.task.get_robot()
+        v.set_joint_efforts(torch.ones((NENV, v.num_dof), device="cuda:0"))
+        e._world.step()
+        e._world.step()
+    sa, sb = _state(ea.task.get_robot()), _state(eb.task.get_robot())
+    for key in sa:
+        assert np.array_equal(sa[key], sb[key]), key
+    ea.close()
+    eb.close()

@@ -23,14 +23,11 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
 
 
-def main():
+def measure(task_name: str = "Humanoid", n: int = 4096, steps: int = 200) -> dict:
     import torch
 
     from omniisaacgymenvs_amd.utils.task_util import make_env
 
-    task_name = sys.argv[1] if len(sys.argv) > 1 else "Humanoid"
-    n = int(sys.argv[2]) if len(sys.argv) > 2 else 4096
-    steps = int(sys.argv[3]) if len(sys.argv) > 3 else 200
     env = make_env(task_name, num_envs=n, device="cuda:0", seed=5)
     t, view, world = env.task, env.task.get_robot(), env._world
     env.reset()
@@ -82,11 +79,19 @@ def main():
            "path_a_launches_per_step": 5 + subs + 5,
            "path_b_fused_ms_per_step": round(ms_b_wall, 4), "path_b_device_ms_per_step": round(ms_b_dev, 4),
            "note": "path A excludes the reference's torch task math (its own code, unchanged)"}
+    env.close()
+    return rec
+
+
+def main():
+    task_name = sys.argv[1] if len(sys.argv) > 1 else "Humanoid"
+    n = int(sys.argv[2]) if len(sys.argv) > 2 else 4096
+    steps = int(sys.argv[3]) if len(sys.argv) > 3 else 200
+    rec = measure(task_name, n, steps)
     print(json.dumps(rec), flush=True)
     os.makedirs(os.path.join(ROOT, "gpurun_out"), exist_ok=True)
     with open(os.path.join(ROOT, "gpurun_out", f"path_a_{task_name.lower()}.json"), "w") as f:
         json.dump(rec, f, indent=1)
-    env.close()
 
 
 if __name__ == "__main__":
