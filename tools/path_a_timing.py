@@ -9,9 +9,11 @@ Path (A) per env-step, the backend calls the reference makes
   controlFrequencyInv = 2 physics substeps: World.step()                     (vec_env_rlgames.py:64-66)
   get_observations: get_world_poses, get_velocities, get_joint_positions,
                     get_joint_velocities, get_force_sensor_forces            (locomotion.py:81-89)
-The reference's own torch task math (jit obs / reward / done) runs on top of these and is not
-counted: it is the reference's code, unchanged. Resets: 1 % of the envs per step (about the
-Humanoid reset rate under a random policy at 4096 envs).
+Resets follow the envs' own terminations (root z below terminationHeight or the episode
+length, locomotion.py:257-268) with the reference's reset_idx draws (:116-145) in torch, so
+the state distribution matches the fused path's; the rest of the reference's torch task math
+(jit observations / reward) runs on top of these and is not counted: it is the reference's
+code, unchanged. Actions U(-1, 1) as in scripts/random_policy.py:57.
 
 usage: path_a_timing.py [Task] [num_envs] [steps] -> one JSON line (+ gpurun_out/path_a_<task>.json)"""
 import json
@@ -34,28 +36,55 @@ def measure(task_name: str = "Humanoid", n: int = 4096, steps: int = 200) -> dic
     dev = "cuda:0"
     D = view.num_dof
     g = torch.Generator(device=dev).manual_seed(0)
-    efforts = torch.rand((n, D), device=dev, generator=g) * 2 - 1
     all_i32 = torch.arange(n, dtype=torch.int32, device=dev)
-    n_reset = max(1, n // 100)
-    q0 = view.get_joint_positions()[:n_reset].clone()
-    qd0 = torch.zeros_like(q0)
-    pos0, rot0 = view.get_world_poses()
-    pos0, rot0 = pos0[:n_reset].clone(), rot0[:n_reset].clone()
-    vel0 = torch.zeros((n_reset, 6), device=dev)
     subs = t.control_frequency_inv
+    # the reference's reset_idx inputs (locomotion.py:116-145): initial root pose, dof limits
+    pos0, rot0 = view.get_world_poses()
+    pos0 = t._env_pos + torch.tensor(t._spawn_translation, device=dev)
+    rot0 = torch.tensor([1.0, 0.0, 0.0, 0.0], device=dev).repeat(n, 1)
+    lim = view.get_dof_limits()[0]
+    lo, hi = lim[:, 0], lim[:, 1]
+    reset_buf = torch.zeros(n, dtype=torch.int64, device=dev)
+    progress = torch.zeros(n, dtype=torch.int64, device=dev)
+    term_h, max_len = float(t.termination_height), float(t._max_episode_length)
+
+    ev = []   # (start, stop) HIP events around each backend call when timing the backend alone
+
+    def backend(fn, *a, **kw):
+        if timing_backend:
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record()
+            r = fn(*a, **kw)
+            e1.record()
+            ev.append((e0, e1))
+            return r
+        return fn(*a, **kw)
 
     def path_a(k):
-        ids = (torch.arange(n_reset, device=dev, dtype=torch.int64) * 97 + k * 13) % n
-        view.set_joint_positions(q0, indices=ids)
-        view.set_joint_velocities(qd0, indices=ids)
-        view.set_world_poses(pos0, rot0, indices=ids)
-        view.set_velocities(vel0, indices=ids)
-        view.set_joint_efforts(efforts, indices=all_i32)
+        # pre_physics_step (locomotion.py:103-114): nonzero() (host sync) -> reset_idx's four
+        # indexed scatters, then the efforts
+        ids = reset_buf.nonzero(as_tuple=False).squeeze(-1)
+        if len(ids) > 0:
+            m = len(ids)
+            q = torch.clamp(torch.rand((m, D), device=dev, generator=g) * 0.4 - 0.2, lo, hi)
+            qd = torch.rand((m, D), device=dev, generator=g) * 0.2 - 0.1
+            pr, rr, z6 = pos0[ids], rot0[ids], torch.zeros((m, 6), device=dev)
+            backend(view.set_joint_positions, q, indices=ids)
+            backend(view.set_joint_velocities, qd, indices=ids)
+            backend(view.set_world_poses, pr, rr, indices=ids)
+            backend(view.set_velocities, z6, indices=ids)
+            reset_buf[ids] = 0
+            progress[ids] = 0
+        forces = (torch.rand((n, D), device=dev, generator=g) * 2 - 1) * t.joint_gears * t.power_scale
+        backend(view.set_joint_efforts, forces, indices=all_i32)
         for _ in range(subs):
             world.step()
-        out = (view.get_world_poses(clone=False), view.get_velocities(clone=False),
-               view.get_joint_positions(clone=False), view.get_joint_velocities(clone=False),
-               view._physics_view.get_force_sensor_forces())
+        out = (backend(view.get_world_poses, clone=False), backend(view.get_velocities, clone=False),
+               backend(view.get_joint_positions, clone=False), backend(view.get_joint_velocities, clone=False),
+               backend(view._physics_view.get_force_sensor_forces))
+        # is_done's state-driving part (locomotion.py:257-268): fallen or timed out -> reset
+        progress.add_(1)
+        reset_buf.copy_(((out[0][0][:, 2] < term_h) | (progress >= max_len - 1)).to(torch.int64))
         return out
 
     def timed(fn, k0):
@@ -71,14 +100,26 @@ def measure(task_name: str = "Humanoid", n: int = 4096, steps: int = 200) -> dic
         torch.cuda.synchronize()
         return (time.perf_counter() - t0) / steps * 1e3, a.elapsed_time(b) / steps
 
+    timing_backend = False
     ms_a_wall, ms_a_dev = timed(path_a, 0)
+    # the same loop with events around the backend calls: the backend's own device time per step
+    # (the deferred physics launch is issued inside get_world_poses, so it is included)
+    timing_backend = True
+    ev.clear()
+    timed(path_a, 5000)
+    torch.cuda.synchronize()
+    backend_ms = sum(a.elapsed_time(b) for a, b in ev[-(len(ev) * steps // (steps + 20)):]) / steps
     acts = torch.rand((8, n, t.num_actions), device=dev, generator=g) * 2 - 1
     ms_b_wall, ms_b_dev = timed(lambda k: env.step(acts[k % 8]), 1000)
-    rec = {"task": task_name, "num_envs": n, "steps": steps, "resets_per_step": n_reset,
-           "path_a_backend_ms_per_step": round(ms_a_wall, 4), "path_a_device_ms_per_step": round(ms_a_dev, 4),
-           "path_a_launches_per_step": 5 + subs + 5,
+    rec = {"task": task_name, "num_envs": n, "steps": steps,
+           "path_a_ms_per_step": round(ms_a_wall, 4), "path_a_device_ms_per_step": round(ms_a_dev, 4),
+           "path_a_backend_device_ms_per_step": round(backend_ms, 4),
+           "path_a_launches_per_step": "1 physics (deferred substeps) + 4 getters + efforts "
+                                       "+ 4 reset scatters when any env is due",
            "path_b_fused_ms_per_step": round(ms_b_wall, 4), "path_b_device_ms_per_step": round(ms_b_dev, 4),
-           "note": "path A excludes the reference's torch task math (its own code, unchanged)"}
+           "note": "path A: the reference's call sequence incl. its reset / termination torch ops and "
+                   "nonzero() host sync; jit observation / reward math excluded. backend_device: "
+                   "the libmi_sim calls alone (HIP events around each)"}
     env.close()
     return rec
 
