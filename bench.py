@@ -262,9 +262,9 @@ def kernel_name(view, task) -> str:
     """Name of the fused env-step kernel this configuration launches."""
     from omniisaacgymenvs_amd import native as N
     path, topo, _ = view.sim_kernel_path()
-    if path == 1 and task.task_params().task_kind != N.MI_TASK_CARTPOLE:   # wave path
-        return "k_env_step_wave<" + {0: "TopoRuntime", 1: "TopoCT<RobotHumanoid>",
-                                     2: "TopoCT<RobotAnt>"}.get(topo, str(topo)) + ">"
+    if path in (1, 2) and task.task_params().task_kind != N.MI_TASK_CARTPOLE:   # wave / paired path
+        return ("k_env_step_wave<" if path == 1 else "k_env_step_pair<") + {
+            0: "TopoRuntime", 1: "TopoCT<RobotHumanoid>", 2: "TopoCT<RobotAnt>"}.get(topo, str(topo)) + ">"
     return "k_env_step"
 
 

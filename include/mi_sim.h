@@ -277,7 +277,8 @@ int mi_get_reset_count(mi_sim* sim, uint32_t* out /*[N] host*/);
 int mi_set_reset_count(mi_sim* sim, const uint32_t* in /*[N] host*/);
 /* Number of env-steps whose physics produced a non-finite state and were forced to reset. */
 int mi_sim_nan_count(mi_sim* sim, int64_t* count);
-/* Diagnostics: which physics kernel runs. path: 0 one-lane-per-env, 1 wavefront-per-env;
+/* Diagnostics: which physics kernel runs. path: 0 one-lane-per-env, 1 wavefront-per-env,
+ * 2 two envs per wavefront (MI_WAVE_PAIR=1, compiled topologies);
  * topology: id of the compile-time (model-specialised) topology, 0 = runtime tables;
  * lds_bytes: LDS per env (= per workgroup) of the wave path. Any output may be NULL. */
 int mi_sim_kernel_path(const mi_sim* sim, int32_t* path, int32_t* topology, int32_t* lds_bytes);

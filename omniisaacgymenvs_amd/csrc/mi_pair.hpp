@@ -1,0 +1,872 @@
+// mi_pair.hpp — two envs per wavefront (gfx950), for compiled topologies with nv <= 32.
+//
+// The wavefront-per-env kernel (mi_wave.hpp) runs most phases on one lane per DOF, link or
+// constraint row: 22-27 of the 64 lanes for the Humanoid. Here each 32-lane half of a wave owns
+// one env, so every instruction advances two envs, and a workgroup of 8 waves holds 16 envs —
+// the whole per-CU share of a 4096-env launch resident in ONE round (the wave kernel runs two
+// rounds of 8 envs per CU: its registers allow 2 waves per SIMD). Same algorithm, same constraint
+// rows in the same order, same task math as mi_wave.hpp and the oracle; what changes is the
+// mapping:
+//   * lane = lane & 31 inside the env's half; cross-lane broadcasts read the half's own lane
+//     (pbc: two v_readlane + a select), ballots are taken per half (hballot);
+//   * per-env counts (contacts, constraint rows, survivors) are per-half values; loops run to
+//     the larger of the two halves with per-half guards;
+//   * LDS per env is cut to what 16 envs per CU allow: no stored J rows (the Delassus set-up
+//     rebuilds J_r in lane r from the contact data), W rows up to the budget (the rest of a
+//     row-heavy substep goes through the env's global slab).
+// Requirements checked on the host: compiled topology, nv <= 32, npts <= 64, even env count.
+#pragma once
+#include "mi_wave.hpp"
+
+namespace mi {
+
+MI_D int pair_l64() { return (int)(threadIdx.x & 63u); }
+// v of lane k of this lane's half (k wave-uniform)
+MI_D float pbc(float v, int k) {
+    const float a = readlane(v, k), b = readlane(v, k + 32);
+    return (pair_l64() & 32) ? b : a;
+}
+MI_D int pbci(int v, int k) {
+    const int a = __builtin_amdgcn_readlane(v, k), b = __builtin_amdgcn_readlane(v, k + 32);
+    return (pair_l64() & 32) ? b : a;
+}
+// ballot of this lane's half, bit j = half lane j
+MI_D unsigned hballot(bool p) {
+    const unsigned long long m = __ballot(p);
+    return (unsigned)(m >> (pair_l64() & 32));
+}
+MI_D unsigned lanemask_lt(int lane) { return (1u << lane) - 1u; }
+// larger of the two halves' (half-uniform) values: wave-uniform
+MI_D int pmax(int v) { return max(__builtin_amdgcn_readlane(v, 0), __builtin_amdgcn_readlane(v, 32)); }
+// sum over each 32-lane half, returned to every lane of the half
+MI_D float psum(float v) { return pbc(half_sums(v), 31); }
+
+// in-register tree LTDL (ct_ltdl) with per-half broadcasts
+template <class T>
+MI_D void ct_ltdl_pair(int lane, float (&Mc)[T::nvc]) {
+    sfor_down<0, T::nv>([&](auto K) {
+        constexpr int k = K;
+        __builtin_amdgcn_sched_barrier(0);
+        const int ln = lane_here(lane);
+        const float inv = __builtin_amdgcn_rcpf(pbc(Mc[k], k));
+        sfor<T::dof.anc_start[k], T::dof.anc_start[k + 1]>([&](auto A) {
+            constexpr int ii = T::dof.anc[A];
+            const float s = pbc(Mc[k], ii) * inv;
+            if (ln <= ii) Mc[ii] -= s * Mc[k];
+        });
+        if (ln < k) Mc[k] = Mc[k] * inv;
+    });
+}
+
+// J_r[c] of this lane's constraint row r (contact or limit), for every DOF c (lane = row)
+template <class TP>
+MI_D void pair_jrow(const MC& mc, const WaveTabs& t, const float* sm, int r, int nr,
+                    float (&J)[TP::nvc]) {
+    const float lk = sm[t.s_rl + r];
+    float f[6] = {0.0f, 0.0f, 0.0f, 0.0f, 0.0f, 0.0f};
+    unsigned msk = 0u, msk2 = 0u;
+    float sg = 0.0f;
+    int kdof = -1;
+    if (lk >= 0.0f) {
+        msk = mc.mask((int)lk);
+        const float l2 = TP::kSelf ? sm[t.s_cl2 + r / 3] : -1.0f;
+        msk2 = l2 >= 0.0f ? mc.mask((int)l2) : 0u;
+        contact_row_f<TP::kSelf>(sm, t, r, f);
+    } else {
+        kdof = (int)(-lk - 1.0f);
+        sg = sm[t.s_lsg + kdof - nr];
+    }
+    const float* Ss = sm + t.s_S;
+    sfor<0, TP::nv>([&](auto C) {
+        constexpr int c = C;
+        float sv[6];
+#pragma unroll
+        for (int q = 0; q < 6; ++q) sv[q] = Ss[6 * c + q];
+        const float v = dot6(sv, f);
+        const bool ia = (msk >> c) & 1u, ib = (msk2 >> c) & 1u;
+        float xc = (ia ? v : 0.0f) - (ib ? v : 0.0f);
+        asm volatile("" : "+v"(xc));
+        J[c] = kdof >= 0 ? (kdof == c ? sg : 0.0f) : xc;
+    });
+}
+
+// W row r of this lane's env: LDS rows [0, w_rows_lds) (one segment: the pair layout has no
+// second), the env's global slab beyond
+MI_D const float* pair_wrow(const WaveTabs& t, const float* sm, const float* gW, int r, int nv) {
+    return r < t.w_rows_lds ? sm + t.s_W + r * nv : gW + (size_t)r * WNV;
+}
+
+// One articulated substep of the env of this lane's half (env i, LDS region sm, W slab gW).
+template <class TP>
+MI_D void pair_artic_substep(const DevModel& m, const WaveTabs& t, const DevState& st,
+                             const SimP& p, int i, const float* mcb, float* sm, float* gW,
+                             bool load_state, bool store_state) {
+    static_assert(TP::kCT && TP::nv <= 32, "paired kernel: compiled topology, nv <= 32");
+    const int lane = pair_l64() & 31;
+    const int N = st.N, L = m.L, D = m.D, nv = m.nv, nr = m.nr;
+    (void)N;
+    const float dt = p.dt;
+    float* us = sm + t.s_us;
+    float* rhs = sm + t.s_r;
+    float* Mx = sm + t.s_M;
+    float* Ss = sm + t.s_S;
+    const MC mc = make_mc(t, mcb, L);
+
+    if (load_state) {
+        if (lane < 3) sm[t.s_rp + lane] = st.root_pos[sx(st, lane, i)];
+        if (lane < 4) sm[t.s_rp + 4 + lane] = st.root_quat[sx(st, lane, i)];
+        if (lane < nr) us[lane] = st.root_vel[sx(st, lane, i)];
+        else if (lane < nv) us[lane] = st.qd[sx(st, lane - nr, i)];
+        if (lane < D) sm[t.s_q + lane] = st.q[sx(st, lane, i)];
+    }
+    if (nr && lane < 6) {
+        float s[6] = {0, 0, 0, 0, 0, 0};
+        if (lane < 3) s[3 + lane] = 1.0f; else s[lane - 3] = 1.0f;
+#pragma unroll
+        for (int c = 0; c < 6; ++c) Ss[6 * lane + c] = s[c];
+    }
+    wave_sync();
+    // ---- P1: local transforms, then chain walks + link inertia / Newton-Euler (lane = link)
+    for (int l = 1 + lane; l < L; l += 32) wave_link_local(mc, t, sm, l);
+    wave_sync();
+    for (int l = lane; l < L; l += 32) wave_link_forward(mc, nr, t, sm, l, p);
+    wave_sync();
+    // ---- P2: composite inertia / force
+    float* aux = sm + t.s_X;
+    {
+        const float4* recs = reinterpret_cast<const float4*>(sm + t.s_F);
+        for (int l = lane; l < L; l += 32) {
+            float4 a0 = recs[4 * l], a1 = recs[4 * l + 1], a2 = recs[4 * l + 2], a3 = recs[4 * l + 3];
+            for (int di = mc.desc_start(l); di < mc.desc_start(l + 1); ++di) {
+                const int d = mc.desc(di);
+                const float4 b0 = recs[4 * d], b1 = recs[4 * d + 1], b2 = recs[4 * d + 2], b3 = recs[4 * d + 3];
+                a0.x += b0.x; a0.y += b0.y; a0.z += b0.z; a0.w += b0.w;
+                a1.x += b1.x; a1.y += b1.y; a1.z += b1.z; a1.w += b1.w;
+                a2.x += b2.x; a2.y += b2.y; a2.z += b2.z; a2.w += b2.w;
+                a3.x += b3.x; a3.y += b3.y; a3.z += b3.z; a3.w += b3.w;
+            }
+            float4* o = reinterpret_cast<float4*>(aux) + 4 * l;
+            o[0] = a0; o[1] = a1; o[2] = a2; o[3] = a3;
+        }
+    }
+    wave_sync();
+    // ---- P3: bias + CRBA rows (lane = DOF)
+    if (lane < nv) {
+        const int k = lane, l = k < nr ? 0 : k - nr + 1;
+        float s[6], I[10], f[6], F[6];
+#pragma unroll
+        for (int c = 0; c < 6; ++c) s[c] = Ss[6 * k + c];
+        {
+            const float4* rec = reinterpret_cast<const float4*>(aux) + 4 * l;
+            const float4 a0 = rec[0], a1 = rec[1], a2 = rec[2], a3 = rec[3];
+            I[0] = a0.x; I[1] = a0.y; I[2] = a0.z; I[3] = a0.w;
+            I[4] = a1.x; I[5] = a1.y; I[6] = a1.z; I[7] = a1.w;
+            I[8] = a2.x; I[9] = a2.y; F[0] = a2.z; F[1] = a2.w;
+            F[2] = a3.x; F[3] = a3.y; F[4] = a3.z; F[5] = a3.w;
+        }
+        inertia_mul(I, s, f);
+        float diag = dot6(s, f);
+        float r = -dot6(s, F);
+        if (k >= nr) {
+            const float damp = mc.lf(MC_DAMP, l);
+            diag += mc.lf(MC_ARM, l) + dt * damp;
+            r += st.eff[sx(st, k - nr, i)] - damp * us[k];
+        }
+        rhs[k] = r;
+        sfor<0, TP::nv>([&](auto J) {
+            constexpr int j = J;
+            float sj[6];
+#pragma unroll
+            for (int c = 0; c < 6; ++c) sj[c] = Ss[6 * j + c];
+            Mx[k * nv + j] = dot6(sj, f);
+        });
+        Mx[k * nv + k] = diag;
+    }
+    wave_sync();
+    // ---- P4: register LTDL (lane = column), factor published to LDS
+    float Mc[TP::nvc];
+    ct_load_columns<TP>(Mx, lane, Mc);
+    ct_ltdl_pair<TP>(lane, Mc);
+    const float dvec = ct_dinv<TP>(lane, Mc);
+    {
+        const int dj = lane < nr ? lane : __builtin_popcount(mc.mask(lane < nv ? lane - nr + 1 : 0)) - 1;
+        ct_publish_factor<TP>(lane, dj, Mc, dvec, sm + t.s_L);
+    }
+    // ---- P8: ground contacts (lanes over candidate points, two passes past 32), ballot
+    // compaction per half in candidate order
+    int ncon = 0;
+    {
+        const float rpz = sm[t.s_rp + 2];
+        for (int c0 = 0; c0 < t.npts; c0 += 32) {
+            const int c = c0 + lane;
+            bool act = false;
+            float pc[3] = {0, 0, 0}, bn = 0.0f;
+            int l = 0;
+            if (c < t.npts) {
+                l = (int)mc.pf(MP_LINK, c);
+                const float pl[3] = {mc.pf(MP_X, c), mc.pf(MP_X + 1, c), mc.pf(MP_X + 2, c)};
+                float R[9], x[3];
+#pragma unroll
+                for (int q = 0; q < 9; ++q) R[q] = sm[t.s_R + 9 * l + q];
+                m3_vec(R, pl, x);
+#pragma unroll
+                for (int q = 0; q < 3; ++q) x[q] += sm[t.s_o + 3 * l + q];
+                const float rr = mc.pf(MP_RAD, c);
+                const float gap = rpz + x[2] - rr;
+                act = gap < p.contact_offset;
+                pc[0] = x[0]; pc[1] = x[1]; pc[2] = x[2] - rr;
+                const float d = gap - p.rest_offset;
+                bn = d >= 0.0f ? -d / dt : -p.erp * d / dt;
+                if (bn > p.max_depen) bn = p.max_depen;
+            }
+            const unsigned mask = hballot(act);
+            if (act) {
+                const int ci = ncon + __popc(mask & lanemask_lt(lane));
+#pragma unroll
+                for (int q = 0; q < 3; ++q) sm[t.s_cp + 3 * ci + q] = pc[q];
+                sm[t.s_cl + ci] = (float)l;
+                sm[t.s_cl2 + ci] = -1.0f;
+#pragma unroll
+                for (int tt = 0; tt < 3; ++tt) {
+                    const int r = 3 * ci + tt;
+                    sm[t.s_rl + r] = (float)l;
+                    sm[t.s_rb + r] = tt == 0 ? bn : 0.0f;
+                    sm[t.s_rk + r] = (float)tt;
+                }
+            }
+            ncon += __popc(mask);
+        }
+    }
+    // self-contacts (Humanoid.yaml:80): lanes over geom pairs, compacted in pair order within the
+    // MI_MAX_ROWS budget, after the ground contacts (as the oracle)
+    if constexpr (TP::kSelf) {
+        if (t.self_on) {
+            float* seg = sm + t.s_seg;
+            float* bnd = seg + 8 * t.ngeoms;
+            const float* geo = mcb + t.mc_geo;
+            const int2* gpr = reinterpret_cast<const int2*>(t.g_pairs);
+            int2 gpf[5];
+#pragma unroll
+            for (int q = 0; q < 5; ++q) {
+                const int pi = 32 * q + lane;
+                gpf[q] = pi < t.npairs ? gpr[pi] : make_int2(0, 0);
+            }
+            for (int g = lane; g < t.ngeoms; g += 32) {
+                const float* A = geo + 8 * g;
+                const int l = (int)A[0];
+                float R[9], a0[3], a1[3];
+#pragma unroll
+                for (int q = 0; q < 9; ++q) R[q] = sm[t.s_R + 9 * l + q];
+                m3_vec(R, A + 1, a0); m3_vec(R, A + 4, a1);
+#pragma unroll
+                for (int q = 0; q < 3; ++q) {
+                    seg[8 * g + q] = a0[q] + sm[t.s_o + 3 * l + q];
+                    seg[8 * g + 3 + q] = a1[q] + sm[t.s_o + 3 * l + q];
+                }
+                seg[8 * g + 6] = A[7];
+                seg[8 * g + 7] = (float)l;
+                float e2 = 0.0f;
+#pragma unroll
+                for (int q = 0; q < 3; ++q) {
+                    bnd[4 * g + q] = sm[t.s_o + 3 * l + q] + 0.5f * (a0[q] + a1[q]);
+                    e2 += (a1[q] - a0[q]) * (a1[q] - a0[q]);
+                }
+                bnd[4 * g + 3] = 0.5f * sqrtf(e2) + A[7];
+            }
+            wave_sync();
+            int* surv = reinterpret_cast<int*>(sm + t.s_surv);
+            int nsv = 0;
+            const float slack = p.contact_offset + 1e-3f;
+            for (int pb = 0; pb < t.npairs; pb += 32) {
+                const int pi = pb + lane;
+                bool keep = false;
+                int2 gp = make_int2(0, 0);
+                if (pi < t.npairs) {
+                    const int q = pb >> 5;
+                    gp = q == 0 ? gpf[0] : q == 1 ? gpf[1] : q == 2 ? gpf[2] : q == 3 ? gpf[3] : q == 4 ? gpf[4] : gpr[pi];
+                    const float4 A = *reinterpret_cast<const float4*>(bnd + 4 * gp.x);
+                    const float4 B = *reinterpret_cast<const float4*>(bnd + 4 * gp.y);
+                    const float cx = A.x - B.x, cy = A.y - B.y, cz = A.z - B.z;
+                    const float reach = A.w + B.w + slack;
+                    keep = cx * cx + cy * cy + cz * cz < reach * reach;
+                }
+                const unsigned mask = hballot(keep);
+                if (keep) surv[nsv + __popc(mask & lanemask_lt(lane))] = gp.x | (gp.y << 16);
+                nsv += __popc(mask);
+            }
+            wave_sync();
+            int budget = (MI_MAX_ROWS - 3 * ncon - t.nlimc) / 3;
+            const int nsv_max = pmax(nsv);
+            for (int sb = 0; sb < nsv_max; sb += 32) {
+                const int sidx = sb + lane;
+                bool act = false;
+                float pc[3], n[3], bn = 0.0f;
+                int la = 0, lb = 0;
+                if (sidx < nsv && budget > 0) {
+                    const int pk = surv[sidx];
+                    const float* A = seg + 8 * (pk & 0xffff);
+                    const float* B = seg + 8 * (pk >> 16);
+                    la = (int)A[7]; lb = (int)B[7];
+                    const float gap = mi_pair_contact(A, A + 3, A[6], B, B + 3, B[6], pc, n);
+                    act = gap < p.contact_offset;
+                    const float d = gap - p.rest_offset;
+                    bn = d >= 0.0f ? -d / dt : -p.erp * d / dt;
+                    if (bn > p.max_depen) bn = p.max_depen;
+                }
+                const unsigned mask = hballot(act);
+                const int rank = __popc(mask & lanemask_lt(lane));
+                if (act && rank < budget) {
+                    const int ci = ncon + rank;
+#pragma unroll
+                    for (int q = 0; q < 3; ++q) { sm[t.s_cp + 3 * ci + q] = pc[q]; sm[t.s_cn + 3 * ci + q] = n[q]; }
+                    sm[t.s_cl + ci] = (float)la;
+                    sm[t.s_cl2 + ci] = (float)lb;
+#pragma unroll
+                    for (int tt = 0; tt < 3; ++tt) {
+                        const int r = 3 * ci + tt;
+                        sm[t.s_rl + r] = (float)la;
+                        sm[t.s_rb + r] = tt == 0 ? bn : 0.0f;
+                        sm[t.s_rk + r] = (float)tt;
+                    }
+                }
+                const int took = budget > 0 ? min(__popc(mask), budget) : 0;
+                ncon += took;
+                budget -= took;
+            }
+        }
+    }
+    const int nc = 3 * ncon;
+    wave_sync();
+    // ---- P7+P9: one batch per half, lanes over solve vectors (rhs, limit candidates, contact
+    // rows); passes of 32 to the larger half's count
+    const int nlim = t.nlimc;
+    const int total = 1 + nlim + nc;
+    const int total_max = pmax(total);
+    int nrows = nc;
+    unsigned limact = 0u;
+    auto limit_rows = [&](const auto& res) {
+        constexpr int NR = sizeof(res) / sizeof(res[0]);
+        if (lane == 0) {
+#pragma unroll
+            for (int c = 0; c < NR; ++c)
+                if (c < nv) us[c] = us[c] + dt * res[c];
+        }
+        wave_sync();
+        bool act = false;
+        float bl = 0.0f, sg = 0.0f;
+        if (lane < D) {
+            const int l = lane + 1, k = nr + lane;
+            const float lo = mc.lf(MC_LO, l), hi = mc.lf(MC_HI, l);
+            if (lo < hi) {
+                const float qj = sm[t.s_q + lane];
+                const float qp = qj + dt * us[k];
+                float d = 0.0f;
+                if (qj < lo || qp < lo) { d = qj - lo; sg = 1.0f; act = true; }
+                else if (qj > hi || qp > hi) { d = hi - qj; sg = -1.0f; act = true; }
+                bl = d >= 0.0f ? -d / dt : -p.erp * d / dt;
+                if (bl > p.max_depen) bl = p.max_depen;
+            }
+        }
+        limact = hballot(act);
+        if (act) {
+            const int rl = nc + __popc(limact & lanemask_lt(lane));
+            sm[t.s_rl + rl] = -(float)(nr + lane) - 1.0f;
+            sm[t.s_lsg + lane] = sg;
+            sm[t.s_rb + rl] = bl;
+            sm[t.s_rk + rl] = 3.0f;
+        }
+        nrows = nc + __popc(limact);
+        wave_sync();
+    };
+    auto file_row = [&](const auto& res, bool on, int r, int kd, float a_contact) {
+        constexpr int NR = sizeof(res) / sizeof(res[0]);
+        int slot = -1;
+        float sc = 1.0f, a = 0.0f;
+        if (on && r >= 0) {
+            slot = r;
+            a = a_contact;
+        } else if (kd >= 0) {
+            const int d = kd - nr;
+            if ((limact >> d) & 1u) {
+                slot = nc + __popc(limact & lanemask_lt(d));
+                sc = sm[t.s_lsg + d];
+                float wk = 0.0f;
+#pragma unroll
+                for (int c = 0; c < NR; ++c) wk = c == kd ? res[c] : wk;
+                a = wk;
+            }
+        }
+        if (slot >= 0) {
+            sm[t.s_ad + slot] = a > 1e-12f ? a : 1e-12f;
+            if (slot < t.w_rows_lds) {
+                float* wl = sm + t.s_W + slot * nv;
+#pragma unroll
+                for (int c = 0; c < NR; ++c)
+                    if (c < nv) wl[c] = res[c] * sc;
+            } else {
+#pragma unroll
+                for (int c = 0; c < WNV; ++c) gW[(size_t)slot * WNV + c] = c < NR ? res[c] * sc : 0.0f;
+            }
+        }
+    };
+    for (int base = 0; base < total_max; base += 32) {
+        const int bv = base + lane;
+        const bool on = bv < total;
+        const int r = bv - 1 - nlim;
+        const int kd = (on && bv > 0 && r < 0) ? nr + mc.lim(bv - 1) : -1;
+        float x[TP::nvc];
+        const bool crow = on && r >= 0;
+        float f[6] = {0.0f, 0.0f, 0.0f, 0.0f, 0.0f, 0.0f};
+        unsigned msk = 0u, msk2 = 0u;
+        if (crow) {
+            const int l = (int)sm[t.s_rl + r];
+            const float l2 = TP::kSelf ? sm[t.s_cl2 + r / 3] : -1.0f;
+            msk = mc.mask(l);
+            msk2 = l2 >= 0.0f ? mc.mask((int)l2) : 0u;
+            contact_row_f<TP::kSelf>(sm, t, r, f);
+        }
+        sfor<0, TP::nv>([&](auto C) {
+            constexpr int c = C;
+            float sv[6];
+#pragma unroll
+            for (int q = 0; q < 6; ++q) sv[q] = Ss[6 * c + q];
+            const float v = dot6(sv, f);
+            const bool ia = (msk >> c) & 1u, ib = (msk2 >> c) & 1u;
+            float xc = (ia ? v : 0.0f) - (ib ? v : 0.0f);
+            float rc = rhs[c];
+            asm volatile("" : "+v"(xc), "+v"(rc));
+            x[c] = crow ? xc : (bv == 0 ? rc : (kd == c ? 1.0f : 0.0f));
+        });
+        float a;
+        ct_solve_l<TP>(sm + t.s_L, x, a);
+        if (base == 0) limit_rows(x);
+        file_row(x, on, r, kd, a);
+    }
+    wave_sync();
+    // ---- P10: projected Gauss-Seidel, 4 sweeps
+    const int nrows_max = pmax(nrows);
+    if (nrows_max <= TP::kLamRows) {
+        // Delassus space: lane r holds row r's v_r = J_r . u and A[r][s] = J_r . W_s (J_r rebuilt
+        // here from the contact data: no J rows in LDS; W rows past the LDS ones from the slab)
+        constexpr int NV = TP::nv;
+        constexpr int RMAX = TP::kLamRows;
+        float b = 0.0f, ia = 1.0f, kd = 0.0f, lam = 0.0f;
+        if (lane < nrows) {
+            b = sm[t.s_rb + lane];
+            ia = 1.0f / sm[t.s_ad + lane];
+            kd = sm[t.s_rk + lane];
+        }
+        const int rl = lane < nrows ? lane : 0;
+        float Jr[TP::nvc];
+        if (nrows > 0) pair_jrow<TP>(mc, t, sm, rl, nr, Jr);
+        else sfor<0, NV>([&](auto C) { Jr[C] = 0.0f; });
+        float v = 0.0f;
+        sfor<0, NV>([&](auto C) { v += Jr[C] * us[C]; });
+        const int last = max(nrows - 1, 0);
+        float Ar[RMAX];
+        static_assert(RMAX % 4 == 0, "Delassus rows are built four at a time");
+#pragma unroll
+        for (int g0 = 0; g0 < RMAX; g0 += 4) {
+            float a0 = 0.0f, a1 = 0.0f, a2 = 0.0f, a3 = 0.0f;
+            if (g0 < nrows_max) {
+                auto dots = [&](const float* w0, const float* w1, const float* w2, const float* w3) {
+                    sfor<0, NV>([&](auto C) {
+                        a0 += Jr[C] * w0[C];
+                        a1 += Jr[C] * w1[C];
+                        a2 += Jr[C] * w2[C];
+                        a3 += Jr[C] * w3[C];
+                    });
+                };
+                if (g0 + 3 < t.w_rows_lds)   // uniform: all four rows in LDS (ds_read)
+                    dots(sm + t.s_W + min(g0, last) * NV, sm + t.s_W + min(g0 + 1, last) * NV,
+                         sm + t.s_W + min(g0 + 2, last) * NV, sm + t.s_W + min(g0 + 3, last) * NV);
+                else
+                    dots(pair_wrow(t, sm, gW, min(g0, last), NV), pair_wrow(t, sm, gW, min(g0 + 1, last), NV),
+                         pair_wrow(t, sm, gW, min(g0 + 2, last), NV), pair_wrow(t, sm, gW, min(g0 + 3, last), NV));
+            }
+            Ar[g0] = a0; Ar[g0 + 1] = a1; Ar[g0 + 2] = a2; Ar[g0 + 3] = a3;
+        }
+        const float mu = p.friction;
+        for (int it = 0; it < p.iters; ++it) {
+            asm volatile("" : "+v"(b), "+v"(ia), "+v"(kd));
+            int nrow_it = nrows_max;
+            asm volatile("" : "+s"(nrow_it));
+            float lamn = 0.0f;
+#pragma unroll
+            for (int rr = 0; rr < RMAX; ++rr) {
+                if (rr >= nrow_it) break;
+                __builtin_amdgcn_sched_barrier(0);
+                const float vr = pbc(v, rr);
+                const float br = pbc(b, rr), iar = pbc(ia, rr);
+                const float l0 = pbc(lam, rr);
+                const int kind = (int)pbc(kd, rr);
+                float ln = l0 + (br - vr) * iar;
+                const bool fric = kind == 1 || kind == 2;
+                const float lim = mu * lamn;
+                ln = fmaxf(ln, fric ? -lim : 0.0f);
+                ln = fric ? fminf(ln, lim) : ln;
+                const bool live_row = rr < nrows;
+                lamn = (live_row && kind == 0) ? ln : lamn;
+                v = live_row ? v + Ar[rr] * (ln - l0) : v;
+                if (live_row && lane_here(lane) == rr) lam = ln;
+            }
+        }
+        float u = lane < NV ? us[lane] : 0.0f;
+        const int kc = lane < NV ? lane : 0;
+#pragma unroll
+        for (int g0 = 0; g0 < RMAX; g0 += 4) {
+            if (g0 >= nrows_max) break;
+            float wq[4], lq[4];
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+                wq[q] = g0 + 3 < t.w_rows_lds ? sm[t.s_W + min(g0 + q, last) * NV + kc]
+                                              : pair_wrow(t, sm, gW, min(g0 + q, last), NV)[kc];
+                lq[q] = pbc(lam, g0 + q);
+            }
+#pragma unroll
+            for (int q = 0; q < 4; ++q) u = g0 + q < nrows ? u + wq[q] * lq[q] : u;
+        }
+        if (lane < NV) us[lane] = u;
+        if (lane < nrows) sm[t.s_ad + lane] = lam;           // reuse: lambda of row lane
+    } else {
+        // fallback (a half with more rows than the Delassus registers hold, 0.4 % of Humanoid
+        // substeps): u-space sweeps row by row, row data from LDS, W rows from LDS / the global
+        // slab, lambdas in LDS (s_lam); lane = DOF
+        float* lamv = sm + t.s_lam;
+        for (int r = lane; r < nrows; r += 32) lamv[r] = 0.0f;
+        float S6[6];
+#pragma unroll
+        for (int q = 0; q < 6; ++q) S6[q] = lane < nv ? Ss[6 * lane + q] : 0.0f;
+        float u = lane < nv ? us[lane] : 0.0f;
+        const int kc = lane < nv ? lane : 0;
+        const float kin = lane < nv ? 1.0f : 0.0f;
+        const float mu = p.friction;
+        wave_sync();
+        for (int it = 0; it < p.iters; ++it) {
+            float lamn = 0.0f;
+            for (int r = 0; r < nrows_max; ++r) {
+                const bool live_row = r < nrows;
+                const int rs = live_row ? r : 0;
+                const float br = sm[t.s_rb + rs], ar = sm[t.s_ad + rs];
+                const int kind = (int)sm[t.s_rk + rs];
+                const float lk = sm[t.s_rl + rs];
+                float jc;
+                if (lk >= 0.0f) {
+                    float fr[6];
+                    contact_row_f<TP::kSelf>(sm, t, rs, fr);
+                    const unsigned msk = mc.mask((int)lk);
+                    const float l2 = TP::kSelf ? sm[t.s_cl2 + rs / 3] : -1.0f;
+                    const unsigned msk2 = l2 >= 0.0f ? mc.mask((int)l2) : 0u;
+                    const float v6 = dot6(S6, fr);
+                    jc = (((msk >> lane) & 1u) ? v6 : 0.0f) - (((msk2 >> lane) & 1u) ? v6 : 0.0f);
+                } else {
+                    const int kdof = (int)(-lk - 1.0f);
+                    jc = lane == kdof ? sm[t.s_lsg + kdof - nr] : 0.0f;
+                }
+                jc *= kin;
+                const float jv = psum(jc * u);
+                const float l0 = lamv[rs];
+                float ln = l0 + (br - jv) * (1.0f / ar);
+                const bool fric = kind == 1 || kind == 2;
+                const float lim = mu * lamn;
+                ln = fmaxf(ln, fric ? -lim : 0.0f);
+                ln = fric ? fminf(ln, lim) : ln;
+                if (live_row) {
+                    lamn = kind == 0 ? ln : lamn;
+                    const float w = pair_wrow(t, sm, gW, rs, nv)[kc] * kin;
+                    u += w * (ln - l0);
+                }
+                wave_sync();
+                if (live_row && lane == 0) lamv[rs] = ln;
+                wave_sync();
+            }
+        }
+        if (lane < nv) us[lane] = u;
+        for (int r = lane; r < nrows; r += 32) sm[t.s_ad + r] = lamv[r];
+    }
+    wave_sync();
+    // ---- P11a: force sensors (lane s)
+    if (lane < m.S) {
+        const int si = lane, l = (int)mc.sf(MS_LINK, si);
+        float R[9], xs[3], F[3] = {0, 0, 0}, T[3] = {0, 0, 0};
+#pragma unroll
+        for (int q = 0; q < 9; ++q) R[q] = sm[t.s_R + 9 * l + q];
+        const float sp[3] = {mc.sf(MS_X, si), mc.sf(MS_X + 1, si), mc.sf(MS_X + 2, si)};
+        m3_vec(R, sp, xs);
+#pragma unroll
+        for (int q = 0; q < 3; ++q) xs[q] += sm[t.s_o + 3 * l + q];
+        for (int c = 0; c < ncon; ++c) {
+#pragma clang fp contract(off)
+            const float sgn = (int)sm[t.s_cl + c] == l ? 1.0f :
+                              ((TP::kSelf && (int)sm[t.s_cl2 + c] == l) ? -1.0f : 0.0f);
+            if (sgn == 0.0f) continue;
+            const float* lamp = sm + t.s_ad;
+            const float fn = lamp[3 * c] / dt, f1 = lamp[3 * c + 1] / dt, f2 = lamp[3 * c + 2] / dt;
+            float d[9];
+            contact_dirs<TP::kSelf>(sm, t, c, d);
+            float fc[3];
+#pragma unroll
+            for (int q = 0; q < 3; ++q) fc[q] = sgn * (fn * d[q] + f1 * d[3 + q] + f2 * d[6 + q]);
+            float rr[3], tc[3];
+#pragma unroll
+            for (int q = 0; q < 3; ++q) rr[q] = sm[t.s_cp + 3 * c + q] - xs[q];
+            cross3(rr, fc, tc);
+#pragma unroll
+            for (int q = 0; q < 3; ++q) { F[q] += fc[q]; T[q] += tc[q]; }
+        }
+        float Fl[3], Tl[3];
+        m3_tvec(R, F, Fl);
+        m3_tvec(R, T, Tl);
+#pragma unroll
+        for (int q = 0; q < 3; ++q) {
+            sm[t.s_rb + 6 * si + q] = Fl[q];
+            sm[t.s_rb + 6 * si + 3 + q] = Tl[q];
+        }
+    }
+    // ---- P11b: integrate; non-finite -> nan flag
+    bool finite = true;
+    if (lane < D) {
+        const float v = us[nr + lane];
+        const float qn = sm[t.s_q + lane] + dt * v;
+        if (store_state) {
+            st.qd[sx(st, lane, i)] = v;
+            st.q[sx(st, lane, i)] = qn;
+        }
+        sm[t.s_q + lane] = qn;
+        finite = isfinite(v) && isfinite(qn);
+    }
+    if (store_state && lane < 6 * m.S) st.sens[ssx(st, lane, i)] = sm[t.s_rb + lane];
+    if (nr && lane == 0) {
+        float u6[6], rp[3], rq[4];
+#pragma unroll
+        for (int k = 0; k < 6; ++k) u6[k] = us[k];
+#pragma unroll
+        for (int k = 0; k < 3; ++k) rp[k] = sm[t.s_rp + k];
+#pragma unroll
+        for (int k = 0; k < 4; ++k) rq[k] = sm[t.s_rp + 4 + k];
+        float* om = u6 + 3;
+        float wn = sqrtf(dot3(om, om));
+        if (wn > p.max_angvel) {
+            const float sc = p.max_angvel / wn;
+            om[0] *= sc; om[1] *= sc; om[2] *= sc;
+            wn = p.max_angvel;
+        }
+#pragma unroll
+        for (int k = 0; k < 3; ++k) rp[k] += dt * u6[k];
+        const float th = wn * dt;
+        if (th > 0.0f) {
+            float sh, ch;
+            sincosf(0.5f * th, &sh, &ch);
+            sh = sh / wn;
+            const float w0 = ch, x0 = om[0] * sh, y0 = om[1] * sh, z0 = om[2] * sh;
+            const float w1 = rq[0], x1 = rq[1], y1 = rq[2], z1 = rq[3];
+            float nq[4] = {w0 * w1 - x0 * x1 - y0 * y1 - z0 * z1,
+                           w0 * x1 + x0 * w1 + y0 * z1 - z0 * y1,
+                           w0 * y1 - x0 * z1 + y0 * w1 + z0 * x1,
+                           w0 * z1 + x0 * y1 - y0 * x1 + z0 * w1};
+            const float nn = 1.0f / sqrtf(nq[0] * nq[0] + nq[1] * nq[1] + nq[2] * nq[2] + nq[3] * nq[3]);
+#pragma unroll
+            for (int k = 0; k < 4; ++k) rq[k] = nq[k] * nn;
+        }
+#pragma unroll
+        for (int k = 0; k < 3; ++k) sm[t.s_rp + k] = rp[k];
+#pragma unroll
+        for (int k = 0; k < 4; ++k) sm[t.s_rp + 4 + k] = rq[k];
+#pragma unroll
+        for (int k = 0; k < 6; ++k) us[k] = u6[k];
+#pragma unroll
+        for (int k = 0; k < 3; ++k) finite &= isfinite(rp[k]);
+#pragma unroll
+        for (int k = 0; k < 4; ++k) finite &= isfinite(rq[k]);
+#pragma unroll
+        for (int k = 0; k < 6; ++k) finite &= isfinite(u6[k]);
+    }
+    if (nr && store_state) {
+        if (lane < 3) st.root_pos[sx(st, lane, i)] = sm[t.s_rp + lane];
+        else if (lane < 7) st.root_quat[sx(st, lane - 3, i)] = sm[t.s_rp + 4 + lane - 3];
+        else if (lane < 13) st.root_vel[sx(st, lane - 7, i)] = us[lane - 7];
+    }
+    if (hballot(!finite) != 0u && lane == 0) st.nan_flag[i] = 1;
+    wave_sync();
+}
+
+// Task layer of the paired kernel: wave_task_pre / wave_loco_post of mi_wave.hpp with the env
+// of this lane's half (lane = lane & 31; the half's lane 0 does the sequential parts).
+MI_D float pair_task_pre(const DevModel& m, const DevState& st, const DevTask& tp, int i,
+                         const float* actions, int64_t* reset_buf, int64_t* progress_buf,
+                         float* potentials, float* prev_potentials, float* actions_out) {
+#pragma clang fp contract(off)
+    const int lane = pair_l64() & 31, N = st.N, D = m.D, A = tp.A;
+    const bool flagged = reset_buf[i] != 0;      // half-uniform
+    mi_dr_env dre{};
+    if (tp.dr_act) dre = dr_begin(st, tp, 1, i, flagged);
+    if (flagged) {
+        const uint64_t gid = (uint64_t)(st.off + i);
+        const uint32_t cnt = st.reset_count[i];
+        const float pn = tp.dof_pos_noise, vn = tp.dof_vel_noise;
+        const float pw = (float)((double)pn - (double)(-pn));
+        const float vw = (float)((double)vn - (double)(-vn));
+        if (lane < D) {
+            const int j = lane;
+            float u[4];
+            uniform4(st.seed, gid, cnt, (uint32_t)(j >> 2), 0, u);
+            float v = tp.init_dof[j] + (pw * u[j & 3] + (-pn));
+            const float lo = m.lower[j + 1], hi = m.upper[j + 1];
+            if (lo < hi) { v = v < hi ? v : hi; v = v > lo ? v : lo; }
+            st.q[sx(st, j, i)] = v;
+            const int s = D + j;
+            uniform4(st.seed, gid, cnt, (uint32_t)(s >> 2), 0, u);
+            st.qd[sx(st, j, i)] = vw * u[s & 3] + (-vn);
+        }
+        if (lane < 3) st.root_pos[sx(st, lane, i)] = st.origins[(size_t)lane * N + i] + tp.init_root_pos[lane];
+        if (lane < 4) st.root_quat[sx(st, lane, i)] = tp.init_root_quat[lane];
+        if (lane < 6) st.root_vel[sx(st, lane, i)] = 0.0f;
+        if (lane == 0) {
+            float rp[3];
+#pragma unroll
+            for (int k = 0; k < 3; ++k) rp[k] = st.origins[(size_t)k * N + i] + tp.init_root_pos[k];
+            float tx = tp.target[0] - rp[0], ty = tp.target[1] - rp[1];
+            float pot = -sqrtf(tx * tx + ty * ty + 0.0f * 0.0f) / tp.task_dt;
+            prev_potentials[i] = pot;
+            potentials[i] = pot;
+            st.reset_count[i] = cnt + 1;
+            reset_buf[i] = 0;
+            progress_buf[i] = 0;
+        }
+    }
+    float a = 0.0f;
+    if (lane < A) {
+        const int j = lane;
+        a = clampf(actions[(size_t)A * i + j], -tp.clip_actions, tp.clip_actions);
+        if (tp.dr_act) a = dr_col(st, tp, 1, dre, i, j, a);
+        if (actions_out) actions_out[(size_t)A * i + j] = a;
+        st.eff[sx(st, j, i)] = a * tp.gears[j] * tp.power_scale;
+    }
+    if (tp.dr_act && lane == 0) dr_store(st, 1, i, dre);
+    return a;
+}
+
+MI_D void pair_loco_post(const DevModel& m, const WaveTabs& t, const DevState& st,
+                         const DevTask& tp, int i, float* sm, float a_lane,
+                         float* obs_out, float* obs_task, float* rew, int64_t* reset_buf,
+                         int64_t* progress_buf, float* potentials, float* prev_potentials,
+                         float* rew_out, int64_t* reset_out) {
+#pragma clang fp contract(off)
+    const int lane = pair_l64() & 31, D = m.D, S = m.S, O = tp.O;
+    const int h0 = pair_l64() & 32;
+    const float co = tp.clip_obs;
+    const float* us = sm + t.s_us;
+    float* out = obs_out + (size_t)O * i;
+    float* raw = obs_task ? obs_task + (size_t)O * i : nullptr;
+    int64_t progress = 0, flagged = 0;
+    int nan_env = 0;
+    if (lane == 0) {
+        progress = progress_buf[i] + 1;
+        flagged = reset_buf[i];
+        nan_env = st.nan_flag[i];
+    }
+    progress = __shfl(progress, h0);
+    flagged = __shfl(flagged, h0);
+    nan_env = __shfl(nan_env, h0);
+    const int64_t done = nan_env ? 1 : loco_done(tp, sm[t.s_rp + 2], flagged, progress);
+    mi_dr_env dre{};
+    if (tp.dr_obs) dre = dr_begin(st, tp, 0, i, done != 0);
+    auto put = [&](int k, float v) {
+        if (tp.dr_obs) v = dr_col(st, tp, 0, dre, i, k, v);
+        if (raw) raw[k] = v;
+        out[k] = clampf(v, -co, co);
+    };
+    float* terms = sm + t.s_rb + 6 * S;
+    if (lane < D) {
+        const int j = lane;
+        const float pos = ref_unscale(sm[t.s_q + j], m.lower[j + 1], m.upper[j + 1]);
+        const float vel = us[m.nr + j] * tp.dof_vel_scale;
+        const float a = a_lane;
+        put(12 + j, pos);
+        put(12 + D + j, vel);
+        put(12 + 2 * D + 6 * S + j, a);
+        terms[j] = a * a;
+        terms[D + j] = fabsf(a * vel) * tp.ratio[j];
+        if (tp.kind == MI_TASK_HUMANOID) {
+            const float aa = fabsf(pos);
+            const float sc = tp.joints_at_limit_cost * (aa - 0.98f) / 0.02f;
+            terms[2 * D + j] = (aa > 0.98f ? 1.0f : 0.0f) * sc * tp.ratio[j];
+        } else {
+            terms[2 * D + j] = pos > 0.99f ? 1.0f : 0.0f;
+        }
+    }
+    for (int k = lane; k < 6 * S; k += 32) put(12 + 2 * D + k, sm[t.s_rb + k] * tp.contact_force_scale);
+    wave_sync();
+    if (lane == 0) {
+        float rp[3], rq[4], rv[6];
+#pragma unroll
+        for (int k = 0; k < 3; ++k) rp[k] = sm[t.s_rp + k];
+#pragma unroll
+        for (int k = 0; k < 4; ++k) rq[k] = sm[t.s_rp + 4 + k];
+#pragma unroll
+        for (int k = 0; k < 6; ++k) rv[k] = us[k];
+        float tt[3] = {tp.target[0] - rp[0], tp.target[1] - rp[1], tp.target[2] - rp[2]};
+        tt[2] = 0.0f;
+        const float prev_p = potentials[i];
+        const float nrm = sqrtf(tt[0] * tt[0] + tt[1] * tt[1] + tt[2] * tt[2]);
+        const float new_p = -nrm / tp.task_dt;
+        const float inv_start[4] = {1.0f, -0.0f, -0.0f, -0.0f};
+        float tq[4];
+        ref_quat_mul(rq, inv_start, tq);
+        const float b0[3] = {1.0f, 0.0f, 0.0f}, b1[3] = {0.0f, 0.0f, 1.0f};
+        float up[3], hd[3];
+        ref_quat_rotate<false>(tq, b1, up);
+        ref_quat_rotate<false>(tq, b0, hd);
+        float tn = sqrtf(tt[0] * tt[0] + tt[1] * tt[1] + tt[2] * tt[2]);
+        tn = tn > 1e-9f ? tn : 1e-9f;
+        const float td[3] = {tt[0] / tn, tt[1] / tn, tt[2] / tn};
+        const float heading_proj = hd[0] * td[0] + hd[1] * td[1] + hd[2] * td[2];
+        float vl[3], al[3];
+        ref_quat_rotate<true>(tq, rv, vl);
+        ref_quat_rotate<true>(tq, rv + 3, al);
+        float roll, pitch, yaw;
+        ref_get_euler_xyz(tq, roll, pitch, yaw);
+        const float walk = atan2f(tp.target[2] - rp[2], tp.target[0] - rp[0]);
+        const float angle_to_target = walk - yaw;
+        const float o10 = up[2], o11 = heading_proj;
+        put(0, rp[2]);
+        put(1, vl[0]); put(2, vl[1]); put(3, vl[2]);
+        put(4, al[0] * tp.angular_velocity_scale);
+        put(5, al[1] * tp.angular_velocity_scale);
+        put(6, al[2] * tp.angular_velocity_scale);
+        put(7, ref_normalize_angle(yaw));
+        put(8, ref_normalize_angle(roll));
+        put(9, ref_normalize_angle(angle_to_target));
+        put(10, o10);
+        put(11, o11);
+        potentials[i] = new_p;
+        prev_potentials[i] = prev_p;
+        float limit_cost = 0.0f, act_cost = 0.0f, elec = 0.0f;
+        if (tp.kind == MI_TASK_HUMANOID) {
+            for (int j = 0; j < D; ++j) limit_cost += terms[2 * D + j];
+        } else {
+            int64_t cnt = 0;
+            for (int j = 0; j < D; ++j) cnt += terms[2 * D + j] != 0.0f;
+            limit_cost = (float)cnt;
+        }
+        const float heading = o11 > 0.8f ? tp.heading_weight : tp.heading_weight * o11 / 0.8f;
+        const float upr = o10 > 0.93f ? 0.0f + tp.up_weight : 0.0f;
+        for (int j = 0; j < D; ++j) act_cost += terms[j];
+        for (int j = 0; j < D; ++j) elec += terms[D + j];
+        float total = (new_p - prev_p) + tp.alive_reward_scale + upr + heading -
+                      tp.actions_cost * act_cost - tp.energy_cost * elec - limit_cost;
+        if (rp[2] < tp.termination_height) total = tp.death_cost;
+        rew[i] = total;
+        if (nan_env) {
+            st.nan_flag[i] = 0;
+            atomicAdd(st.nan_total, 1ull);
+        }
+        if (tp.dr_obs) dr_store(st, 0, i, dre);
+        reset_buf[i] = done;
+        progress_buf[i] = progress;
+        if (rew_out) rew_out[i] = total;
+        if (reset_out) reset_out[i] = done;
+    }
+}
+
+}  // namespace mi

@@ -19,6 +19,7 @@
 #include "mi_device.hpp"
 #include "mi_task.hpp"
 #include "mi_wave.hpp"
+#include "mi_pair.hpp"
 
 using namespace mi;
 
@@ -64,6 +65,7 @@ struct mi_sim {
     DevTask tp{};
     bool task_ok = false;
     bool wave = false;      // wavefront-per-env articulation path (mi_wave.hpp)
+    bool pair = false;      // two envs per wavefront (mi_pair.hpp), 16 envs per workgroup
     int topo = 0;           // generated compile-time topology id (0: runtime tables)
     WaveTabs wt{};
     float* rows = nullptr;  // per-env global constraint-row slab of the wave path
@@ -418,7 +420,7 @@ static void with_topo(int id, F&& f) {
     }
 }
 
-static inline dim3 wave_block(const mi_sim* s) { return dim3(64 * s->wt.envs_per_wg); }
+static inline dim3 wave_block(const mi_sim* s) { return dim3((s->pair ? 32 : 64) * s->wt.envs_per_wg); }
 static inline dim3 wave_grid(const mi_sim* s) {
     return dim3((s->N + s->wt.envs_per_wg - 1) / s->wt.envs_per_wg);
 }
@@ -733,6 +735,69 @@ __global__ __launch_bounds__(256) MI_WAVE_OCC void k_env_step_wave(const KParams
     wave_loco_post(m, t, st, tp, i, sm, a_lane, obs_out, obs_task, rew, reset_buf, progress_buf,
                    pot, prev, rew_out, reset_out);
     STAMP(14);
+}
+
+// ---- paired kernels (mi_pair.hpp): 8 waves x 2 envs = 16 envs per workgroup, 2 waves / SIMD
+// env of this lane's half: workgroup slot (threadIdx.x >> 5) = 2 wave + half
+__device__ __forceinline__ int pair_env() { return (int)(xcd_block() * (blockDim.x >> 5) + (threadIdx.x >> 5)); }
+__device__ __forceinline__ float* pair_env_lds(const WaveTabs& t, float* smem) {
+    return smem + (threadIdx.x >> 5) * t.env_stride;
+}
+// the first env of this lane's wave (N is even: both halves of a wave are live together)
+__device__ __forceinline__ bool pair_live(int N) {
+    return (int)(xcd_block() * (blockDim.x >> 5) + ((threadIdx.x >> 6) << 1)) < N;
+}
+#define MI_PAIR_OCC __attribute__((amdgpu_waves_per_eu(2, 2)))
+
+template <class T>
+__global__ __launch_bounds__(512) MI_PAIR_OCC void k_sim_step_pair(const KParams* __restrict__ kp, int substeps) {
+    extern __shared__ __attribute__((aligned(16))) float smem[];
+    const WaveTabs& t = kp->t;
+    const int i = pair_env();
+    stage_model_constants(t, smem);
+    if (!pair_live(kp->st.N)) return;
+    float* gW = kp->rows + (size_t)i * t.g_row_stride;
+    float* sm = pair_env_lds(t, smem);
+    for (int s = 0; s < substeps; ++s) {
+        const KParams* k = opaque_kp(kp);
+        pair_artic_substep<T>(k->m, k->t, k->st, k->p, i, smem, sm, gW, s == 0, s == substeps - 1);
+    }
+}
+
+template <class T>
+__global__ __launch_bounds__(512) MI_PAIR_OCC void k_env_step_pair(const KParams* __restrict__ kp,
+                                                    const float* actions, int substeps,
+                                                    float* obs_out, float* obs_task, float* rew,
+                                                    int64_t* reset_buf, int64_t* progress_buf,
+                                                    float* pot, float* prev, float* actions_out,
+                                                    float* rew_out, int64_t* reset_out) {
+    extern __shared__ __attribute__((aligned(16))) float smem[];
+    const DevModel& m = kp->m;
+    const WaveTabs& t = kp->t;
+    const DevState& st = kp->st;
+    const DevTask& tp = kp->tp;
+    const int i = pair_env();
+    const bool live = pair_live(st.N);
+    float a_lane = 0.0f;
+    if (live)
+        a_lane = pair_task_pre(m, st, tp, i, actions, reset_buf, progress_buf, pot, prev, actions_out);
+    stage_model_constants(t, smem);
+    if (!live) return;
+    float* gW = kp->rows + (size_t)i * t.g_row_stride;
+    float* sm = pair_env_lds(t, smem);
+    for (int s = 0; s < substeps; ++s) {
+        const KParams* k = opaque_kp(kp);
+        pair_artic_substep<T>(k->m, k->t, k->st, k->p, i, smem, sm, gW, s == 0, s == substeps - 1);
+    }
+    pair_loco_post(m, t, st, tp, i, sm, a_lane, obs_out, obs_task, rew, reset_buf, progress_buf,
+                   pot, prev, rew_out, reset_out);
+}
+
+// launch a paired kernel for the topologies that have one (compiled, nv <= 32)
+template <class T>
+constexpr bool has_pair() {
+    if constexpr (T::kCT) return T::nv <= 32;
+    else return false;
 }
 
 // Randomizer.apply_{observations,actions}_randomization (randomize.py:212-260), modular path
@@ -1168,16 +1233,25 @@ int mi_sim_create(const mi_model_desc* md, const mi_sim_params* prm, int32_t N, 
         // in one round). E envs per workgroup share one copy of the constant block; each env's
         // region [s_R, s_total) gets the floats that leave envs_cu envs inside the CU's 160 KB.
         int waves = 2, lam_rows = 0;
-        with_topo(s->topo, [&](auto T) { waves = decltype(T)::kWaves; lam_rows = decltype(T)::kLamRows; });
-        const int envs_cu = 4 * std::max(1, waves);
-        t.envs_per_wg = ct && waves >= 4 ? 4 : 1;
-        if (const char* e = getenv("MI_WAVE_ENVS")) t.envs_per_wg = std::max(1, std::min(4, atoi(e)));
+        bool pair_ok = false;
+        with_topo(s->topo, [&](auto T) {
+            waves = decltype(T)::kWaves; lam_rows = decltype(T)::kLamRows;
+            pair_ok = has_pair<decltype(T)>();
+        });
+        // paired kernels (mi_pair.hpp, two envs per wavefront, 16 per workgroup): MI_WAVE_PAIR=1
+        const char* pe = getenv("MI_WAVE_PAIR");
+        s->pair = ct && pair_ok && N % 2 == 0 && pe && atoi(pe) != 0;
+        const int envs_cu = s->pair ? 16 : 4 * std::max(1, waves);
+        t.envs_per_wg = s->pair ? 16 : (ct && waves >= 4 ? 4 : 1);
+        if (const char* e = getenv("MI_WAVE_ENVS"); e && !s->pair) t.envs_per_wg = std::max(1, std::min(4, atoi(e)));
         const int E = t.envs_per_wg;
         const int env_budget = ((163840 / (int)sizeof(float)) / std::max(1, envs_cu / E) - al4(t.mc_len)) / E;
         // CT path: J rows of the first constraint rows for the PGS; a 16-envs/CU budget keeps
-        // the rows the Delassus-space sweeps use (kLamRows), the 8-envs/CU one up to 48
-        t.j_rows_lds = ct ? std::min(waves >= 4 ? lam_rows : 48, m.max_rows) : 0;
-        t.s_J = take(ct ? t.j_rows_lds * m.nv : 4);
+        // the rows the Delassus-space sweeps use (kLamRows), the 8-envs/CU one up to 48; the
+        // paired kernels rebuild J rows instead
+        t.j_rows_lds = ct && !s->pair ? std::min(waves >= 4 ? lam_rows : 48, m.max_rows) : 0;
+        t.s_J = take(t.j_rows_lds > 0 ? t.j_rows_lds * m.nv : 4);
+        t.s_lam = take(s->pair ? R : 4);   // paired u-space fallback: lambda per row
         // CT path: W rows for the P9 -> P10 hand-over. First choice: the rest of the dead
         // span; when that holds fewer rows than a one-bank PGS can use and the LDS budget of
         // the wave path (8 envs / CU, 20 KB each) has room, a dedicated region instead, so
@@ -1193,10 +1267,10 @@ int mi_sim_create(const mi_model_desc* md, const mi_sim_params* prm, int32_t N, 
             const int lds_budget_floats = t.s_R + env_budget;   // end of this env's share
             int fit = want;   // the most W rows a dedicated region can hold within the share
             while (fit > 0 && so + al4(fit * m.nv) > lds_budget_floats) --fit;
-            if (ct && t.w_rows_lds < fit && (fit == want || !self_on)) {
+            if (ct && t.w_rows_lds < fit && (fit == want || !self_on || s->pair)) {
                 t.s_W = take(fit * m.nv);
                 t.w_rows_lds = t.w_rows_a = fit;
-            } else if (ct && self_on && t.w_rows_lds < want) {   // (w_row<kSelf> on device)
+            } else if (ct && self_on && t.w_rows_lds < want && !s->pair) {   // (w_row<kSelf> on device)
                 const int extra = std::min(want - t.w_rows_lds, (lds_budget_floats - so - 3) / m.nv);
                 if (extra > 0) {
                     t.s_W2 = take(extra * m.nv);
@@ -1213,7 +1287,7 @@ int mi_sim_create(const mi_model_desc* md, const mi_sim_params* prm, int32_t N, 
             // span (overlay) or between s_rp and s_xs
             const int offs[] = {t.s_mc, t.s_R, t.s_o, t.s_S, t.s_F, t.s_Ic, t.s_M, t.s_X,
                                 t.s_D, t.s_r, t.s_us, t.s_q, t.s_rp, t.s_xs, t.s_L, t.s_J,
-                                t.s_total};
+                                t.s_lam, t.s_total};
             for (size_t c = 1; c < sizeof(offs) / sizeof(offs[0]); ++c)
                 if (offs[c] <= offs[c - 1]) return cleanup(fail(MI_E_STATE, "wave LDS layout: region %zu overlaps", c));
             const bool rows_ok = overlay ? (t.s_cp == span0 && ro <= span1)
@@ -1230,6 +1304,9 @@ int mi_sim_create(const mi_model_desc* md, const mi_sim_params* prm, int32_t N, 
             t.s_surv = ro + al4(12 * md->num_geoms);
         }
         s->lds_bytes = (size_t)(so + (t.envs_per_wg - 1) * t.env_stride) * sizeof(float);
+        if (s->pair && ((self_on && t.s_seg < 0) || s->lds_bytes > 163840))
+            return cleanup(fail(MI_E_STATE, "paired wave layout does not fit (%zu B of LDS per workgroup)",
+                                s->lds_bytes));
     }
     s->lower.assign(md->lower, md->lower + L);
     s->upper.assign(md->upper, md->upper + L);
@@ -1296,6 +1373,15 @@ int mi_sim_create(const mi_model_desc* md, const mi_sim_params* prm, int32_t N, 
     if (s->wave && s->lds_bytes > 64 * 1024) {   // above the default dynamic-LDS limit
         hipError_t e1 = hipSuccess, e2 = hipSuccess;
         with_topo(s->topo, [&](auto T) {
+            if constexpr (has_pair<decltype(T)>()) {
+                if (s->pair) {
+                    e1 = hipFuncSetAttribute((const void*)k_env_step_pair<decltype(T)>,
+                                             hipFuncAttributeMaxDynamicSharedMemorySize, (int)s->lds_bytes);
+                    e2 = hipFuncSetAttribute((const void*)k_sim_step_pair<decltype(T)>,
+                                             hipFuncAttributeMaxDynamicSharedMemorySize, (int)s->lds_bytes);
+                    return;
+                }
+            }
             e1 = hipFuncSetAttribute((const void*)k_env_step_wave<decltype(T)>,
                                      hipFuncAttributeMaxDynamicSharedMemorySize, (int)s->lds_bytes);
             e2 = hipFuncSetAttribute((const void*)k_sim_step_wave<decltype(T)>,
@@ -1339,6 +1425,13 @@ int mi_sim_info(const mi_sim* s, int32_t* num_envs, int32_t* num_dof, int32_t* n
 static int launch_sim(mi_sim* s, int substeps, hipStream_t stream) {
     if (s->wave)
         with_topo(s->topo, [&](auto T) {
+            if constexpr (has_pair<decltype(T)>()) {
+                if (s->pair) {
+                    hipLaunchKernelGGL(k_sim_step_pair<decltype(T)>, wave_grid(s), wave_block(s), s->lds_bytes,
+                                       stream, (const KParams*)s->kp_dev, substeps);
+                    return;
+                }
+            }
             hipLaunchKernelGGL(k_sim_step_wave<decltype(T)>, wave_grid(s), wave_block(s), s->lds_bytes,
                                stream, (const KParams*)s->kp_dev, substeps);
         });
@@ -1720,6 +1813,22 @@ int mi_env_step(mi_sim* s, const float* actions, int32_t substeps, float* obs_ou
     HIP_TRY(timed_launch(s, stream, &ev0, &ev1));
     if (s->wave && s->tp.kind != MI_TASK_CARTPOLE)
         with_topo(s->topo, [&](auto T) {
+            if constexpr (has_pair<decltype(T)>()) {
+                if (s->pair) {
+                    if (ev0)
+                        hipExtLaunchKernelGGL(k_env_step_pair<decltype(T)>, wave_grid(s), wave_block(s),
+                                              (uint32_t)s->lds_bytes, STREAM(stream), ev0, ev1, 0,
+                                              (const KParams*)s->kp_dev, actions, substeps, obs_out, obs_task,
+                                              rew, reset_buf, progress_buf, potentials, prev_potentials,
+                                              actions_out, rew_out, reset_out);
+                    else
+                        hipLaunchKernelGGL(k_env_step_pair<decltype(T)>, wave_grid(s), wave_block(s), s->lds_bytes,
+                                           STREAM(stream), (const KParams*)s->kp_dev, actions, substeps,
+                                           obs_out, obs_task, rew, reset_buf, progress_buf, potentials,
+                                           prev_potentials, actions_out, rew_out, reset_out);
+                    return;
+                }
+            }
             if (ev0)
                 hipExtLaunchKernelGGL(k_env_step_wave<decltype(T)>, wave_grid(s), wave_block(s),
                                       (uint32_t)s->lds_bytes, STREAM(stream), ev0, ev1, 0,
@@ -1880,6 +1989,7 @@ int mi_sim_kernel_path(const mi_sim* s, int32_t* path, int32_t* topology, int32_
     if (topology) *topology = s->wave ? s->topo : 0;
     // per env: the workgroup's LDS (shared constants + envs_per_wg env regions) / envs_per_wg
     if (lds_bytes) *lds_bytes = s->wave ? (int32_t)(s->lds_bytes / s->wt.envs_per_wg) : 0;
+    if (path && s->pair) *path = 2;
     return MI_OK;
 }
 

@@ -136,6 +136,8 @@ struct WaveTabs {
                        // bounding spheres [G][4] at s_seg + 8G, broad-phase survivors [P];
                        // s_seg < 0: not enough room, direct path
     int ngeoms;
+    // paired-env kernels (mi_pair.hpp): lambda per constraint row of the u-space fallback sweeps
+    int s_lam;
 };
 
 // Per-model constants in the LDS block, structure-of-arrays so lane-indexed reads (lane = link,
