@@ -530,10 +530,11 @@ MI_D void pair_artic_substep(const DevModel& m, const WaveTabs& t, const DevStat
         if (lane < nrows) sm[t.s_ad + lane] = lam;           // reuse: lambda of row lane
     } else {
         // fallback (a half with more rows than the Delassus registers hold, 0.4 % of Humanoid
-        // substeps): u-space sweeps row by row, row data from LDS, W rows from LDS / the global
-        // slab, lambdas in LDS (s_lam); lane = DOF
-        float* lamv = sm + t.s_lam;
-        for (int r = lane; r < nrows; r += 32) lamv[r] = 0.0f;
+        // substeps): u-space sweeps, lane = DOF. Rows 0..63 as the wave kernel's one-bank
+        // sweeps with 32-lane banks: row r's data in lane r & 31 of bank r >> 5 (J rebuilt per row
+        // from the contact force direction and the lane's DOF subspace), W rows prefetched into
+        // registers; rows 64.. (a handful of substeps in a million) row by row from LDS and the
+        // slab, lambdas in s_lam.
         float S6[6];
 #pragma unroll
         for (int q = 0; q < 6; ++q) S6[q] = lane < nv ? Ss[6 * lane + q] : 0.0f;
@@ -541,10 +542,70 @@ MI_D void pair_artic_substep(const DevModel& m, const WaveTabs& t, const DevStat
         const int kc = lane < nv ? lane : 0;
         const float kin = lane < nv ? 1.0f : 0.0f;
         const float mu = p.friction;
+        float b0 = 0.0f, b1 = 0.0f, ia0 = 1.0f, ia1 = 1.0f, k0 = 0.0f, k1 = 0.0f, lam0 = 0.0f, lam1 = 0.0f;
+        float fa[6] = {0, 0, 0, 0, 0, 0}, fb[6] = {0, 0, 0, 0, 0, 0};
+        unsigned ma = 0u, mb = 0u, ma2 = 0u, mb2 = 0u;
+        auto load_row = [&](int r, float& b, float& ia, float& k, float (&f)[6], unsigned& msk,
+                            unsigned& msk2) {
+            b = sm[t.s_rb + r];
+            ia = 1.0f / sm[t.s_ad + r];
+            k = sm[t.s_rk + r];
+            const float lk = sm[t.s_rl + r];
+            if (lk >= 0.0f) {
+                contact_row_f<TP::kSelf>(sm, t, r, f);
+                msk = mc.mask((int)lk);
+                const float l2 = TP::kSelf ? sm[t.s_cl2 + r / 3] : -1.0f;
+                msk2 = l2 >= 0.0f ? mc.mask((int)l2) : 0u;
+            } else {
+                const int kdof = (int)(-lk - 1.0f);
+                f[0] = sm[t.s_lsg + kdof - nr];      // limit row: J = sg e_k
+                msk = 1u << kdof;
+            }
+        };
+        if (lane < nrows) load_row(lane, b0, ia0, k0, fa, ma, ma2);
+        if (lane + 32 < nrows) load_row(lane + 32, b1, ia1, k1, fb, mb, mb2);
+        float Wr[64];
+#pragma unroll
+        for (int rr = 0; rr < 64; ++rr) {   // uniform branch per row: LDS rows, then the slab
+            if (rr < t.w_rows_lds) Wr[rr] = sm[t.s_W + rr * nv + kc] * kin;
+            else Wr[rr] = gW[(size_t)rr * WNV + kc] * kin;
+        }
+        float* lamv = sm + t.s_lam;
+        for (int r = 64 + lane; r < nrows; r += 32) lamv[r] = 0.0f;
         wave_sync();
         for (int it = 0; it < p.iters; ++it) {
+            asm volatile("" : "+v"(b0), "+v"(b1), "+v"(ia0), "+v"(ia1), "+v"(k0), "+v"(k1),
+                         "+v"(ma), "+v"(mb), "+v"(ma2), "+v"(mb2));
+            int nrow_it = nrows_max;
+            asm volatile("" : "+s"(nrow_it));
             float lamn = 0.0f;
-            for (int r = 0; r < nrows_max; ++r) {
+#pragma unroll
+            for (int rr = 0; rr < 64; ++rr) {
+                if (rr >= nrow_it) continue;   // no early exit: Wr stays register-indexed
+                __builtin_amdgcn_sched_barrier(0);
+                const int bank = rr >> 5, w = rr & 31;
+                float fr[6];
+#pragma unroll
+                for (int q = 0; q < 6; ++q) fr[q] = pbc(bank ? fb[q] : fa[q], w);
+                const unsigned msk = (unsigned)pbci((int)(bank ? mb : ma), w);
+                const unsigned msk2 = (unsigned)pbci((int)(bank ? mb2 : ma2), w);
+                const int kind = (int)pbc(bank ? k1 : k0, w);
+                const float j0 = kind == 3 ? fr[0] : dot6(S6, fr);
+                const float jc = ((((msk >> lane) & 1u) ? j0 : 0.0f) - (((msk2 >> lane) & 1u) ? j0 : 0.0f)) * kin;
+                const float jv = psum(jc * u);
+                const float br = pbc(bank ? b1 : b0, w), iar = pbc(bank ? ia1 : ia0, w);
+                const float l0 = pbc(bank ? lam1 : lam0, w);
+                float ln = l0 + (br - jv) * iar;
+                const bool fric = kind == 1 || kind == 2;
+                const float lim = mu * lamn;
+                ln = fmaxf(ln, fric ? -lim : 0.0f);
+                ln = fric ? fminf(ln, lim) : ln;
+                const bool live_row = rr < nrows;
+                lamn = (live_row && kind == 0) ? ln : lamn;
+                u = live_row ? u + Wr[rr] * (ln - l0) : u;
+                if (live_row && lane_here(lane) == w) { if (bank) lam1 = ln; else lam0 = ln; }
+            }
+            for (int r = 64; r < nrow_it; ++r) {
                 const bool live_row = r < nrows;
                 const int rs = live_row ? r : 0;
                 const float br = sm[t.s_rb + rs], ar = sm[t.s_ad + rs];
@@ -565,7 +626,7 @@ MI_D void pair_artic_substep(const DevModel& m, const WaveTabs& t, const DevStat
                 }
                 jc *= kin;
                 const float jv = psum(jc * u);
-                const float l0 = lamv[rs];
+                const float l0 = live_row ? lamv[rs] : 0.0f;
                 float ln = l0 + (br - jv) * (1.0f / ar);
                 const bool fric = kind == 1 || kind == 2;
                 const float lim = mu * lamn;
@@ -573,8 +634,7 @@ MI_D void pair_artic_substep(const DevModel& m, const WaveTabs& t, const DevStat
                 ln = fric ? fminf(ln, lim) : ln;
                 if (live_row) {
                     lamn = kind == 0 ? ln : lamn;
-                    const float w = pair_wrow(t, sm, gW, rs, nv)[kc] * kin;
-                    u += w * (ln - l0);
+                    u += gW[(size_t)rs * WNV + kc] * kin * (ln - l0);
                 }
                 wave_sync();
                 if (live_row && lane == 0) lamv[rs] = ln;
@@ -582,7 +642,9 @@ MI_D void pair_artic_substep(const DevModel& m, const WaveTabs& t, const DevStat
             }
         }
         if (lane < nv) us[lane] = u;
-        for (int r = lane; r < nrows; r += 32) sm[t.s_ad + r] = lamv[r];
+        if (lane < nrows) sm[t.s_ad + lane] = lam0;          // reuse: lambda of row lane
+        if (lane + 32 < nrows) sm[t.s_ad + lane + 32] = lam1;
+        for (int r = 64 + lane; r < nrows; r += 32) sm[t.s_ad + r] = lamv[r];
     }
     wave_sync();
     // ---- P11a: force sensors (lane s)

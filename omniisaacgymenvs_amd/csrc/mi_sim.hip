@@ -1304,6 +1304,11 @@ int mi_sim_create(const mi_model_desc* md, const mi_sim_params* prm, int32_t N, 
             t.s_surv = ro + al4(12 * md->num_geoms);
         }
         s->lds_bytes = (size_t)(so + (t.envs_per_wg - 1) * t.env_stride) * sizeof(float);
+        if (getenv("MI_SIM_DEBUG"))
+            fprintf(stderr, "[mi_sim] wave layout: pair=%d envs/wg=%d lds/wg=%zu B env_stride=%d floats "
+                            "mc=%d w_rows_lds=%d (a %d) j_rows_lds=%d s_seg=%d max_rows=%d ncmax=%d\n",
+                    (int)s->pair, t.envs_per_wg, s->lds_bytes, t.env_stride, t.mc_len, t.w_rows_lds,
+                    t.w_rows_a, t.j_rows_lds, t.s_seg, m.max_rows, t.ncmax);
         if (s->pair && ((self_on && t.s_seg < 0) || s->lds_bytes > 163840))
             return cleanup(fail(MI_E_STATE, "paired wave layout does not fit (%zu B of LDS per workgroup)",
                                 s->lds_bytes));
