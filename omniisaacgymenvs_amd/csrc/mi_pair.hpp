@@ -112,6 +112,7 @@ MI_D void pair_artic_substep(const DevModel& m, const WaveTabs& t, const DevStat
     float* Ss = sm + t.s_S;
     const MC mc = make_mc(t, mcb, L);
 
+    STAMP_BEGIN();
     if (load_state) {
         if (lane < 3) sm[t.s_rp + lane] = st.root_pos[sx(st, lane, i)];
         if (lane < 4) sm[t.s_rp + 4 + lane] = st.root_quat[sx(st, lane, i)];
@@ -126,11 +127,13 @@ MI_D void pair_artic_substep(const DevModel& m, const WaveTabs& t, const DevStat
         for (int c = 0; c < 6; ++c) Ss[6 * lane + c] = s[c];
     }
     wave_sync();
+    STAMP(0);
     // ---- P1: local transforms, then chain walks + link inertia / Newton-Euler (lane = link)
     for (int l = 1 + lane; l < L; l += 32) wave_link_local(mc, t, sm, l);
     wave_sync();
     for (int l = lane; l < L; l += 32) wave_link_forward(mc, nr, t, sm, l, p);
     wave_sync();
+    STAMP(1);
     // ---- P2: composite inertia / force
     float* aux = sm + t.s_X;
     {
@@ -150,6 +153,7 @@ MI_D void pair_artic_substep(const DevModel& m, const WaveTabs& t, const DevStat
         }
     }
     wave_sync();
+    STAMP(2);
     // ---- P3: bias + CRBA rows (lane = DOF)
     if (lane < nv) {
         const int k = lane, l = k < nr ? 0 : k - nr + 1;
@@ -183,6 +187,7 @@ MI_D void pair_artic_substep(const DevModel& m, const WaveTabs& t, const DevStat
         Mx[k * nv + k] = diag;
     }
     wave_sync();
+    STAMP(3);
     // ---- P4: register LTDL (lane = column), factor published to LDS
     float Mc[TP::nvc];
     ct_load_columns<TP>(Mx, lane, Mc);
@@ -192,6 +197,7 @@ MI_D void pair_artic_substep(const DevModel& m, const WaveTabs& t, const DevStat
         const int dj = lane < nr ? lane : __builtin_popcount(mc.mask(lane < nv ? lane - nr + 1 : 0)) - 1;
         ct_publish_factor<TP>(lane, dj, Mc, dvec, sm + t.s_L);
     }
+    STAMP(4);
     // ---- P8: ground contacts (lanes over candidate points, two passes past 32), ballot
     // compaction per half in candidate order
     int ncon = 0;
@@ -337,6 +343,7 @@ MI_D void pair_artic_substep(const DevModel& m, const WaveTabs& t, const DevStat
     }
     const int nc = 3 * ncon;
     wave_sync();
+    STAMP(6);
     // ---- P7+P9: one batch per half, lanes over solve vectors (rhs, limit candidates, contact
     // rows); passes of 32 to the larger half's count
     const int nlim = t.nlimc;
@@ -437,25 +444,37 @@ MI_D void pair_artic_substep(const DevModel& m, const WaveTabs& t, const DevStat
             asm volatile("" : "+v"(xc), "+v"(rc));
             x[c] = crow ? xc : (bv == 0 ? rc : (kd == c ? 1.0f : 0.0f));
         });
+        STAMP(7);
         float a;
         ct_solve_l<TP>(sm + t.s_L, x, a);
+        STAMP(8);
         if (base == 0) limit_rows(x);
+        STAMP(9);
         file_row(x, on, r, kd, a);
+        STAMP(10);
     }
     wave_sync();
+    STAT(15, pmax(nrows));
+    STAT(16, total_max > 32);
+    STAT(17, pmax(nrows) > 64);
+    STAT(18, total_max > 64);
+    STAT(19, pmax(nrows) > TP::kLamRows);
+    STAT(20, pmax(ncon));
+    STAT(21, pmax(nrows) > 16);
+    STAT(22, pmax(nrows) > 24);
+    STAT(23, pmax(nrows) > 20);
+    STAT(26, t.w_rows_lds);
     // ---- P10: projected Gauss-Seidel, 4 sweeps
     const int nrows_max = pmax(nrows);
+    const float mu = p.friction;
     if (nrows_max <= TP::kLamRows) {
         // Delassus space: lane r holds row r's v_r = J_r . u and A[r][s] = J_r . W_s (J_r rebuilt
-        // here from the contact data: no J rows in LDS; W rows past the LDS ones from the slab)
+        // here from the contact data: no J rows in LDS; W rows past the LDS ones from the slab).
+        // Every lane keeps every row's lambda in registers (it computes each row's update anyway),
+        // and reads the row's bias / A_rr / kind from LDS ahead of the chain, so a row costs one
+        // cross-lane broadcast (v_r) instead of five.
         constexpr int NV = TP::nv;
         constexpr int RMAX = TP::kLamRows;
-        float b = 0.0f, ia = 1.0f, kd = 0.0f, lam = 0.0f;
-        if (lane < nrows) {
-            b = sm[t.s_rb + lane];
-            ia = 1.0f / sm[t.s_ad + lane];
-            kd = sm[t.s_rk + lane];
-        }
         const int rl = lane < nrows ? lane : 0;
         float Jr[TP::nvc];
         if (nrows > 0) pair_jrow<TP>(mc, t, sm, rl, nr, Jr);
@@ -486,7 +505,19 @@ MI_D void pair_artic_substep(const DevModel& m, const WaveTabs& t, const DevStat
             }
             Ar[g0] = a0; Ar[g0 + 1] = a1; Ar[g0 + 2] = a2; Ar[g0 + 3] = a3;
         }
-        const float mu = p.friction;
+        // lane r's own row: bias, 1 / A_rr, kind (contact rows are (normal, friction, friction)
+        // triples 3c..3c+2, then the limit rows)
+        float b = 0.0f, ia = 1.0f;
+        int kd = 0;
+        if (lane < nrows) {
+            b = sm[t.s_rb + lane];
+            ia = 1.0f / sm[t.s_ad + lane];
+            kd = (int)sm[t.s_rk + lane];
+        }
+        const int nnorm = 3 * ncon;   // rows below this with r % 3 == 0 are normal rows
+        float lamv[RMAX];
+#pragma unroll
+        for (int rr = 0; rr < RMAX; ++rr) lamv[rr] = 0.0f;
         for (int it = 0; it < p.iters; ++it) {
             asm volatile("" : "+v"(b), "+v"(ia), "+v"(kd));
             int nrow_it = nrows_max;
@@ -496,19 +527,19 @@ MI_D void pair_artic_substep(const DevModel& m, const WaveTabs& t, const DevStat
             for (int rr = 0; rr < RMAX; ++rr) {
                 if (rr >= nrow_it) break;
                 __builtin_amdgcn_sched_barrier(0);
-                const float vr = pbc(v, rr);
-                const float br = pbc(b, rr), iar = pbc(ia, rr);
-                const float l0 = pbc(lam, rr);
-                const int kind = (int)pbc(kd, rr);
-                float ln = l0 + (br - vr) * iar;
-                const bool fric = kind == 1 || kind == 2;
+                // the row's owner (lane rr of each half) holds v_rr, b, 1 / A_rr and its kind:
+                // it alone projects, and one broadcast hands the new lambda to its half
+                const float l0 = lamv[rr];
+                float mine = l0 + (b - v) * ia;
+                const bool fric = kd == 1 || kd == 2;
                 const float lim = mu * lamn;
-                ln = fmaxf(ln, fric ? -lim : 0.0f);
-                ln = fric ? fminf(ln, lim) : ln;
+                mine = fmaxf(mine, fric ? -lim : 0.0f);
+                mine = fric ? fminf(mine, lim) : mine;
                 const bool live_row = rr < nrows;
-                lamn = (live_row && kind == 0) ? ln : lamn;
-                v = live_row ? v + Ar[rr] * (ln - l0) : v;
-                if (live_row && lane_here(lane) == rr) lam = ln;
+                const float ln = live_row ? pbc(mine, rr) : l0;
+                if (rr % 3 == 0) lamn = rr < nnorm ? ln : lamn;
+                v += Ar[rr] * (ln - l0);
+                lamv[rr] = ln;
             }
         }
         float u = lane < NV ? us[lane] : 0.0f;
@@ -516,32 +547,32 @@ MI_D void pair_artic_substep(const DevModel& m, const WaveTabs& t, const DevStat
 #pragma unroll
         for (int g0 = 0; g0 < RMAX; g0 += 4) {
             if (g0 >= nrows_max) break;
-            float wq[4], lq[4];
+            float wq[4];
 #pragma unroll
-            for (int q = 0; q < 4; ++q) {
+            for (int q = 0; q < 4; ++q)
                 wq[q] = g0 + 3 < t.w_rows_lds ? sm[t.s_W + min(g0 + q, last) * NV + kc]
                                               : pair_wrow(t, sm, gW, min(g0 + q, last), NV)[kc];
-                lq[q] = pbc(lam, g0 + q);
-            }
 #pragma unroll
-            for (int q = 0; q < 4; ++q) u = g0 + q < nrows ? u + wq[q] * lq[q] : u;
+            for (int q = 0; q < 4; ++q) u = g0 + q < nrows ? u + wq[q] * lamv[g0 + q] : u;
         }
         if (lane < NV) us[lane] = u;
-        if (lane < nrows) sm[t.s_ad + lane] = lam;           // reuse: lambda of row lane
+        wave_sync();
+#pragma unroll
+        for (int rr = 0; rr < RMAX; ++rr)            // reuse: lambda of row rr
+            if (lane == rr && rr < nrows) sm[t.s_ad + rr] = lamv[rr];
     } else {
         // fallback (a half with more rows than the Delassus registers hold, 0.4 % of Humanoid
         // substeps): u-space sweeps, lane = DOF. Rows 0..63 as the wave kernel's one-bank
         // sweeps with 32-lane banks: row r's data in lane r & 31 of bank r >> 5 (J rebuilt per row
         // from the contact force direction and the lane's DOF subspace), W rows prefetched into
         // registers; rows 64.. (a handful of substeps in a million) row by row from LDS and the
-        // slab, lambdas in s_lam.
+        // slab, their lambdas in the slab's spare column.
         float S6[6];
 #pragma unroll
         for (int q = 0; q < 6; ++q) S6[q] = lane < nv ? Ss[6 * lane + q] : 0.0f;
         float u = lane < nv ? us[lane] : 0.0f;
         const int kc = lane < nv ? lane : 0;
         const float kin = lane < nv ? 1.0f : 0.0f;
-        const float mu = p.friction;
         float b0 = 0.0f, b1 = 0.0f, ia0 = 1.0f, ia1 = 1.0f, k0 = 0.0f, k1 = 0.0f, lam0 = 0.0f, lam1 = 0.0f;
         float fa[6] = {0, 0, 0, 0, 0, 0}, fb[6] = {0, 0, 0, 0, 0, 0};
         unsigned ma = 0u, mb = 0u, ma2 = 0u, mb2 = 0u;
@@ -570,9 +601,9 @@ MI_D void pair_artic_substep(const DevModel& m, const WaveTabs& t, const DevStat
             if (rr < t.w_rows_lds) Wr[rr] = sm[t.s_W + rr * nv + kc] * kin;
             else Wr[rr] = gW[(size_t)rr * WNV + kc] * kin;
         }
-        float* lamv = sm + t.s_lam;
-        for (int r = 64 + lane; r < nrows; r += 32) lamv[r] = 0.0f;
-        wave_sync();
+        for (int r = 64 + lane; r < nrows; r += 32) gW[(size_t)r * WNV + (WNV - 1)] = 0.0f;
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
         for (int it = 0; it < p.iters; ++it) {
             asm volatile("" : "+v"(b0), "+v"(b1), "+v"(ia0), "+v"(ia1), "+v"(k0), "+v"(k1),
                          "+v"(ma), "+v"(mb), "+v"(ma2), "+v"(mb2));
@@ -626,7 +657,8 @@ MI_D void pair_artic_substep(const DevModel& m, const WaveTabs& t, const DevStat
                 }
                 jc *= kin;
                 const float jv = psum(jc * u);
-                const float l0 = live_row ? lamv[rs] : 0.0f;
+                float* lp = gW + (size_t)rs * WNV + (WNV - 1);
+                const float l0 = live_row ? *lp : 0.0f;
                 float ln = l0 + (br - jv) * (1.0f / ar);
                 const bool fric = kind == 1 || kind == 2;
                 const float lim = mu * lamn;
@@ -636,17 +668,18 @@ MI_D void pair_artic_substep(const DevModel& m, const WaveTabs& t, const DevStat
                     lamn = kind == 0 ? ln : lamn;
                     u += gW[(size_t)rs * WNV + kc] * kin * (ln - l0);
                 }
-                wave_sync();
-                if (live_row && lane == 0) lamv[rs] = ln;
-                wave_sync();
+                __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+                if (live_row && lane == 0) *lp = ln;
+                __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
             }
         }
         if (lane < nv) us[lane] = u;
         if (lane < nrows) sm[t.s_ad + lane] = lam0;          // reuse: lambda of row lane
         if (lane + 32 < nrows) sm[t.s_ad + lane + 32] = lam1;
-        for (int r = 64 + lane; r < nrows; r += 32) sm[t.s_ad + r] = lamv[r];
+        for (int r = 64 + lane; r < nrows; r += 32) sm[t.s_ad + r] = gW[(size_t)r * WNV + (WNV - 1)];
     }
     wave_sync();
+    STAMP(11);
     // ---- P11a: force sensors (lane s)
     if (lane < m.S) {
         const int si = lane, l = (int)mc.sf(MS_LINK, si);
@@ -750,6 +783,8 @@ MI_D void pair_artic_substep(const DevModel& m, const WaveTabs& t, const DevStat
     }
     if (hballot(!finite) != 0u && lane == 0) st.nan_flag[i] = 1;
     wave_sync();
+    STAMP(12);
+    STAMP_END();
 }
 
 // Task layer of the paired kernel: wave_task_pre / wave_loco_post of mi_wave.hpp with the env

@@ -778,19 +778,23 @@ __global__ __launch_bounds__(512) MI_PAIR_OCC void k_env_step_pair(const KParams
     const DevTask& tp = kp->tp;
     const int i = pair_env();
     const bool live = pair_live(st.N);
+    STAMP_BEGIN();
     float a_lane = 0.0f;
     if (live)
         a_lane = pair_task_pre(m, st, tp, i, actions, reset_buf, progress_buf, pot, prev, actions_out);
     stage_model_constants(t, smem);
     if (!live) return;
+    STAMP(13);
     float* gW = kp->rows + (size_t)i * t.g_row_stride;
     float* sm = pair_env_lds(t, smem);
     for (int s = 0; s < substeps; ++s) {
         const KParams* k = opaque_kp(kp);
         pair_artic_substep<T>(k->m, k->t, k->st, k->p, i, smem, sm, gW, s == 0, s == substeps - 1);
     }
+    STAMP_RESET();
     pair_loco_post(m, t, st, tp, i, sm, a_lane, obs_out, obs_task, rew, reset_buf, progress_buf,
                    pot, prev, rew_out, reset_out);
+    STAMP(14);
 }
 
 // launch a paired kernel for the topologies that have one (compiled, nv <= 32)
@@ -910,6 +914,20 @@ int mi_debug_stamps(unsigned long long* out, int n) {
         out[k] = acc;
     }
     std::fill(all.begin(), all.end(), 0ull);   // read-and-reset
+    HIP_TRY(hipMemcpyToSymbol(HIP_SYMBOL(g_phase), all.data(), all.size() * sizeof(unsigned long long)));
+    return MI_OK;
+}
+#endif
+#ifdef MI_STAMPS
+// diagnostic build only: the raw per-wave phase accumulators [slots][32] (slot = wave index of
+// the launch modulo MI_STAMP_SLOTS), read-and-reset (tools/pair_tail.py)
+int mi_debug_stamps_raw(unsigned long long* out, int slots) {
+    if (!out || slots <= 0 || slots > MI_STAMP_SLOTS) return MI_E_ARG;
+    HIP_TRY(hipDeviceSynchronize());
+    std::vector<unsigned long long> all((size_t)MI_STAMP_SLOTS * 32);
+    HIP_TRY(hipMemcpyFromSymbol(all.data(), HIP_SYMBOL(g_phase), all.size() * sizeof(unsigned long long)));
+    std::copy(all.begin(), all.begin() + (size_t)slots * 32, out);
+    std::fill(all.begin(), all.end(), 0ull);
     HIP_TRY(hipMemcpyToSymbol(HIP_SYMBOL(g_phase), all.data(), all.size() * sizeof(unsigned long long)));
     return MI_OK;
 }
@@ -1194,44 +1212,11 @@ int mi_sim_create(const mi_model_desc* md, const mi_sim_params* prm, int32_t N, 
         const bool ct = s->topo != 0;
         int so = 0;
         auto take = [&](int n) { const int at = so; so += al4(n); return at; };
-        t.s_mc = take(t.mc_len);
-        t.s_R = take(9 * L); t.s_o = take(3 * L); t.s_S = take(6 * m.nv);
-        // P1..P4 working span: link inertias / forces, M, aux (local transforms, composites).
-        // On the compiled-topology path it is dead once P4 has moved M into registers, and
-        // P8/P9 reuse it for the contact and row data and the first W rows.
-        const int span0 = so;
-        t.s_F = take(16 * L);   // per-link records: inertia (10) + Newton-Euler force (6)
-        t.s_Ic = take(4);       // (kept for the layout order; records live at s_F)
-        t.s_M = take(m.nv * m.nv);
-        t.s_X = take(16 * L);
-        const int span1 = so;
-        t.s_D = take(ct ? 4 : WNV); t.s_r = take(WNV); t.s_us = take(WNV);
-        t.s_q = take(WNV); t.s_rp = take(8);
-        const int R = m.max_rows;
-        // contacts: ground points + self pairs, at most MI_MAX_ROWS / 3 in total
-        t.self_on = self_on ? 1 : 0;
-        t.npairs = self_on ? md->num_pairs : 0;
-        t.ncmax = std::min(m.npts + t.npairs, MI_MAX_ROWS / 3);
-        const int C = t.ncmax;
-        const int rows_len = 8 * al4(C) + 4 * al4(R) + WNV;
-        const bool overlay = ct && rows_len <= span1 - span0;
-        int ro = overlay ? span0 : so;
-        auto take_r = [&](int n) { const int at = ro; ro += al4(n); return at; };
-        t.s_cp = take_r(3 * C); t.s_cl = take_r(C); t.s_cl2 = take_r(C); t.s_cn = take_r(3 * C);
-        t.s_rl = take_r(R);
-        t.s_rb = take_r(R); t.s_rk = take_r(R); t.s_ad = take_r(R); t.s_lsg = take_r(WNV);
-        if (!overlay) so = ro;
-        // lane-private solve vectors of the runtime-table solves (CT solves run in registers)
-        t.s_xs = take(ct ? 4 : WNV * 64);
-        {   // CT path: published factor rows (each padded to 4) + 1/D (DofTree::lrow)
-            int lr = 0;
-            for (int k = 0; k < m.nv; ++k) lr += (anc_start[k + 1] - anc_start[k] + 3) & ~3;
-            t.s_L = take(ct ? lr + m.nv : 4);
-        }
         // Residency: the kernels' register budget allows TopoCT::kWaves waves per SIMD, i.e.
         // envs_cu = 4 kWaves resident envs per CU (Humanoid 8, Ant 16: all 4096 envs of a launch
-        // in one round). E envs per workgroup share one copy of the constant block; each env's
-        // region [s_R, s_total) gets the floats that leave envs_cu envs inside the CU's 160 KB.
+        // in one round); the paired kernels hold 16 envs per CU (two per wave, 2 waves per SIMD).
+        // E envs per workgroup share one copy of the constant block; each env's region
+        // [s_R, s_total) gets the floats that leave envs_cu envs inside the CU's 160 KB.
         int waves = 2, lam_rows = 0;
         bool pair_ok = false;
         with_topo(s->topo, [&](auto T) {
@@ -1246,12 +1231,78 @@ int mi_sim_create(const mi_model_desc* md, const mi_sim_params* prm, int32_t N, 
         if (const char* e = getenv("MI_WAVE_ENVS"); e && !s->pair) t.envs_per_wg = std::max(1, std::min(4, atoi(e)));
         const int E = t.envs_per_wg;
         const int env_budget = ((163840 / (int)sizeof(float)) / std::max(1, envs_cu / E) - al4(t.mc_len)) / E;
+        const int R = m.max_rows;
+        t.self_on = self_on ? 1 : 0;
+        t.npairs = self_on ? md->num_pairs : 0;
+        t.ncmax = std::min(m.npts + t.npairs, MI_MAX_ROWS / 3);
+        const int C = t.ncmax;
+        int lr = 0;   // CT path: published factor rows (each padded to 4) + 1/D (DofTree::lrow)
+        for (int k = 0; k < m.nv; ++k) lr += (anc_start[k + 1] - anc_start[k] + 3) & ~3;
+        bool overlay = false;
+        int span0 = 0, span1 = 0, ro = 0;
+        if (s->pair) {
+            // paired layout: the persistent regions first, then the P1-P4 span whose dead space
+            // takes the contact / row data and the W rows, which continue past the span up to
+            // the env's share (one W segment); no J rows (rebuilt), no second W segment
+            t.s_mc = take(t.mc_len);
+            t.s_R = take(9 * L); t.s_o = take(3 * L); t.s_S = take(6 * m.nv);
+            t.s_D = take(4); t.s_r = take(WNV); t.s_us = take(WNV); t.s_q = take(WNV); t.s_rp = take(8);
+            t.s_xs = take(4);
+            t.s_L = take(lr + m.nv);
+            t.j_rows_lds = 0;
+            t.s_J = take(4);
+            t.s_lam = take(4);
+            span0 = so;
+            t.s_F = take(16 * L); t.s_Ic = take(4); t.s_M = take(m.nv * m.nv); t.s_X = take(16 * L);
+            span1 = so;
+            overlay = true;
+            ro = span0;
+            auto take_r = [&](int n) { const int at = ro; ro += al4(n); return at; };
+            t.s_cp = take_r(3 * C); t.s_cl = take_r(C); t.s_cl2 = take_r(C); t.s_cn = take_r(3 * C);
+            t.s_rl = take_r(R); t.s_rb = take_r(R); t.s_rk = take_r(R); t.s_ad = take_r(R);
+            t.s_lsg = take_r(WNV);
+            t.s_W = ro;
+            int w = std::min(64, (t.s_R + env_budget - ro) / m.nv);
+            while (w > 0 && ro + al4(w * m.nv) > t.s_R + env_budget) --w;
+            t.w_rows_lds = t.w_rows_a = std::max(0, w);
+            t.s_W2 = 0;
+            so = std::max(span1, ro + al4(t.w_rows_lds * m.nv));
+        } else {
+        t.s_mc = take(t.mc_len);
+        t.s_R = take(9 * L); t.s_o = take(3 * L); t.s_S = take(6 * m.nv);
+        // P1..P4 working span: link inertias / forces, M, aux (local transforms, composites).
+        // On the compiled-topology path it is dead once P4 has moved M into registers, and
+        // P8/P9 reuse it for the contact and row data and the first W rows.
+        span0 = so;
+        t.s_F = take(16 * L);   // per-link records: inertia (10) + Newton-Euler force (6)
+        t.s_Ic = take(4);       // (kept for the layout order; records live at s_F)
+        t.s_M = take(m.nv * m.nv);
+        t.s_X = take(16 * L);
+        span1 = so;
+        t.s_D = take(ct ? 4 : WNV); t.s_r = take(WNV); t.s_us = take(WNV);
+        t.s_q = take(WNV); t.s_rp = take(8);
+        // contacts: ground points + self pairs, at most MI_MAX_ROWS / 3 in total
+        const int rows_len = 8 * al4(C) + 4 * al4(R) + WNV;
+        overlay = ct && rows_len <= span1 - span0;
+        ro = overlay ? span0 : so;
+        auto take_r = [&](int n) { const int at = ro; ro += al4(n); return at; };
+        t.s_cp = take_r(3 * C); t.s_cl = take_r(C); t.s_cl2 = take_r(C); t.s_cn = take_r(3 * C);
+        t.s_rl = take_r(R);
+        t.s_rb = take_r(R); t.s_rk = take_r(R); t.s_ad = take_r(R); t.s_lsg = take_r(WNV);
+        if (!overlay) so = ro;
+        // lane-private solve vectors of the runtime-table solves (CT solves run in registers)
+        t.s_xs = take(ct ? 4 : WNV * 64);
+        t.s_L = take(ct ? lr + m.nv : 4);
+        // Residency: the kernels' register budget allows TopoCT::kWaves waves per SIMD, i.e.
+        // envs_cu = 4 kWaves resident envs per CU (Humanoid 8, Ant 16: all 4096 envs of a launch
+        // in one round). E envs per workgroup share one copy of the constant block; each env's
+        // region [s_R, s_total) gets the floats that leave envs_cu envs inside the CU's 160 KB.
         // CT path: J rows of the first constraint rows for the PGS; a 16-envs/CU budget keeps
         // the rows the Delassus-space sweeps use (kLamRows), the 8-envs/CU one up to 48; the
         // paired kernels rebuild J rows instead
         t.j_rows_lds = ct && !s->pair ? std::min(waves >= 4 ? lam_rows : 48, m.max_rows) : 0;
         t.s_J = take(t.j_rows_lds > 0 ? t.j_rows_lds * m.nv : 4);
-        t.s_lam = take(s->pair ? R : 4);   // paired u-space fallback: lambda per row
+        t.s_lam = take(4);
         // CT path: W rows for the P9 -> P10 hand-over. First choice: the rest of the dead
         // span; when that holds fewer rows than a one-bank PGS can use and the LDS budget of
         // the wave path (8 envs / CU, 20 KB each) has room, a dedicated region instead, so
@@ -1278,12 +1329,13 @@ int mi_sim_create(const mi_model_desc* md, const mi_sim_params* prm, int32_t N, 
                 }
             }
         }
+        }
         t.s_total = so;
         // E envs per workgroup share the constant block [0, s_env); env w's region is shifted
         // by w * env_stride
         t.s_env = t.s_R;
         t.env_stride = so - t.s_env;
-        {   // the sequential regions strictly increase; the row data sits inside the dead
+        if (!s->pair) {   // the sequential regions strictly increase; the row data sits inside the dead
             // span (overlay) or between s_rp and s_xs
             const int offs[] = {t.s_mc, t.s_R, t.s_o, t.s_S, t.s_F, t.s_Ic, t.s_M, t.s_X,
                                 t.s_D, t.s_r, t.s_us, t.s_q, t.s_rp, t.s_xs, t.s_L, t.s_J,
