@@ -484,8 +484,8 @@ MI_D void pair_artic_substep(const DevModel& m, const WaveTabs& t, const DevStat
         const int last = max(nrows - 1, 0);
         float Ar[RMAX];
         static_assert(RMAX % 4 == 0, "Delassus rows are built four at a time");
-#pragma unroll
-        for (int g0 = 0; g0 < RMAX; g0 += 4) {
+        sfor<0, RMAX / 4>([&](auto G) {
+            constexpr int g0 = 4 * G;
             float a0 = 0.0f, a1 = 0.0f, a2 = 0.0f, a3 = 0.0f;
             if (g0 < nrows_max) {
                 auto dots = [&](const float* w0, const float* w1, const float* w2, const float* w3) {
@@ -504,7 +504,7 @@ MI_D void pair_artic_substep(const DevModel& m, const WaveTabs& t, const DevStat
                          pair_wrow(t, sm, gW, min(g0 + 2, last), NV), pair_wrow(t, sm, gW, min(g0 + 3, last), NV));
             }
             Ar[g0] = a0; Ar[g0 + 1] = a1; Ar[g0 + 2] = a2; Ar[g0 + 3] = a3;
-        }
+        });
         // lane r's own row: bias, 1 / A_rr, kind (contact rows are (normal, friction, friction)
         // triples 3c..3c+2, then the limit rows)
         float b = 0.0f, ia = 1.0f;
@@ -523,38 +523,40 @@ MI_D void pair_artic_substep(const DevModel& m, const WaveTabs& t, const DevStat
             int nrow_it = nrows_max;
             asm volatile("" : "+s"(nrow_it));
             float lamn = 0.0f;
-#pragma unroll
-            for (int rr = 0; rr < RMAX; ++rr) {
-                if (rr >= nrow_it) break;
-                __builtin_amdgcn_sched_barrier(0);
-                // the row's owner (lane rr of each half) holds v_rr, b, 1 / A_rr and its kind:
-                // it alone projects, and one broadcast hands the new lambda to its half
-                const float l0 = lamv[rr];
-                float mine = l0 + (b - v) * ia;
-                const bool fric = kd == 1 || kd == 2;
-                const float lim = mu * lamn;
-                mine = fmaxf(mine, fric ? -lim : 0.0f);
-                mine = fric ? fminf(mine, lim) : mine;
-                const bool live_row = rr < nrows;
-                const float ln = live_row ? pbc(mine, rr) : l0;
-                if (rr % 3 == 0) lamn = rr < nnorm ? ln : lamn;
-                v += Ar[rr] * (ln - l0);
-                lamv[rr] = ln;
-            }
+            sfor<0, RMAX>([&](auto RR) {   // fully unrolled: Ar / lamv stay register-indexed
+                constexpr int rr = RR;
+                if (rr < nrow_it) {           // uniform
+                    __builtin_amdgcn_sched_barrier(0);
+                    // the row's owner (lane rr of each half) holds v_rr, b, 1 / A_rr and its kind:
+                    // it alone projects, and one broadcast hands the new lambda to its half
+                    const float l0 = lamv[rr];
+                    float mine = l0 + (b - v) * ia;
+                    const bool fric = kd == 1 || kd == 2;
+                    const float lim = mu * lamn;
+                    mine = fmaxf(mine, fric ? -lim : 0.0f);
+                    mine = fric ? fminf(mine, lim) : mine;
+                    const float bc = pbc(mine, rr);
+                    const float ln = rr < nrows ? bc : l0;
+                    if constexpr (rr % 3 == 0) lamn = rr < nnorm ? ln : lamn;
+                    v += Ar[rr] * (ln - l0);
+                    lamv[rr] = ln;
+                }
+            });
         }
         float u = lane < NV ? us[lane] : 0.0f;
         const int kc = lane < NV ? lane : 0;
+        sfor<0, RMAX / 4>([&](auto G) {
+            constexpr int g0 = 4 * G;
+            if (g0 < nrows_max) {
+                float wq[4];
 #pragma unroll
-        for (int g0 = 0; g0 < RMAX; g0 += 4) {
-            if (g0 >= nrows_max) break;
-            float wq[4];
+                for (int q = 0; q < 4; ++q)
+                    wq[q] = g0 + 3 < t.w_rows_lds ? sm[t.s_W + min(g0 + q, last) * NV + kc]
+                                                  : pair_wrow(t, sm, gW, min(g0 + q, last), NV)[kc];
 #pragma unroll
-            for (int q = 0; q < 4; ++q)
-                wq[q] = g0 + 3 < t.w_rows_lds ? sm[t.s_W + min(g0 + q, last) * NV + kc]
-                                              : pair_wrow(t, sm, gW, min(g0 + q, last), NV)[kc];
-#pragma unroll
-            for (int q = 0; q < 4; ++q) u = g0 + q < nrows ? u + wq[q] * lamv[g0 + q] : u;
-        }
+                for (int q = 0; q < 4; ++q) u = g0 + q < nrows ? u + wq[q] * lamv[g0 + q] : u;
+            }
+        });
         if (lane < NV) us[lane] = u;
         wave_sync();
 #pragma unroll
@@ -595,6 +597,7 @@ MI_D void pair_artic_substep(const DevModel& m, const WaveTabs& t, const DevStat
         };
         if (lane < nrows) load_row(lane, b0, ia0, k0, fa, ma, ma2);
         if (lane + 32 < nrows) load_row(lane + 32, b1, ia1, k1, fb, mb, mb2);
+        const int nnorm = 3 * ncon;
         float Wr[64];
 #pragma unroll
         for (int rr = 0; rr < 64; ++rr) {   // uniform branch per row: LDS rows, then the slab
@@ -605,7 +608,7 @@ MI_D void pair_artic_substep(const DevModel& m, const WaveTabs& t, const DevStat
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
         for (int it = 0; it < p.iters; ++it) {
-            asm volatile("" : "+v"(b0), "+v"(b1), "+v"(ia0), "+v"(ia1), "+v"(k0), "+v"(k1),
+            asm volatile("" : "+v"(b0), "+v"(b1), "+v"(ia0), "+v"(ia1),
                          "+v"(ma), "+v"(mb), "+v"(ma2), "+v"(mb2));
             int nrow_it = nrows_max;
             asm volatile("" : "+s"(nrow_it));
@@ -620,8 +623,10 @@ MI_D void pair_artic_substep(const DevModel& m, const WaveTabs& t, const DevStat
                 for (int q = 0; q < 6; ++q) fr[q] = pbc(bank ? fb[q] : fa[q], w);
                 const unsigned msk = (unsigned)pbci((int)(bank ? mb : ma), w);
                 const unsigned msk2 = (unsigned)pbci((int)(bank ? mb2 : ma2), w);
-                const int kind = (int)pbc(bank ? k1 : k0, w);
-                const float j0 = kind == 3 ? fr[0] : dot6(S6, fr);
+                const int kind = rr < nnorm ? rr % 3 : 3;   // (normal, friction, friction) triples, limits
+                float d6 = dot6(S6, fr);
+                asm volatile("" : "+v"(d6));                 // computed on every lane: no branch
+                const float j0 = kind == 3 ? fr[0] : d6;
                 const float jc = ((((msk >> lane) & 1u) ? j0 : 0.0f) - (((msk2 >> lane) & 1u) ? j0 : 0.0f)) * kin;
                 const float jv = psum(jc * u);
                 const float br = pbc(bank ? b1 : b0, w), iar = pbc(bank ? ia1 : ia0, w);
@@ -634,7 +639,9 @@ MI_D void pair_artic_substep(const DevModel& m, const WaveTabs& t, const DevStat
                 const bool live_row = rr < nrows;
                 lamn = (live_row && kind == 0) ? ln : lamn;
                 u = live_row ? u + Wr[rr] * (ln - l0) : u;
-                if (live_row && lane_here(lane) == w) { if (bank) lam1 = ln; else lam0 = ln; }
+                const bool own = live_row && lane_here(lane) == w;
+                if (bank) lam1 = own ? ln : lam1;
+                else lam0 = own ? ln : lam0;
             }
             for (int r = 64; r < nrow_it; ++r) {
                 const bool live_row = r < nrows;
