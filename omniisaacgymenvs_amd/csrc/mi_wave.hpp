@@ -1195,27 +1195,32 @@ MI_D void wave_artic_substep(const DevModel& m, const WaveTabs& t, const DevStat
             const float mu = p.friction;
             for (int it = 0; it < p.iters; ++it) {
                 // opaque per sweep: keeps the loop-invariant readlanes inside the sweep
-                asm volatile("" : "+v"(b), "+v"(ia), "+v"(kd));
+                asm volatile("" : "+v"(b), "+v"(ia));
                 int nrow_it = nrows;
                 asm volatile("" : "+s"(nrow_it));
                 float lamn = 0.0f;
-#pragma unroll
-                for (int rr = 0; rr < RMAX; ++rr) {
-                    if (rr >= nrow_it) break;
-                    __builtin_amdgcn_sched_barrier(0);
-                    const float vr = readlane(v, rr);
-                    const float br = readlane(b, rr), iar = readlane(ia, rr);
-                    const float l0 = readlane(lam, rr);
-                    const int kind = (int)readlane(kd, rr);
-                    float ln = l0 + (br - vr) * iar;
-                    const bool fric = kind == 1 || kind == 2;
-                    const float lim = mu * lamn;
-                    ln = fmaxf(ln, fric ? -lim : 0.0f);     // normal / limit: lambda >= 0
-                    ln = fric ? fminf(ln, lim) : ln;         // friction: |lambda| <= mu lambda_n
-                    lamn = kind == 0 ? ln : lamn;
-                    v += Ar[rr] * (ln - l0);
-                    if (lane_here(lane) == rr) lam = ln;
-                }
+                // fully unrolled by template (a rolled loop indexes Ar through s_set_gpr_idx and
+                // branches per row); rows past nrows skipped by a uniform branch. Row kinds follow
+                // from the row index: contact rows are (normal, friction, friction) triples, then
+                // the limit rows.
+                sfor<0, RMAX>([&](auto RR) {
+                    constexpr int rr = RR;
+                    if (rr < nrow_it) {
+                        __builtin_amdgcn_sched_barrier(0);
+                        const float vr = readlane(v, rr);
+                        const float br = readlane(b, rr), iar = readlane(ia, rr);
+                        const float l0 = readlane(lam, rr);
+                        const int kind = rr < nc ? rr % 3 : 3;
+                        float ln = l0 + (br - vr) * iar;
+                        const bool fric = kind == 1 || kind == 2;
+                        const float lim = mu * lamn;
+                        ln = fmaxf(ln, fric ? -lim : 0.0f);     // normal / limit: lambda >= 0
+                        ln = fric ? fminf(ln, lim) : ln;         // friction: |lambda| <= mu lambda_n
+                        if constexpr (rr % 3 == 0) lamn = kind == 0 ? ln : lamn;
+                        v += Ar[rr] * (ln - l0);
+                        lam = lane_here(lane) == rr ? ln : lam;
+                    }
+                });
             }
             float u = lane < NV ? us[lane] : 0.0f;
             const int kc = lane < NV ? lane : 0;
