@@ -507,7 +507,7 @@ MI_D void pair_artic_substep(const DevModel& m, const WaveTabs& t, const DevStat
         });
         // lane r's own row: bias, 1 / A_rr, kind (contact rows are (normal, friction, friction)
         // triples 3c..3c+2, then the limit rows)
-        float b = 0.0f, ia = 1.0f;
+        float b = 0.0f, ia = 0.0f;   // ia 0: a dead row's projection keeps its lambda 0
         int kd = 0;
         if (lane < nrows) {
             b = sm[t.s_rb + lane];
@@ -529,14 +529,15 @@ MI_D void pair_artic_substep(const DevModel& m, const WaveTabs& t, const DevStat
                     __builtin_amdgcn_sched_barrier(0);
                     // the row's owner (lane rr of each half) holds v_rr, b, 1 / A_rr and its kind:
                     // it alone projects, and one broadcast hands the new lambda to its half
+                    // (a row past its half's count projects to its lambda 0 unchanged: the
+                    // owner lane holds ia = 0, kind 0)
                     const float l0 = lamv[rr];
-                    float mine = l0 + (b - v) * ia;
                     const bool fric = kd == 1 || kd == 2;
                     const float lim = mu * lamn;
-                    mine = fmaxf(mine, fric ? -lim : 0.0f);
-                    mine = fric ? fminf(mine, lim) : mine;
-                    const float bc = pbc(mine, rr);
-                    const float ln = rr < nrows ? bc : l0;
+                    // one med3: max(., lo) then, for friction, min(., lim) (lo <= hi: lamn >= 0)
+                    const float mine = __builtin_amdgcn_fmed3f(l0 + (b - v) * ia, fric ? -lim : 0.0f,
+                                                               fric ? lim : __builtin_huge_valf());
+                    const float ln = pbc(mine, rr);
                     if constexpr (rr % 3 == 0) lamn = rr < nnorm ? ln : lamn;
                     v += Ar[rr] * (ln - l0);
                     lamv[rr] = ln;

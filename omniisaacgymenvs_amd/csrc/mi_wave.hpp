@@ -1211,11 +1211,12 @@ MI_D void wave_artic_substep(const DevModel& m, const WaveTabs& t, const DevStat
                         const float br = readlane(b, rr), iar = readlane(ia, rr);
                         const float l0 = readlane(lam, rr);
                         const int kind = rr < nc ? rr % 3 : 3;
-                        float ln = l0 + (br - vr) * iar;
                         const bool fric = kind == 1 || kind == 2;
                         const float lim = mu * lamn;
-                        ln = fmaxf(ln, fric ? -lim : 0.0f);     // normal / limit: lambda >= 0
-                        ln = fric ? fminf(ln, lim) : ln;         // friction: |lambda| <= mu lambda_n
+                        // normal / limit: lambda >= 0; friction: |lambda| <= mu lambda_n (one med3;
+                        // lamn >= 0)
+                        const float ln = __builtin_amdgcn_fmed3f(l0 + (br - vr) * iar, fric ? -lim : 0.0f,
+                                                                 fric ? lim : __builtin_huge_valf());
                         if constexpr (rr % 3 == 0) lamn = kind == 0 ? ln : lamn;
                         v += Ar[rr] * (ln - l0);
                         lam = lane_here(lane) == rr ? ln : lam;

@@ -66,6 +66,9 @@ def main():
            "phases_slow2pct_vs_median": {PHASES[p]: [round(a[slow, p].mean()), round(a[mid, p].mean())] for p in ph},
            "stats_slow2pct_vs_median_per_substep": {STATS[s]: [round(a[slow, s].mean() / 2, 3), round(a[mid, s].mean() / 2, 3)]
                                                     for s in STATS}}
+    top = order[-5:][::-1]
+    out["slowest5"] = [{"cycles": round(tot[w]), "P10": round(a[w, 11]), "rows": a[w, 15] / 2,
+                        "rows>lam": a[w, 19] / 2, "contacts": a[w, 20] / 2} for w in top]
     print(json.dumps(out), flush=True)
 
 
