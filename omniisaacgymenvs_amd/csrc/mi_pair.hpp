@@ -92,6 +92,10 @@ MI_D void pair_jrow(const MC& mc, const WaveTabs& t, const float* sm, int r, int
 
 // W row r of this lane's env: LDS rows [0, w_rows_lds) (one segment: the pair layout has no
 // second), the env's global slab beyond
+// LDS-typed pointer: loads through it are ds_reads even where the compiler would merge them
+// with the slab path of the same expression into flat loads
+typedef const float __attribute__((address_space(3)))* lds_cf;
+MI_D lds_cf lds_ptr(const float* p) { return (lds_cf)p; }
 MI_D const float* pair_wrow(const WaveTabs& t, const float* sm, const float* gW, int r, int nv) {
     return r < t.w_rows_lds ? sm + t.s_W + r * nv : gW + (size_t)r * WNV;
 }
@@ -283,13 +287,12 @@ MI_D void pair_artic_substep(const DevModel& m, const WaveTabs& t, const DevStat
             int* surv = reinterpret_cast<int*>(sm + t.s_surv);
             int nsv = 0;
             const float slack = p.contact_offset + 1e-3f;
-            for (int pb = 0; pb < t.npairs; pb += 32) {
+            auto broad = [&](int pb, int2 gpq, bool pref) {
                 const int pi = pb + lane;
                 bool keep = false;
                 int2 gp = make_int2(0, 0);
                 if (pi < t.npairs) {
-                    const int q = pb >> 5;
-                    gp = q == 0 ? gpf[0] : q == 1 ? gpf[1] : q == 2 ? gpf[2] : q == 3 ? gpf[3] : q == 4 ? gpf[4] : gpr[pi];
+                    gp = pref ? gpq : gpr[pi];
                     const float4 A = *reinterpret_cast<const float4*>(bnd + 4 * gp.x);
                     const float4 B = *reinterpret_cast<const float4*>(bnd + 4 * gp.y);
                     const float cx = A.x - B.x, cy = A.y - B.y, cz = A.z - B.z;
@@ -299,7 +302,10 @@ MI_D void pair_artic_substep(const DevModel& m, const WaveTabs& t, const DevStat
                 const unsigned mask = hballot(keep);
                 if (keep) surv[nsv + __popc(mask & lanemask_lt(lane))] = gp.x | (gp.y << 16);
                 nsv += __popc(mask);
-            }
+            };
+            // the prefetched blocks by compile-time index (a runtime pick among them went to scratch)
+            sfor<0, 5>([&](auto Q) { if (32 * (int)Q < t.npairs) broad(32 * (int)Q, gpf[Q], true); });
+            for (int pb = 160; pb < t.npairs; pb += 32) broad(pb, make_int2(0, 0), false);
             wave_sync();
             int budget = (MI_MAX_ROWS - 3 * ncon - t.nlimc) / 3;
             const int nsv_max = pmax(nsv);
@@ -488,7 +494,7 @@ MI_D void pair_artic_substep(const DevModel& m, const WaveTabs& t, const DevStat
             constexpr int g0 = 4 * G;
             float a0 = 0.0f, a1 = 0.0f, a2 = 0.0f, a3 = 0.0f;
             if (g0 < nrows_max) {
-                auto dots = [&](const float* w0, const float* w1, const float* w2, const float* w3) {
+                auto dots = [&](auto w0, auto w1, auto w2, auto w3) {
                     sfor<0, NV>([&](auto C) {
                         a0 += Jr[C] * w0[C];
                         a1 += Jr[C] * w1[C];
@@ -496,10 +502,11 @@ MI_D void pair_artic_substep(const DevModel& m, const WaveTabs& t, const DevStat
                         a3 += Jr[C] * w3[C];
                     });
                 };
-                if (g0 + 3 < t.w_rows_lds)   // uniform: all four rows in LDS (ds_read)
-                    dots(sm + t.s_W + min(g0, last) * NV, sm + t.s_W + min(g0 + 1, last) * NV,
-                         sm + t.s_W + min(g0 + 2, last) * NV, sm + t.s_W + min(g0 + 3, last) * NV);
-                else
+                if (g0 + 3 < t.w_rows_lds) {   // uniform: all four rows in LDS (ds_read)
+                    const lds_cf W = lds_ptr(sm + t.s_W);
+                    dots(W + min(g0, last) * NV, W + min(g0 + 1, last) * NV,
+                         W + min(g0 + 2, last) * NV, W + min(g0 + 3, last) * NV);
+                } else
                     dots(pair_wrow(t, sm, gW, min(g0, last), NV), pair_wrow(t, sm, gW, min(g0 + 1, last), NV),
                          pair_wrow(t, sm, gW, min(g0 + 2, last), NV), pair_wrow(t, sm, gW, min(g0 + 3, last), NV));
             }
@@ -515,6 +522,7 @@ MI_D void pair_artic_substep(const DevModel& m, const WaveTabs& t, const DevStat
             kd = (int)sm[t.s_rk + lane];
         }
         const int nnorm = 3 * ncon;   // rows below this with r % 3 == 0 are normal rows
+        STAMP(27);
         float lamv[RMAX];
 #pragma unroll
         for (int rr = 0; rr < RMAX; ++rr) lamv[rr] = 0.0f;
@@ -544,6 +552,7 @@ MI_D void pair_artic_substep(const DevModel& m, const WaveTabs& t, const DevStat
                 }
             });
         }
+        STAMP(28);
         float u = lane < NV ? us[lane] : 0.0f;
         const int kc = lane < NV ? lane : 0;
         sfor<0, RMAX / 4>([&](auto G) {
@@ -552,7 +561,7 @@ MI_D void pair_artic_substep(const DevModel& m, const WaveTabs& t, const DevStat
                 float wq[4];
 #pragma unroll
                 for (int q = 0; q < 4; ++q)
-                    wq[q] = g0 + 3 < t.w_rows_lds ? sm[t.s_W + min(g0 + q, last) * NV + kc]
+                    wq[q] = g0 + 3 < t.w_rows_lds ? lds_ptr(sm + t.s_W)[min(g0 + q, last) * NV + kc]
                                                   : pair_wrow(t, sm, gW, min(g0 + q, last), NV)[kc];
 #pragma unroll
                 for (int q = 0; q < 4; ++q) u = g0 + q < nrows ? u + wq[q] * lamv[g0 + q] : u;
@@ -608,6 +617,7 @@ MI_D void pair_artic_substep(const DevModel& m, const WaveTabs& t, const DevStat
         for (int r = 64 + lane; r < nrows; r += 32) gW[(size_t)r * WNV + (WNV - 1)] = 0.0f;
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+        STAMP(27);
         for (int it = 0; it < p.iters; ++it) {
             asm volatile("" : "+v"(b0), "+v"(b1), "+v"(ia0), "+v"(ia1),
                          "+v"(ma), "+v"(mb), "+v"(ma2), "+v"(mb2));
@@ -681,6 +691,7 @@ MI_D void pair_artic_substep(const DevModel& m, const WaveTabs& t, const DevStat
                 __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
             }
         }
+        STAMP(28);
         if (lane < nv) us[lane] = u;
         if (lane < nrows) sm[t.s_ad + lane] = lam0;          // reuse: lambda of row lane
         if (lane + 32 < nrows) sm[t.s_ad + lane + 32] = lam1;

@@ -1223,9 +1223,13 @@ int mi_sim_create(const mi_model_desc* md, const mi_sim_params* prm, int32_t N, 
             waves = decltype(T)::kWaves; lam_rows = decltype(T)::kLamRows;
             pair_ok = has_pair<decltype(T)>();
         });
-        // paired kernels (mi_pair.hpp, two envs per wavefront, 16 per workgroup): MI_WAVE_PAIR=1
+        // paired kernels (mi_pair.hpp, two envs per wavefront, 16 per workgroup): the default for
+        // the compiled topologies whose one-env-per-wave kernel is register-capped at 2 waves per
+        // SIMD (Humanoid: 8 envs/CU -> 16, 4096 envs in one resident round); MI_WAVE_PAIR=0 / 1
+        // forces the choice
         const char* pe = getenv("MI_WAVE_PAIR");
-        s->pair = ct && pair_ok && N % 2 == 0 && pe && atoi(pe) != 0;
+        const bool pair_want = pe ? atoi(pe) != 0 : waves <= 2;
+        s->pair = ct && pair_ok && N % 2 == 0 && pair_want;
         const int envs_cu = s->pair ? 16 : 4 * std::max(1, waves);
         t.envs_per_wg = s->pair ? 16 : (ct && waves >= 4 ? 4 : 1);
         if (const char* e = getenv("MI_WAVE_ENVS"); e && !s->pair) t.envs_per_wg = std::max(1, std::min(4, atoi(e)));

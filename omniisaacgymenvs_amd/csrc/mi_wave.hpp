@@ -830,13 +830,12 @@ MI_D void wave_artic_substep(const DevModel& m, const WaveTabs& t, const DevStat
         int* surv = reinterpret_cast<int*>(sm + t.s_surv);
         int nsv = 0;
         const float slack = p.contact_offset + 1e-3f;
-        for (int pb = 0; pb < t.npairs; pb += 64) {
+        auto broad = [&](int pb, int2 gpq, bool pref) {
             const int pi = pb + lane;
             bool keep = false;
             int2 gp = make_int2(0, 0);
             if (pi < t.npairs) {
-                const int q = pb >> 6;
-                gp = q == 0 ? gpf[0] : q == 1 ? gpf[1] : q == 2 ? gpf[2] : q == 3 ? gpf[3] : gpr[pi];
+                gp = pref ? gpq : gpr[pi];
                 const float4 A = *reinterpret_cast<const float4*>(bnd + 4 * gp.x);
                 const float4 B = *reinterpret_cast<const float4*>(bnd + 4 * gp.y);
                 const float cx = A.x - B.x, cy = A.y - B.y, cz = A.z - B.z;
@@ -846,7 +845,10 @@ MI_D void wave_artic_substep(const DevModel& m, const WaveTabs& t, const DevStat
             const unsigned long long mask = __ballot(keep);
             if (keep) surv[nsv + __popcll(mask & ((1ull << lane) - 1ull))] = gp.x | (gp.y << 16);
             nsv += __popcll(mask);
-        }
+        };
+        // the prefetched blocks by compile-time index (a runtime pick among them went to scratch)
+        sfor<0, 4>([&](auto Q) { if (64 * (int)Q < t.npairs) broad(64 * (int)Q, gpf[Q], true); });
+        for (int pb = 256; pb < t.npairs; pb += 64) broad(pb, make_int2(0, 0), false);
         nsv = __builtin_amdgcn_readfirstlane(nsv);
         wave_sync();
         // narrow phase on the survivors (mi_geom.h, as the oracle)

@@ -2,7 +2,7 @@
 # instruction count of the Humanoid env-step kernel per source phase (line tables):
 # tools/codesize.sh [extra hipcc flags...]
 D=$(mktemp -d)
-cd "$D" && /opt/rocm/bin/hipcc -O3 -std=c++17 -fPIC -shared --offload-arch=gfx950 -Wno-unused-function \
+cd "$D" && /opt/rocm/bin/hipcc -O3 -std=c++17 -fPIC -shared --offload-arch=gfx950 -fno-slp-vectorize -Wno-unused-function \
   -Wno-unused-variable -gline-tables-only "$@" -save-temps /root/repo/omniisaacgymenvs_amd/csrc/mi_sim.hip -o t.so 2>&1 | grep -i " error"
 S=mi_sim-hip-amdgcn-amd-amdhsa-gfx950.s
 start=$(grep -n "^_Z15k_env_step_waveIN2mi6TopoCTINS0_13RobotHumanoid.*:" $S | cut -d: -f1)

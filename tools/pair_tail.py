@@ -55,7 +55,11 @@ def main():
     rows.append(np.ctypeslib.as_array(buf).reshape(nw, 32).copy())
     env.close()
     a = np.concatenate(rows).astype(np.float64)          # [waves x launches, 32]
-    ph = [k for k in PHASES if k != 5]
+    phases = dict(PHASES)
+    phases[11] = "P10 pgs: u update"
+    phases[27] = "P10 pgs: set-up (Delassus rows / W registers)"
+    phases[28] = "P10 pgs: sweeps"
+    ph = [k for k in phases if k != 5]
     tot = a[:, ph].sum(axis=1)
     order = np.argsort(tot)
     k = max(1, len(tot) // 50)
@@ -63,11 +67,11 @@ def main():
     out = {"task": task, "envs": n, "pair": pair, "waves": int(len(tot)),
            "wave_cycles": {q: float(np.quantile(tot, v)) for q, v in
                            (("p50", .5), ("p90", .9), ("p99", .99), ("max", 1.0))},
-           "phases_slow2pct_vs_median": {PHASES[p]: [round(a[slow, p].mean()), round(a[mid, p].mean())] for p in ph},
+           "phases_slow2pct_vs_median": {phases[p]: [round(a[slow, p].mean()), round(a[mid, p].mean())] for p in ph},
            "stats_slow2pct_vs_median_per_substep": {STATS[s]: [round(a[slow, s].mean() / 2, 3), round(a[mid, s].mean() / 2, 3)]
                                                     for s in STATS}}
     top = order[-5:][::-1]
-    out["slowest5"] = [{"cycles": round(tot[w]), "P10": round(a[w, 11]), "rows": a[w, 15] / 2,
+    out["slowest5"] = [{"cycles": round(tot[w]), "P10": [round(a[w, 27]), round(a[w, 28]), round(a[w, 11])], "rows": a[w, 15] / 2,
                         "rows>lam": a[w, 19] / 2, "contacts": a[w, 20] / 2} for w in top]
     print(json.dumps(out), flush=True)
 

@@ -3,7 +3,7 @@
 # tables on): KERNEL=RobotAnt|RobotHumanoid [KNAME=k_env_step_pair] tools/spills.sh [extra hipcc flags...]
 D=$(mktemp -d)
 K=${KERNEL:-RobotHumanoid}
-cd "$D" && /opt/rocm/bin/hipcc -O3 -std=c++17 -fPIC -shared --offload-arch=gfx950 -Wno-unused-function \
+cd "$D" && /opt/rocm/bin/hipcc -O3 -std=c++17 -fPIC -shared --offload-arch=gfx950 -fno-slp-vectorize -Wno-unused-function \
   -Wno-unused-variable ${SPILL_FLAGS:-} -gline-tables-only "$@" -save-temps /root/repo/omniisaacgymenvs_amd/csrc/mi_sim.hip -o t.so 2>&1 | grep -i " error"
 S=mi_sim-hip-amdgcn-amd-amdhsa-gfx950.s
 start=$(grep -n "^_Z[0-9]*${KNAME:-k_env_step_wave}IN2mi6TopoCTINS0_[0-9]*${K}.*:" $S | cut -d: -f1)
