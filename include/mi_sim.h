@@ -278,8 +278,7 @@ int mi_set_reset_count(mi_sim* sim, const uint32_t* in /*[N] host*/);
 /* Number of env-steps whose physics produced a non-finite state and were forced to reset. */
 int mi_sim_nan_count(mi_sim* sim, int64_t* count);
 /* Diagnostics: which physics kernel runs. path: 0 one-lane-per-env, 1 wavefront-per-env,
- * 2 two envs per wavefront (compiled topologies at 2 waves/SIMD, i.e. Humanoid, unless
- *   MI_WAVE_PAIR=0; MI_WAVE_PAIR=1 forces it for the others);
+ * 2 two envs per wavefront (the compiled topologies' default; MI_WAVE_PAIR=0 selects path 1);
  * topology: id of the compile-time (model-specialised) topology, 0 = runtime tables;
  * lds_bytes: LDS per env (= per workgroup) of the wave path. Any output may be NULL. */
 int mi_sim_kernel_path(const mi_sim* sim, int32_t* path, int32_t* topology, int32_t* lds_bytes);

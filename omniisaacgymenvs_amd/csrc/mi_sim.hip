@@ -1223,12 +1223,12 @@ int mi_sim_create(const mi_model_desc* md, const mi_sim_params* prm, int32_t N, 
             waves = decltype(T)::kWaves; lam_rows = decltype(T)::kLamRows;
             pair_ok = has_pair<decltype(T)>();
         });
-        // paired kernels (mi_pair.hpp, two envs per wavefront, 16 per workgroup): the default for
-        // the compiled topologies whose one-env-per-wave kernel is register-capped at 2 waves per
-        // SIMD (Humanoid: 8 envs/CU -> 16, 4096 envs in one resident round); MI_WAVE_PAIR=0 / 1
-        // forces the choice
+        // paired kernels (mi_pair.hpp, two envs per wavefront, 16 per workgroup, 2 waves per
+        // SIMD): the default for the compiled topologies (Humanoid 0.219 -> 0.205 ms, Ant 0.0765
+        // -> 0.0589 ms against their one-env-per-wave kernels at 2 and 4 waves per SIMD; 4096
+        // envs in one resident round either way); MI_WAVE_PAIR=0 selects one env per wave
         const char* pe = getenv("MI_WAVE_PAIR");
-        const bool pair_want = pe ? atoi(pe) != 0 : waves <= 2;
+        const bool pair_want = pe ? atoi(pe) != 0 : true;
         s->pair = ct && pair_ok && N % 2 == 0 && pair_want;
         const int envs_cu = s->pair ? 16 : 4 * std::max(1, waves);
         t.envs_per_wg = s->pair ? 16 : (ct && waves >= 4 ? 4 : 1);
