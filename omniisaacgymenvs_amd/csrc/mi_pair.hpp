@@ -572,6 +572,101 @@ MI_D void pair_artic_substep(const DevModel& m, const WaveTabs& t, const DevStat
 #pragma unroll
         for (int rr = 0; rr < RMAX; ++rr)            // reuse: lambda of row rr
             if (lane == rr && rr < nrows) sm[t.s_ad + rr] = lamv[rr];
+    } else if (nrows_max <= 64) {
+        // Wide Delassus (a half with 33..64 rows: 0.4 % of Humanoid substeps, but they set the
+        // launch's slowest waves): the two envs one after the other, each on all 64 lanes, lane
+        // r = row r of that env. Per row: the owner lane projects, one v_readlane hands the new
+        // lambda to the wave (its old one is read off the chain), one FMA per lane updates v.
+        constexpr int NV = TP::nv;
+        const int l64 = pair_l64(), me = l64 >> 5;
+        const int kc = l64 < NV ? l64 : 0;
+        for (int h = 0; h < 2; ++h) {
+            const int nrh = __builtin_amdgcn_readlane(nrows, 32 * h);
+            const int nnh = 3 * __builtin_amdgcn_readlane(ncon, 32 * h);
+            if (nrh == 0) continue;
+            float* smh = sm + (h - me) * t.env_stride;                 // env of half h
+            const float* gWh = gW + (ptrdiff_t)(h - me) * (ptrdiff_t)t.g_row_stride;
+            const int last = nrh - 1;
+            const int rl = l64 < nrh ? l64 : 0;
+            float Jr[TP::nvc];
+            pair_jrow<TP>(mc, t, smh, rl, nr, Jr);
+            const float* ush = smh + t.s_us;
+            float v = 0.0f;
+            sfor<0, NV>([&](auto C) { v += Jr[C] * ush[C]; });
+            float Ar[64];
+            sfor<0, 16>([&](auto G) {
+                constexpr int g0 = 4 * G;
+                float a0 = 0.0f, a1 = 0.0f, a2 = 0.0f, a3 = 0.0f;
+                if (g0 < nrh) {
+                    auto dots = [&](auto w0, auto w1, auto w2, auto w3) {
+                        sfor<0, NV>([&](auto C) {
+                            a0 += Jr[C] * w0[C];
+                            a1 += Jr[C] * w1[C];
+                            a2 += Jr[C] * w2[C];
+                            a3 += Jr[C] * w3[C];
+                        });
+                    };
+                    if (g0 + 3 < t.w_rows_lds) {
+                        const lds_cf W = lds_ptr(smh + t.s_W);
+                        dots(W + min(g0, last) * NV, W + min(g0 + 1, last) * NV,
+                             W + min(g0 + 2, last) * NV, W + min(g0 + 3, last) * NV);
+                    } else {
+                        dots(pair_wrow(t, smh, gWh, min(g0, last), NV), pair_wrow(t, smh, gWh, min(g0 + 1, last), NV),
+                             pair_wrow(t, smh, gWh, min(g0 + 2, last), NV), pair_wrow(t, smh, gWh, min(g0 + 3, last), NV));
+                    }
+                }
+                Ar[g0] = a0; Ar[g0 + 1] = a1; Ar[g0 + 2] = a2; Ar[g0 + 3] = a3;
+            });
+            float b = 0.0f, ia = 0.0f, lam = 0.0f;    // ia 0: a dead row keeps its lambda 0
+            int kd = 0;
+            if (l64 < nrh) {
+                b = smh[t.s_rb + l64];
+                ia = 1.0f / smh[t.s_ad + l64];
+                kd = l64 < nnh ? l64 % 3 : 3;
+            }
+            for (int it = 0; it < p.iters; ++it) {
+                asm volatile("" : "+v"(b), "+v"(ia), "+v"(kd));
+                int nrow_it = nrh;
+                asm volatile("" : "+s"(nrow_it));
+                float lamn = 0.0f;
+                sfor<0, 64>([&](auto RR) {
+                    constexpr int rr = RR;
+                    if (rr < nrow_it) {
+                        __builtin_amdgcn_sched_barrier(0);
+                        const bool fric = kd == 1 || kd == 2;
+                        const float lim = mu * lamn;
+                        const float mine = __builtin_amdgcn_fmed3f(lam + (b - v) * ia, fric ? -lim : 0.0f,
+                                                                   fric ? lim : __builtin_huge_valf());
+                        const float l0 = readlane(lam, rr);
+                        const float ln = readlane(mine, rr);
+                        if constexpr (rr % 3 == 0) lamn = rr < nnh ? ln : lamn;
+                        v += Ar[rr] * (ln - l0);
+                        lam = l64 == rr ? ln : lam;
+                    }
+                });
+            }
+            // u = u* + sum_r W_r lambda_r, lane = DOF
+            float u = ush[kc];
+            sfor<0, 16>([&](auto G) {
+                constexpr int g0 = 4 * G;
+                if (g0 < nrh) {
+                    float wq[4];
+#pragma unroll
+                    for (int q = 0; q < 4; ++q)
+                        wq[q] = g0 + 3 < t.w_rows_lds ? lds_ptr(smh + t.s_W)[min(g0 + q, last) * NV + kc]
+                                                      : pair_wrow(t, smh, gWh, min(g0 + q, last), NV)[kc];
+#pragma unroll
+                    for (int q = 0; q < 4; ++q) {
+                        const float lq = readlane(lam, g0 + q);
+                        u = g0 + q < nrh ? u + wq[q] * lq : u;
+                    }
+                }
+            });
+            wave_sync();
+            if (l64 < NV) smh[t.s_us + l64] = u;
+            if (l64 < nrh) smh[t.s_ad + l64] = lam;            // reuse: lambda of row l64
+            wave_sync();
+        }
     } else {
         // fallback (a half with more rows than the Delassus registers hold, 0.4 % of Humanoid
         // substeps): u-space sweeps, lane = DOF. Rows 0..63 as the wave kernel's one-bank
