@@ -32,7 +32,7 @@
 extern "C" {
 #endif
 
-#define MI_ABI_VERSION 2
+#define MI_ABI_VERSION 3
 
 enum {
     MI_OK = 0,
@@ -171,6 +171,17 @@ int mi_set_dof_state(mi_sim* sim, const float* q /*[n,D]|NULL*/, const float* qd
 int mi_set_root_state(mi_sim* sim, const float* pos /*[n,3]|NULL*/, const float* quat /*[n,4]|NULL*/,
                       const float* vel /*[n,6]|NULL*/, const int64_t* idx /*[n]|NULL*/, int32_t n,
                       void* stream);
+/* State mirrors: row-major copies of the articulation state in caller-owned device buffers, the
+ * tensors ArticulationView getters hand out with clone=False (get_world_poses, get_velocities,
+ * get_joint_positions / velocities, _physics_view.get_force_sensor_forces: locomotion.py:81-89;
+ * Isaac returns views of its own buffers there too). Register all six (or all NULL to stop);
+ * mi_get_state_mirror issues any deferred substeps and refreshes every stale mirror in ONE launch
+ * (none when nothing wrote the state since the last refresh), so the five getter calls of one
+ * get_observations cost at most one gather launch. Every entry point that writes the state marks
+ * the mirrors stale; mi_set_dof_efforts does not (efforts are not mirrored). */
+int mi_sim_set_mirror(mi_sim* sim, float* pos /*[N,3]*/, float* quat /*[N,4]*/, float* vel /*[N,6]*/,
+                      float* q /*[N,D]*/, float* qd /*[N,D]*/, float* sens /*[N,S,6]*/);
+int mi_get_state_mirror(mi_sim* sim, void* stream);
 
 /* --- physics step: World.step x controlFrequencyInv (envs/vec_env_rlgames.py:64-66) --- */
 /* Substeps are deferred and coalesced: consecutive mi_sim_step calls on one stream with no

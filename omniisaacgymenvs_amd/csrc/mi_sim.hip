@@ -80,6 +80,10 @@ struct mi_sim {
     int pending = 0;
     hipStream_t pending_stream = nullptr;
     hipEvent_t pending_ev = nullptr;
+    // state mirrors (mi_sim_set_mirror): row-major pos, quat, vel, q, qd, sens; valid = every
+    // mirror equals the state (set by mi_get_state_mirror, cleared by every state write)
+    float* mir[6] = {nullptr, nullptr, nullptr, nullptr, nullptr, nullptr};
+    bool mir_valid = false;
     std::vector<float> lower, upper;  // host copy for mi_sim_info
     std::vector<void*> allocs;
     // launch timing (mi_sim_time_launches): every tev_every-th mi_env_step launch carries a
@@ -831,11 +835,14 @@ __global__ void k_reset_idx(DevModel m, DevState st, DevTask tp, const int64_t* 
 // field-major reads in, row-major writes out, both coalesced.
 constexpr int MI_GATHER_TILE = 256, MI_GATHER_MAXC = 32;
 // Several fields of one ArticulationView call (get_world_poses: pos + quat; set_world_poses;
-// get / set_velocities, ...) in ONE launch: blockIdx.y picks the field.
-struct GField { const float* src; float* dst; int C; };
-struct GFields { GField f[3]; };
-__global__ __launch_bounds__(256) void k_soa_to_rows_multi(GFields fs3, int N, int fs, int es) {
+// get / set_velocities, ...), or all six state mirrors, in ONE launch: blockIdx.y picks the field.
+// fs / es: the state side's field / env strides of this field (gathers: per field, since the
+// sensor wrenches have strides of their own; scatters take the record strides as arguments)
+struct GField { const float* src; float* dst; int C; int fs = 0, es = 0; };
+struct GFields { GField f[6]; };
+__global__ __launch_bounds__(256) void k_soa_to_rows_multi(GFields fs3, int N) {
     const GField g = fs3.f[blockIdx.y];
+    const int fs = g.fs, es = g.es;
     const int64_t e0 = (int64_t)blockIdx.x * MI_GATHER_TILE;
     const int ne = (int)min((int64_t)MI_GATHER_TILE, (int64_t)N - e0);
     const int C = g.C, tot = ne * C;
@@ -1484,6 +1491,7 @@ int mi_sim_info(const mi_sim* s, int32_t* num_envs, int32_t* num_dof, int32_t* n
 #define NEED(p) if (!(p)) return fail(MI_E_NULL, "%s: null %s", __func__, #p)
 
 static int launch_sim(mi_sim* s, int substeps, hipStream_t stream) {
+    s->mir_valid = false;
     if (s->wave)
         with_topo(s->topo, [&](auto T) {
             if constexpr (has_pair<decltype(T)>()) {
@@ -1531,11 +1539,11 @@ static int flush_pending(mi_sim* s, void* stream) {
 }
 #define FLUSH(s, stream) do { int rc_ = flush_pending((s), (stream)); if (rc_) return rc_; } while (0)
 
-static int gather_fields(mi_sim* s, GFields f, int nf, int fs, int es, void* stream) {
+static int gather_fields(mi_sim* s, GFields f, int nf, void* stream) {
     if (nf == 0) return MI_OK;
     dim3 g = gather_grid(s->N);
     g.y = (unsigned)nf;
-    hipLaunchKernelGGL(k_soa_to_rows_multi, g, dim3(256), 0, STREAM(stream), f, s->N, fs, es);
+    hipLaunchKernelGGL(k_soa_to_rows_multi, g, dim3(256), 0, STREAM(stream), f, s->N);
     LAUNCH_CHECK();
     return MI_OK;
 }
@@ -1559,10 +1567,11 @@ int mi_get_root_state(mi_sim* s, float* pos, float* quat, float* vel, void* stre
     FLUSH(s, stream);
     GFields f{};
     int nf = 0;
-    if (pos) f.f[nf++] = {s->ds.root_pos, pos, 3};
-    if (quat) f.f[nf++] = {s->ds.root_quat, quat, 4};
-    if (vel) f.f[nf++] = {s->ds.root_vel, vel, 6};
-    return gather_fields(s, f, nf, s->ds.fs, s->ds.es, stream);
+    const int fs = s->ds.fs, es = s->ds.es;
+    if (pos) f.f[nf++] = {s->ds.root_pos, pos, 3, fs, es};
+    if (quat) f.f[nf++] = {s->ds.root_quat, quat, 4, fs, es};
+    if (vel) f.f[nf++] = {s->ds.root_vel, vel, 6, fs, es};
+    return gather_fields(s, f, nf, stream);
 }
 
 int mi_get_dof_state(mi_sim* s, float* q, float* qd, void* stream) {
@@ -1571,9 +1580,10 @@ int mi_get_dof_state(mi_sim* s, float* q, float* qd, void* stream) {
     FLUSH(s, stream);
     GFields f{};
     int nf = 0;
-    if (q) f.f[nf++] = {s->ds.q, q, s->dm.D};
-    if (qd) f.f[nf++] = {s->ds.qd, qd, s->dm.D};
-    return gather_fields(s, f, nf, s->ds.fs, s->ds.es, stream);
+    const int fs = s->ds.fs, es = s->ds.es;
+    if (q) f.f[nf++] = {s->ds.q, q, s->dm.D, fs, es};
+    if (qd) f.f[nf++] = {s->ds.qd, qd, s->dm.D, fs, es};
+    return gather_fields(s, f, nf, stream);
 }
 
 int mi_get_sensor_wrench(mi_sim* s, float* out, void* stream) {
@@ -1582,8 +1592,8 @@ int mi_get_sensor_wrench(mi_sim* s, float* out, void* stream) {
     FLUSH(s, stream);
     if (s->dm.S == 0) return MI_OK;
     GFields f{};
-    f.f[0] = {s->ds.sens, out, 6 * s->dm.S};
-    return gather_fields(s, f, 1, s->ds.sfs, s->ds.ses, stream);
+    f.f[0] = {s->ds.sens, out, 6 * s->dm.S, s->ds.sfs, s->ds.ses};
+    return gather_fields(s, f, 1, stream);
 }
 
 int mi_set_dof_efforts(mi_sim* s, const float* eff, const int32_t* idx, int32_t n, void* stream) {
@@ -1606,6 +1616,7 @@ int mi_set_dof_state(mi_sim* s, const float* q, const float* qd, const int64_t* 
     int nf = 0;
     if (q) f.f[nf++] = {q, s->ds.q, s->dm.D};
     if (qd) f.f[nf++] = {qd, s->ds.qd, s->dm.D};
+    if (nf && n) s->mir_valid = false;
     return scatter_fields<int64_t>(s, f, nf, n, idx, stream);
 }
 
@@ -1620,7 +1631,41 @@ int mi_set_root_state(mi_sim* s, const float* pos, const float* quat, const floa
     if (pos) f.f[nf++] = {pos, s->ds.root_pos, 3};
     if (quat) f.f[nf++] = {quat, s->ds.root_quat, 4};
     if (vel) f.f[nf++] = {vel, s->ds.root_vel, 6};
+    if (nf && n) s->mir_valid = false;
     return scatter_fields<int64_t>(s, f, nf, n, idx, stream);
+}
+
+int mi_sim_set_mirror(mi_sim* s, float* pos, float* quat, float* vel, float* q, float* qd, float* sens) {
+    NEED(s);
+    float* m[6] = {pos, quat, vel, q, qd, sens};
+    int set = 0;
+    for (int k = 0; k < 6; ++k) set += m[k] != nullptr;
+    if (s->dm.S == 0 && !sens && set == 5) ++set;          // no sensors: no sensor mirror needed
+    if (set != 0 && set != 6) return fail(MI_E_NULL, "mi_sim_set_mirror: register all six mirrors or none");
+    for (int k = 0; k < 6; ++k) s->mir[k] = m[k];
+    s->mir_valid = false;
+    return MI_OK;
+}
+
+int mi_get_state_mirror(mi_sim* s, void* stream) {
+    NEED(s);
+    if (!s->mir[0]) return fail(MI_E_STATE, "mi_get_state_mirror: no mirrors registered (mi_sim_set_mirror)");
+    HIP_TRY(hipSetDevice(s->device));
+    FLUSH(s, stream);
+    if (s->mir_valid) return MI_OK;
+    GFields f{};
+    int nf = 0;
+    const int fs = s->ds.fs, es = s->ds.es;
+    f.f[nf++] = {s->ds.root_pos, s->mir[0], 3, fs, es};
+    f.f[nf++] = {s->ds.root_quat, s->mir[1], 4, fs, es};
+    f.f[nf++] = {s->ds.root_vel, s->mir[2], 6, fs, es};
+    f.f[nf++] = {s->ds.q, s->mir[3], s->dm.D, fs, es};
+    f.f[nf++] = {s->ds.qd, s->mir[4], s->dm.D, fs, es};
+    if (s->dm.S > 0) f.f[nf++] = {s->ds.sens, s->mir[5], 6 * s->dm.S, s->ds.sfs, s->ds.ses};
+    const int rc = gather_fields(s, f, nf, stream);
+    if (rc) return rc;
+    s->mir_valid = true;
+    return MI_OK;
 }
 
 int mi_sim_step(mi_sim* s, int32_t substeps, void* stream) {
@@ -1698,6 +1743,7 @@ int mi_task_pre_step(mi_sim* s, const float* actions, int64_t* reset_buf, int64_
     if (s->tp.kind != MI_TASK_CARTPOLE) { NEED(potentials); NEED(prev_potentials); }
     HIP_TRY(hipSetDevice(s->device));
     FLUSH(s, stream);
+    s->mir_valid = false;   // the mask-driven resets write the state
     hipLaunchKernelGGL(k_pre_step, grid_for(s, s->N), dim3(s->block), 0, STREAM(stream), s->dm,
                        s->ds, s->tp, actions, reset_buf, progress_buf, potentials, prev_potentials,
                        actions_out);
@@ -1712,6 +1758,7 @@ int mi_task_reset_idx(mi_sim* s, const int64_t* env_ids, int32_t n, int64_t* res
     HIP_TRY(hipSetDevice(s->device));
     FLUSH(s, stream);
     if (n == 0) return MI_OK;
+    s->mir_valid = false;
     hipLaunchKernelGGL(k_reset_idx, grid_for(s, n), dim3(s->block), 0, STREAM(stream), s->dm, s->ds,
                        s->tp, env_ids, n, reset_buf, progress_buf, potentials, prev_potentials);
     LAUNCH_CHECK();
@@ -1870,6 +1917,7 @@ int mi_env_step(mi_sim* s, const float* actions, int32_t substeps, float* obs_ou
     if (substeps < 0 || substeps > 64) return fail(MI_E_ARG, "substeps %d out of range", substeps);
     HIP_TRY(hipSetDevice(s->device));
     FLUSH(s, stream);
+    s->mir_valid = false;
     hipEvent_t ev0 = nullptr, ev1 = nullptr;
     HIP_TRY(timed_launch(s, stream, &ev0, &ev1));
     if (s->wave && s->tp.kind != MI_TASK_CARTPOLE)

@@ -64,12 +64,11 @@ class _PhysicsView:
         self._view = view
 
     def get_force_sensor_forces(self) -> torch.Tensor:
+        """[count, S, 6] sensor wrenches: the view's state mirror (omni.physics.tensors hands out
+        its own buffer as well; locomotion.py:89 only reads it before the next step)."""
         v = self._view
-        out = torch.empty((v.count, v.num_sensors, 6), dtype=torch.float32, device=v.device)
-        if v.num_sensors:
-            N.check(N.lib().mi_get_sensor_wrench(v.handle, out.data_ptr(), v.stream()),
-                    "mi_get_sensor_wrench")
-        return out
+        v._refresh_mirror()
+        return v._mir_sens
 
 
 class ArticulationView:
@@ -106,6 +105,21 @@ class ArticulationView:
                                   origins.ctypes.data, int(seed), C.byref(h)), "mi_sim_create")
         self.handle = h.value
         self.env_origins = origins
+        # hot-path bindings (resolved once: the ArticulationView calls are per env-step)
+        self._lib = lib
+        self._dev_index = int(dev_index)
+        self._raw_stream = getattr(torch._C, "_cuda_getCurrentRawStream", None)
+        # state mirrors (include/mi_sim.h mi_sim_set_mirror): the tensors the getters hand out
+        n, D, S = self.count, self.num_dof, self.num_sensors
+        f32 = dict(dtype=torch.float32, device=dev)
+        self._mir_pos, self._mir_rot = torch.zeros((n, 3), **f32), torch.zeros((n, 4), **f32)
+        self._mir_vel = torch.zeros((n, 6), **f32)
+        self._mir_q, self._mir_qd = torch.zeros((n, D), **f32), torch.zeros((n, D), **f32)
+        self._mir_sens = torch.zeros((n, S, 6), **f32)
+        N.check(lib.mi_sim_set_mirror(self.handle, self._mir_pos.data_ptr(), self._mir_rot.data_ptr(),
+                                      self._mir_vel.data_ptr(), self._mir_q.data_ptr(),
+                                      self._mir_qd.data_ptr(),
+                                      self._mir_sens.data_ptr() if S else None), "mi_sim_set_mirror")
 
     def close(self) -> None:
         if self.handle:
@@ -119,6 +133,8 @@ class ArticulationView:
             pass
 
     def stream(self) -> int:
+        if self._raw_stream is not None:
+            return self._raw_stream(self._dev_index)
         return torch.cuda.current_stream(self.device).cuda_stream
 
     # ---- sizes ----
@@ -142,90 +158,107 @@ class ArticulationView:
         return lim.unsqueeze(0).repeat(self.count, 1, 1).to(self.device)
 
     # ---- getters ----
+    # Getters hand out the view's state mirrors (row-major copies the library refreshes in ONE
+    # launch after the state changed, include/mi_sim.h mi_get_state_mirror): with clone=False the
+    # mirror itself, which the next physics step overwrites — Isaac's clone=False returns its
+    # internal buffer the same way (locomotion.py:81-88 reads them before stepping again); with
+    # clone=True (the default) a copy.
     def _empty(self, *shape) -> torch.Tensor:
         return torch.empty(shape, dtype=torch.float32, device=self.device)
 
-    def get_world_poses(self, indices=None, clone: bool = True):
-        pos, rot = self._empty(self.count, 3), self._empty(self.count, 4)
-        N.check(N.lib().mi_get_root_state(self.handle, pos.data_ptr(), rot.data_ptr(), None,
-                                          self.stream()), "mi_get_root_state")
+    def _refresh_mirror(self) -> None:
+        rc = self._lib.mi_get_state_mirror(self.handle, self.stream())
+        if rc:
+            N.check(rc, "mi_get_state_mirror")
+
+    @staticmethod
+    def _out(t: torch.Tensor, indices, clone: bool) -> torch.Tensor:
         if indices is not None:
-            return pos[indices.long()], rot[indices.long()]
-        return pos, rot
+            return t[indices.long()]
+        return t.clone() if clone else t
+
+    def get_world_poses(self, indices=None, clone: bool = True):
+        self._refresh_mirror()
+        return self._out(self._mir_pos, indices, clone), self._out(self._mir_rot, indices, clone)
 
     def get_velocities(self, indices=None, clone: bool = True) -> torch.Tensor:
-        vel = self._empty(self.count, 6)
-        N.check(N.lib().mi_get_root_state(self.handle, None, None, vel.data_ptr(), self.stream()),
-                "mi_get_root_state")
-        return vel if indices is None else vel[indices.long()]
+        self._refresh_mirror()
+        return self._out(self._mir_vel, indices, clone)
 
     def get_joint_positions(self, indices=None, clone: bool = True) -> torch.Tensor:
-        q = self._empty(self.count, self.num_dof)
-        N.check(N.lib().mi_get_dof_state(self.handle, q.data_ptr(), None, self.stream()),
-                "mi_get_dof_state")
-        return q if indices is None else q[indices.long()]
+        self._refresh_mirror()
+        return self._out(self._mir_q, indices, clone)
 
     def get_joint_velocities(self, indices=None, clone: bool = True) -> torch.Tensor:
-        qd = self._empty(self.count, self.num_dof)
-        N.check(N.lib().mi_get_dof_state(self.handle, None, qd.data_ptr(), self.stream()),
-                "mi_get_dof_state")
-        return qd if indices is None else qd[indices.long()]
+        self._refresh_mirror()
+        return self._out(self._mir_qd, indices, clone)
 
     # ---- setters (indices: env ids, rows of the value tensors align with them) ----
     @staticmethod
     def _f32(t: Optional[torch.Tensor]) -> Optional[torch.Tensor]:
-        return None if t is None else t.to(torch.float32).contiguous()
+        if t is None:
+            return None
+        if t.dtype is torch.float32 and t.is_contiguous():
+            return t
+        return t.to(torch.float32).contiguous()
 
-    def _idx64(self, indices) -> (Optional[torch.Tensor], int):
+    def _idx(self, indices, dtype) -> (Optional[torch.Tensor], int):
         if indices is None:
             return None, self.count
-        idx = torch.as_tensor(indices, device=self.device).to(torch.int64).contiguous()
+        if (isinstance(indices, torch.Tensor) and indices.dtype is dtype and indices.device == self.device
+                and indices.is_contiguous()):
+            return indices, indices.numel()
+        idx = torch.as_tensor(indices, device=self.device).to(dtype).contiguous()
         return idx, int(idx.numel())
+
+    def _idx64(self, indices) -> (Optional[torch.Tensor], int):
+        return self._idx(indices, torch.int64)
 
     def set_joint_efforts(self, efforts: torch.Tensor, indices=None) -> None:
         e = self._f32(efforts)
-        if indices is None:
-            idx, n = None, self.count
-        else:
-            idx = torch.as_tensor(indices, device=self.device).to(torch.int32).contiguous()
-            n = int(idx.numel())
-            if n == 0:          # empty index list: nothing to write
-                return
-        N.check(N.lib().mi_set_dof_efforts(self.handle, e.data_ptr(),
-                                           None if idx is None else idx.data_ptr(), n,
-                                           self.stream()), "mi_set_dof_efforts")
+        idx, n = self._idx(indices, torch.int32)
+        if n == 0:              # empty index list: nothing to write
+            return
+        rc = self._lib.mi_set_dof_efforts(self.handle, e.data_ptr(), None if idx is None else idx.data_ptr(),
+                                          n, self.stream())
+        if rc:
+            N.check(rc, "mi_set_dof_efforts")
 
     def set_joint_positions(self, positions: torch.Tensor, indices=None) -> None:
         q = self._f32(positions)
         idx, n = self._idx64(indices)
         if n == 0:              # empty index list: nothing to write
             return
-        N.check(N.lib().mi_set_dof_state(self.handle, q.data_ptr(), None, N.ptr(idx), n,
-                                         self.stream()), "mi_set_dof_state")
+        rc = self._lib.mi_set_dof_state(self.handle, q.data_ptr(), None, N.ptr(idx), n, self.stream())
+        if rc:
+            N.check(rc, "mi_set_dof_state")
 
     def set_joint_velocities(self, velocities: torch.Tensor, indices=None) -> None:
         qd = self._f32(velocities)
         idx, n = self._idx64(indices)
         if n == 0:              # empty index list: nothing to write
             return
-        N.check(N.lib().mi_set_dof_state(self.handle, None, qd.data_ptr(), N.ptr(idx), n,
-                                         self.stream()), "mi_set_dof_state")
+        rc = self._lib.mi_set_dof_state(self.handle, None, qd.data_ptr(), N.ptr(idx), n, self.stream())
+        if rc:
+            N.check(rc, "mi_set_dof_state")
 
     def set_world_poses(self, positions=None, orientations=None, indices=None) -> None:
         p, r = self._f32(positions), self._f32(orientations)
         idx, n = self._idx64(indices)
         if n == 0:              # empty index list: nothing to write
             return
-        N.check(N.lib().mi_set_root_state(self.handle, N.ptr(p), N.ptr(r), None, N.ptr(idx), n,
-                                          self.stream()), "mi_set_root_state")
+        rc = self._lib.mi_set_root_state(self.handle, N.ptr(p), N.ptr(r), None, N.ptr(idx), n, self.stream())
+        if rc:
+            N.check(rc, "mi_set_root_state")
 
     def set_velocities(self, velocities: torch.Tensor, indices=None) -> None:
         v = self._f32(velocities)
         idx, n = self._idx64(indices)
         if n == 0:              # empty index list: nothing to write
             return
-        N.check(N.lib().mi_set_root_state(self.handle, None, None, v.data_ptr(), N.ptr(idx), n,
-                                          self.stream()), "mi_set_root_state")
+        rc = self._lib.mi_set_root_state(self.handle, None, None, v.data_ptr(), N.ptr(idx), n, self.stream())
+        if rc:
+            N.check(rc, "mi_set_root_state")
 
     # ---- physics ----
     def sim_step(self, substeps: int = 1) -> None:

@@ -162,3 +162,69 @@ def test_deferred_substeps_equal_immediate_launches(gpu, name, monkeypatch):
         assert np.array_equal(sa[key], sb[key]), key
     ea.close()
     eb.close()
+
+
+def _direct(view):
+    """The state through the per-call gathers (mi_get_root_state / mi_get_dof_state /
+    mi_get_sensor_wrench), bypassing the view's mirrors."""
+    from omniisaacgymenvs_amd import native as N
+    lib, n, D, S = N.lib(), view.count, view.num_dof, view.num_sensors
+    t = {k: torch.empty(s, device="cuda:0") for k, s in
+         (("pos", (n, 3)), ("rot", (n, 4)), ("vel", (n, 6)), ("q", (n, D)), ("qd", (n, D)), ("sens", (n, S, 6)))}
+    st = view.stream()
+    assert lib.mi_get_root_state(view.handle, t["pos"].data_ptr(), t["rot"].data_ptr(), t["vel"].data_ptr(), st) == 0
+    assert lib.mi_get_dof_state(view.handle, t["q"].data_ptr(), t["qd"].data_ptr(), st) == 0
+    if S:
+        assert lib.mi_get_sensor_wrench(view.handle, t["sens"].data_ptr(), st) == 0
+    torch.cuda.synchronize()
+    return {k: v.cpu().numpy() for k, v in t.items()}
+
+
+def _mirrored(view):
+    p, r = view.get_world_poses(clone=False)
+    out = {"pos": p, "rot": r, "vel": view.get_velocities(clone=False), "q": view.get_joint_positions(clone=False),
+           "qd": view.get_joint_velocities(clone=False), "sens": view._physics_view.get_force_sensor_forces()}
+    torch.cuda.synchronize()
+    return {k: v.cpu().numpy() for k, v in out.items()}
+
+
+@pytest.mark.parametrize("name", ["Humanoid", "Ant", "Cartpole"])
+def test_state_mirrors_track_every_state_write(gpu, name):
+    """The getters' state mirrors (include/mi_sim.h mi_sim_set_mirror / mi_get_state_mirror) equal
+    the per-call gathers bit for bit after every kind of state write: deferred World.step()s,
+    indexed setters (reset_idx's shapes), the fused env step (its mask-driven resets included) and
+    the method-by-method step; clone=False hands out the mirror itself (a view the next step
+    overwrites, as Isaac's clone=False), clone=True a copy."""
+    env = make_env(name, num_envs=NENV, device="cuda:0", seed=12)
+    env.reset()
+    view = env.task.get_robot()
+    D = view.num_dof
+
+    def same():
+        a, b = _mirrored(view), _direct(view)
+        for k in a:
+            assert np.array_equal(a[k], b[k]), k
+
+    same()
+    q0 = view.get_joint_positions(clone=False)
+    qc = view.get_joint_positions()
+    assert view.get_joint_positions(clone=False) is q0 and qc is not q0 and torch.equal(qc, q0)
+    before = qc.clone()
+    view.set_joint_efforts(torch.full((NENV, D), 3.0, device="cuda:0"))
+    env._world.step()
+    env._world.step()
+    same()                                                   # the deferred substeps, then one refresh
+    assert torch.equal(qc, before) and not torch.equal(q0, before)   # the clone kept, the view moved
+    ids = torch.tensor([1, 5, 77], dtype=torch.int64, device="cuda:0")
+    view.set_joint_velocities(torch.full((3, D), 0.25, device="cuda:0"), indices=ids)
+    same()
+    if name != "Cartpole":
+        view.set_velocities(torch.full((3, 6), 0.5, device="cuda:0"), indices=ids)
+        same()
+    g = torch.Generator().manual_seed(2)
+    for fused in (True, False):
+        env.use_fused(fused)
+        for _ in range(3):
+            env.step((torch.rand((NENV, env.num_actions), generator=g) * 2 - 1).cuda())
+            same()
+    env.close()

@@ -111,7 +111,7 @@ def test_library_exports_every_header_symbol():
     for s in syms:
         assert hasattr(lib, s), s
     assert set(syms) == set(N.EXPORTED_SYMBOLS)
-    assert lib.mi_abi_version() == 2
+    assert lib.mi_abi_version() == 3
 
 
 def test_abi_rejects_bad_input_without_touching_a_gpu():
