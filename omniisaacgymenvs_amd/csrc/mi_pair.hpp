@@ -580,6 +580,7 @@ MI_D void pair_artic_substep(const DevModel& m, const WaveTabs& t, const DevStat
         constexpr int NV = TP::nv;
         const int l64 = pair_l64(), me = l64 >> 5;
         const int kc = l64 < NV ? l64 : 0;
+        STAMP(29);
         for (int h = 0; h < 2; ++h) {
             const int nrh = __builtin_amdgcn_readlane(nrows, 32 * h);
             const int nnh = 3 * __builtin_amdgcn_readlane(ncon, 32 * h);
@@ -593,6 +594,7 @@ MI_D void pair_artic_substep(const DevModel& m, const WaveTabs& t, const DevStat
             const float* ush = smh + t.s_us;
             float v = 0.0f;
             sfor<0, NV>([&](auto C) { v += Jr[C] * ush[C]; });
+            STAMP(30);
             float Ar[64];
             sfor<0, 16>([&](auto G) {
                 constexpr int g0 = 4 * G;
@@ -617,6 +619,7 @@ MI_D void pair_artic_substep(const DevModel& m, const WaveTabs& t, const DevStat
                 }
                 Ar[g0] = a0; Ar[g0 + 1] = a1; Ar[g0 + 2] = a2; Ar[g0 + 3] = a3;
             });
+            STAMP(27);
             float b = 0.0f, ia = 0.0f, lam = 0.0f;    // ia 0: a dead row keeps its lambda 0
             int kd = 0;
             if (l64 < nrh) {
@@ -645,6 +648,7 @@ MI_D void pair_artic_substep(const DevModel& m, const WaveTabs& t, const DevStat
                     }
                 });
             }
+            STAMP(28);
             // u = u* + sum_r W_r lambda_r, lane = DOF
             float u = ush[kc];
             sfor<0, 16>([&](auto G) {
@@ -666,6 +670,7 @@ MI_D void pair_artic_substep(const DevModel& m, const WaveTabs& t, const DevStat
             if (l64 < NV) smh[t.s_us + l64] = u;
             if (l64 < nrh) smh[t.s_ad + l64] = lam;            // reuse: lambda of row l64
             wave_sync();
+            STAMP(11);
         }
     } else {
         // fallback (a half with more rows than the Delassus registers hold, 0.4 % of Humanoid

@@ -59,6 +59,8 @@ def main():
     phases[11] = "P10 pgs: u update"
     phases[27] = "P10 pgs: set-up (Delassus rows / W registers)"
     phases[28] = "P10 pgs: sweeps"
+    phases[29] = "P10 wide: entry (P9 tail, syncs)"
+    phases[30] = "P10 wide: J rows + v"
     ph = [k for k in phases if k != 5]
     tot = a[:, ph].sum(axis=1)
     order = np.argsort(tot)
@@ -71,7 +73,8 @@ def main():
            "stats_slow2pct_vs_median_per_substep": {STATS[s]: [round(a[slow, s].mean() / 2, 3), round(a[mid, s].mean() / 2, 3)]
                                                     for s in STATS}}
     top = order[-5:][::-1]
-    out["slowest5"] = [{"cycles": round(tot[w]), "P10": [round(a[w, 27]), round(a[w, 28]), round(a[w, 11])], "rows": a[w, 15] / 2,
+    out["slowest5"] = [{"cycles": round(tot[w]), "P10": [round(a[w, 29]), round(a[w, 30]), round(a[w, 27]), round(a[w, 28]),
+                                                          round(a[w, 11])], "rows": a[w, 15] / 2,
                         "rows>lam": a[w, 19] / 2, "contacts": a[w, 20] / 2} for w in top]
     print(json.dumps(out), flush=True)
 
