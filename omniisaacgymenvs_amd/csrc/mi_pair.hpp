@@ -26,6 +26,18 @@ MI_D float pbc(float v, int k) {
     const float a = readlane(v, k), b = readlane(v, k + 32);
     return (pair_l64() & 32) ? b : a;
 }
+// the same for a compile-time k, without SGPRs: row_newbcast:(k % 16) (DPP, gfx90a+) gives every
+// 16-lane row the value of its own lane k % 16; v_permlane16_swap (gfx950) of that register with
+// itself then spreads the even rows (k < 16: rows 0 and 2 hold lanes k and 32 + k) or the odd
+// rows (k >= 16) over their 32-lane half. Two VALU ops instead of two v_readlane, two v_mov and
+// a v_cndmask; exact (a broadcast)
+template <int K>
+MI_D float pbcc(float v) {
+    static_assert(K >= 0 && K < 32, "lane of the half");
+    const int t = __builtin_amdgcn_mov_dpp(__float_as_int(v), 0x150 + (K & 15), 0xF, 0xF, false);
+    const auto r = __builtin_amdgcn_permlane16_swap(t, t, false, false);
+    return __int_as_float((int)(K < 16 ? r[0] : r[1]));
+}
 MI_D int pbci(int v, int k) {
     const int a = __builtin_amdgcn_readlane(v, k), b = __builtin_amdgcn_readlane(v, k + 32);
     return (pair_l64() & 32) ? b : a;
@@ -48,10 +60,10 @@ MI_D void ct_ltdl_pair(int lane, float (&Mc)[T::nvc]) {
         constexpr int k = K;
         __builtin_amdgcn_sched_barrier(0);
         const int ln = lane_here(lane);
-        const float inv = __builtin_amdgcn_rcpf(pbc(Mc[k], k));
+        const float inv = __builtin_amdgcn_rcpf(pbcc<k>(Mc[k]));
         sfor<T::dof.anc_start[k], T::dof.anc_start[k + 1]>([&](auto A) {
             constexpr int ii = T::dof.anc[A];
-            const float s = pbc(Mc[k], ii) * inv;
+            const float s = pbcc<ii>(Mc[k]) * inv;
             if (ln <= ii) Mc[ii] -= s * Mc[k];
         });
         if (ln < k) Mc[k] = Mc[k] * inv;
@@ -545,7 +557,7 @@ MI_D void pair_artic_substep(const DevModel& m, const WaveTabs& t, const DevStat
                     // one med3: max(., lo) then, for friction, min(., lim) (lo <= hi: lamn >= 0)
                     const float mine = __builtin_amdgcn_fmed3f(l0 + (b - v) * ia, fric ? -lim : 0.0f,
                                                                fric ? lim : __builtin_huge_valf());
-                    const float ln = pbc(mine, rr);
+                    const float ln = pbcc<rr>(mine);
                     if constexpr (rr % 3 == 0) lamn = rr < nnorm ? ln : lamn;
                     v += Ar[rr] * (ln - l0);
                     lamv[rr] = ln;

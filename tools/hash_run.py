@@ -1,0 +1,33 @@
+#!/usr/bin/env python3
+"""Bit-exactness check between two builds of libmi_sim.so: 40 fused env steps of Humanoid and
+Ant (4096 envs, fixed seeds and actions), SHA-256 of every returned obs / reward tensor. Run once
+per build (MI_SIM_LIB=<path> selects the library) and compare the printed HASH lines; a change
+that only moves data (e.g. a different cross-lane broadcast) must leave the hash unchanged.
+
+usage: [MI_SIM_LIB=...] python tools/hash_run.py"""
+import hashlib
+import os
+import sys
+
+import torch
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+from omniisaacgymenvs_amd.utils.task_util import make_env  # noqa: E402
+
+
+def main():
+    h = hashlib.sha256()
+    for task in ("Humanoid", "Ant"):
+        env = make_env(task, num_envs=4096, device="cuda:0", seed=3)
+        env.reset()
+        g = torch.Generator(device="cuda:0").manual_seed(0)
+        for _ in range(40):
+            o, r, _, _ = env.step(torch.rand((4096, env.num_actions), device="cuda:0", generator=g) * 2 - 1)
+            h.update(o["obs"].cpu().numpy().tobytes())
+            h.update(r.cpu().numpy().tobytes())
+        env.close()
+    print("HASH", h.hexdigest(), flush=True)
+
+
+if __name__ == "__main__":
+    main()
