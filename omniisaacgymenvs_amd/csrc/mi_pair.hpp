@@ -18,6 +18,22 @@
 #pragma once
 #include "mi_wave.hpp"
 
+// Issue priority by contact load: the launch lasts as long as its slowest waves, and those are
+// the contact-heavy envs (constraint rows grow every later phase: P9 solves and filing, the PGS
+// width, the sensor sums). Once a half of the wave has more than MI_PRIO_C1 / C2 / C3 contact rows
+// in a substep, the wave takes its SIMD's issue slots ahead of a lighter partner at priority
+// 1 / 2 / 3 for the rest of its life (never lowered: `prio` carries across substeps). The light
+// partner has slack: it finishes early anyway. Priority moves the schedule, never a result.
+#ifndef MI_PRIO_C1
+#define MI_PRIO_C1 12
+#endif
+#ifndef MI_PRIO_C2
+#define MI_PRIO_C2 18
+#endif
+#ifndef MI_PRIO_C3
+#define MI_PRIO_C3 27
+#endif
+
 namespace mi {
 
 MI_D int pair_l64() { return (int)(threadIdx.x & 63u); }
@@ -116,7 +132,7 @@ MI_D const float* pair_wrow(const WaveTabs& t, const float* sm, const float* gW,
 template <class TP>
 MI_D void pair_artic_substep(const DevModel& m, const WaveTabs& t, const DevState& st,
                              const SimP& p, int i, const float* mcb, float* sm, float* gW,
-                             bool load_state, bool store_state) {
+                             bool load_state, bool store_state, int& prio) {
     static_assert(TP::kCT && TP::nv <= 32, "paired kernel: compiled topology, nv <= 32");
     const int lane = pair_l64() & 31;
     const int N = st.N, L = m.L, D = m.D, nv = m.nv, nr = m.nr;
@@ -360,6 +376,12 @@ MI_D void pair_artic_substep(const DevModel& m, const WaveTabs& t, const DevStat
         }
     }
     const int nc = 3 * ncon;
+    {
+        const int cr = pmax(nc);                              // uniform
+        if (cr > MI_PRIO_C3 && prio < 3) { __builtin_amdgcn_s_setprio(3); prio = 3; }
+        else if (cr > MI_PRIO_C2 && prio < 2) { __builtin_amdgcn_s_setprio(2); prio = 2; }
+        else if (cr > MI_PRIO_C1 && prio < 1) { __builtin_amdgcn_s_setprio(1); prio = 1; }
+    }
     wave_sync();
     STAMP(6);
     // ---- P7+P9: one batch per half, lanes over solve vectors (rhs, limit candidates, contact

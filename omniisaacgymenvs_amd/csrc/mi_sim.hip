@@ -762,9 +762,10 @@ __global__ __launch_bounds__(512) MI_PAIR_OCC void k_sim_step_pair(const KParams
     if (!pair_live(kp->st.N)) return;
     float* gW = kp->rows + (size_t)i * t.g_row_stride;
     float* sm = pair_env_lds(t, smem);
+    int prio = 0;                          // issue priority so far (mi_pair.hpp MI_PRIO_C*)
     for (int s = 0; s < substeps; ++s) {
         const KParams* k = opaque_kp(kp);
-        pair_artic_substep<T>(k->m, k->t, k->st, k->p, i, smem, sm, gW, s == 0, s == substeps - 1);
+        pair_artic_substep<T>(k->m, k->t, k->st, k->p, i, smem, sm, gW, s == 0, s == substeps - 1, prio);
     }
 }
 
@@ -791,9 +792,10 @@ __global__ __launch_bounds__(512) MI_PAIR_OCC void k_env_step_pair(const KParams
     STAMP(13);
     float* gW = kp->rows + (size_t)i * t.g_row_stride;
     float* sm = pair_env_lds(t, smem);
+    int prio = 0;                          // issue priority so far (mi_pair.hpp MI_PRIO_C*)
     for (int s = 0; s < substeps; ++s) {
         const KParams* k = opaque_kp(kp);
-        pair_artic_substep<T>(k->m, k->t, k->st, k->p, i, smem, sm, gW, s == 0, s == substeps - 1);
+        pair_artic_substep<T>(k->m, k->t, k->st, k->p, i, smem, sm, gW, s == 0, s == substeps - 1, prio);
     }
     STAMP_RESET();
     pair_loco_post(m, t, st, tp, i, sm, a_lane, obs_out, obs_task, rew, reset_buf, progress_buf,
