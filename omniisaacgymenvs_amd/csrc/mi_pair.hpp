@@ -24,6 +24,9 @@
 // in a substep, the wave takes its SIMD's issue slots ahead of a lighter partner at priority
 // 1 / 2 / 3 for the rest of its life (never lowered: `prio` carries across substeps). The light
 // partner has slack: it finishes early anyway. Priority moves the schedule, never a result.
+#ifndef MI_PAIR_SOLVE_PD
+#define MI_PAIR_SOLVE_PD 3   // factor-entry prefetch depth of the P9 solves (ct_solve_l)
+#endif
 #ifndef MI_PRIO_C1
 #define MI_PRIO_C1 12
 #endif
@@ -486,7 +489,7 @@ MI_D void pair_artic_substep(const DevModel& m, const WaveTabs& t, const DevStat
         });
         STAMP(7);
         float a;
-        ct_solve_l<TP>(sm + t.s_L, x, a);
+        ct_solve_l<TP, MI_PAIR_SOLVE_PD>(sm + t.s_L, x, a);
         STAMP(8);
         if (base == 0) limit_rows(x);
         STAMP(9);
