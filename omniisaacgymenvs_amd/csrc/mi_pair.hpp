@@ -89,6 +89,31 @@ MI_D void ct_ltdl_pair(int lane, float (&Mc)[T::nvc]) {
     });
 }
 
+// Per-DOF loop over the motion subspaces S_c (6 floats per DOF in LDS, uniform per half) and,
+// with R, the rhs entries R[c]: fn(c, S_c, R[c]) with the loads of DOF c + SP issued before DOF c's
+// arithmetic, into a ring of SP + 1 buffers indexed at compile time. Each DOF's arithmetic is a
+// handful of VALU ops, so with the loads in line every DOF exposed a full LDS round trip.
+template <class TP, int SP, bool WITH_R, class F>
+MI_D void sdof_loop(const float* Ss, const float* R, F&& fn) {
+    constexpr int NB = SP + 1;
+    float sb[NB][6], rb[NB];
+    auto load = [&](auto C) {
+        constexpr int c = C;
+#pragma unroll
+        for (int q = 0; q < 6; ++q) sb[c % NB][q] = Ss[6 * c + q];
+        if constexpr (WITH_R) rb[c % NB] = R[c];
+    };
+    sfor<0, (SP < TP::nv ? SP : TP::nv)>([&](auto C) { load(C); });
+    sfor<0, TP::nv>([&](auto C) {
+        constexpr int c = C;
+        if constexpr (c + SP < TP::nv) load(std::integral_constant<int, c + SP>{});
+        fn(C, sb[c % NB], WITH_R ? rb[c % NB] : 0.0f);
+    });
+}
+#ifndef MI_PAIR_SDOF_PD
+#define MI_PAIR_SDOF_PD 3   // DOF-loop prefetch depth (sdof_loop)
+#endif
+
 // J_r[c] of this lane's constraint row r (contact or limit), for every DOF c (lane = row)
 template <class TP>
 MI_D void pair_jrow(const MC& mc, const WaveTabs& t, const float* sm, int r, int nr,
@@ -108,11 +133,8 @@ MI_D void pair_jrow(const MC& mc, const WaveTabs& t, const float* sm, int r, int
         sg = sm[t.s_lsg + kdof - nr];
     }
     const float* Ss = sm + t.s_S;
-    sfor<0, TP::nv>([&](auto C) {
+    sdof_loop<TP, MI_PAIR_SDOF_PD, false>(Ss, nullptr, [&](auto C, const float (&sv)[6], float) {
         constexpr int c = C;
-        float sv[6];
-#pragma unroll
-        for (int q = 0; q < 6; ++q) sv[q] = Ss[6 * c + q];
         const float v = dot6(sv, f);
         const bool ia = (msk >> c) & 1u, ib = (msk2 >> c) & 1u;
         float xc = (ia ? v : 0.0f) - (ib ? v : 0.0f);
@@ -475,15 +497,12 @@ MI_D void pair_artic_substep(const DevModel& m, const WaveTabs& t, const DevStat
             msk2 = l2 >= 0.0f ? mc.mask((int)l2) : 0u;
             contact_row_f<TP::kSelf>(sm, t, r, f);
         }
-        sfor<0, TP::nv>([&](auto C) {
+        sdof_loop<TP, MI_PAIR_SDOF_PD, true>(Ss, rhs, [&](auto C, const float (&sv)[6], float rcl) {
             constexpr int c = C;
-            float sv[6];
-#pragma unroll
-            for (int q = 0; q < 6; ++q) sv[q] = Ss[6 * c + q];
             const float v = dot6(sv, f);
             const bool ia = (msk >> c) & 1u, ib = (msk2 >> c) & 1u;
             float xc = (ia ? v : 0.0f) - (ib ? v : 0.0f);
-            float rc = rhs[c];
+            float rc = rcl;
             asm volatile("" : "+v"(xc), "+v"(rc));
             x[c] = crow ? xc : (bv == 0 ? rc : (kd == c ? 1.0f : 0.0f));
         });
