@@ -234,11 +234,8 @@ MI_D void pair_artic_substep(const DevModel& m, const WaveTabs& t, const DevStat
             r += st.eff[sx(st, k - nr, i)] - damp * us[k];
         }
         rhs[k] = r;
-        sfor<0, TP::nv>([&](auto J) {
+        sdof_loop<TP, MI_PAIR_SDOF_PD, false>(Ss, nullptr, [&](auto J, const float (&sj)[6], float) {
             constexpr int j = J;
-            float sj[6];
-#pragma unroll
-            for (int c = 0; c < 6; ++c) sj[c] = Ss[6 * j + c];
             Mx[k * nv + j] = dot6(sj, f);
         });
         Mx[k * nv + k] = diag;
@@ -551,11 +548,22 @@ MI_D void pair_artic_substep(const DevModel& m, const WaveTabs& t, const DevStat
             float a0 = 0.0f, a1 = 0.0f, a2 = 0.0f, a3 = 0.0f;
             if (g0 < nrows_max) {
                 auto dots = [&](auto w0, auto w1, auto w2, auto w3) {
+                    // W entries of DOF C + MI_PAIR_SDOF_PD loaded before DOF C's FMAs (a ring
+                    // indexed at compile time; see sdof_loop)
+                    constexpr int PD = MI_PAIR_SDOF_PD, NB = PD + 1;
+                    float wb[NB][4];
+                    auto ld = [&](auto C) {
+                        constexpr int c = C;
+                        wb[c % NB][0] = w0[c]; wb[c % NB][1] = w1[c]; wb[c % NB][2] = w2[c]; wb[c % NB][3] = w3[c];
+                    };
+                    sfor<0, (PD < NV ? PD : NV)>([&](auto C) { ld(C); });
                     sfor<0, NV>([&](auto C) {
-                        a0 += Jr[C] * w0[C];
-                        a1 += Jr[C] * w1[C];
-                        a2 += Jr[C] * w2[C];
-                        a3 += Jr[C] * w3[C];
+                        constexpr int c = C;
+                        if constexpr (c + PD < NV) ld(std::integral_constant<int, c + PD>{});
+                        a0 += Jr[C] * wb[c % NB][0];
+                        a1 += Jr[C] * wb[c % NB][1];
+                        a2 += Jr[C] * wb[c % NB][2];
+                        a3 += Jr[C] * wb[c % NB][3];
                     });
                 };
                 if (g0 + 3 < t.w_rows_lds) {   // uniform: all four rows in LDS (ds_read)
@@ -657,11 +665,20 @@ MI_D void pair_artic_substep(const DevModel& m, const WaveTabs& t, const DevStat
                 float a0 = 0.0f, a1 = 0.0f, a2 = 0.0f, a3 = 0.0f;
                 if (g0 < nrh) {
                     auto dots = [&](auto w0, auto w1, auto w2, auto w3) {
+                        constexpr int PD = MI_PAIR_SDOF_PD, NB = PD + 1;   // prefetch ring, as above
+                        float wb[NB][4];
+                        auto ld = [&](auto C) {
+                            constexpr int c = C;
+                            wb[c % NB][0] = w0[c]; wb[c % NB][1] = w1[c]; wb[c % NB][2] = w2[c]; wb[c % NB][3] = w3[c];
+                        };
+                        sfor<0, (PD < NV ? PD : NV)>([&](auto C) { ld(C); });
                         sfor<0, NV>([&](auto C) {
-                            a0 += Jr[C] * w0[C];
-                            a1 += Jr[C] * w1[C];
-                            a2 += Jr[C] * w2[C];
-                            a3 += Jr[C] * w3[C];
+                            constexpr int c = C;
+                            if constexpr (c + PD < NV) ld(std::integral_constant<int, c + PD>{});
+                            a0 += Jr[C] * wb[c % NB][0];
+                            a1 += Jr[C] * wb[c % NB][1];
+                            a2 += Jr[C] * wb[c % NB][2];
+                            a3 += Jr[C] * wb[c % NB][3];
                         });
                     };
                     if (g0 + 3 < t.w_rows_lds) {
