@@ -110,6 +110,9 @@ MI_D void sdof_loop(const float* Ss, const float* R, F&& fn) {
         fn(C, sb[c % NB], WITH_R ? rb[c % NB] : 0.0f);
     });
 }
+#ifndef MI_PAIR_WIDE_PD
+#define MI_PAIR_WIDE_PD 4   // W-row prefetch depth of the wide Delassus set-up (1-4 all spill: see DESIGN)
+#endif
 #ifndef MI_PAIR_SDOF_PD
 #define MI_PAIR_SDOF_PD 4   // DOF-loop prefetch depth (sdof_loop): 2 -> 0.1609 ms, 4 -> 0.1592 (A/B)
 #endif
@@ -665,7 +668,7 @@ MI_D void pair_artic_substep(const DevModel& m, const WaveTabs& t, const DevStat
                 float a0 = 0.0f, a1 = 0.0f, a2 = 0.0f, a3 = 0.0f;
                 if (g0 < nrh) {
                     auto dots = [&](auto w0, auto w1, auto w2, auto w3) {
-                        constexpr int PD = MI_PAIR_SDOF_PD, NB = PD + 1;   // prefetch ring, as above
+                        constexpr int PD = MI_PAIR_WIDE_PD, NB = PD + 1;   // prefetch ring, as above
                         float wb[NB][4];
                         auto ld = [&](auto C) {
                             constexpr int c = C;
