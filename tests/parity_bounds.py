@@ -1,0 +1,113 @@
+"""Per-env bounds of the one-step device-vs-oracle parity checks (tests/test_gpu_parity.py,
+test_golden.py, test_gpu_fullsize.py; tools/parity_stats.py reports the same quantities).
+
+After ONE fused env step from identical state, every obs entry and the reward of every env away
+from a contact / limit decision threshold must be within a per-task, per-field-group bound
+(FAR_TOL: ~4x the largest such error measured over 4 steps x 4096 envs at HEAD,
+profiles/r04/parity_stats_<task>.log). Two allowances may widen it, both computed on the ORACLE
+side, never from the device's own error:
+  * conditioning: SENS_K x the oracle's response to a 2-ulp perturbation of its own input
+    state (tests/helpers.py oracle_sensitivity) — stacked contacts and near-singular Delassus
+    blocks amplify rounding. Capped at SENS_CAP, and fewer than WIDEN_MAX_FRAC of the envs of a
+    step may NEED it (error above the base bound); the widest bound applied is reported;
+  * the reward carries potentials - prev_potentials with |potentials| ~ 6e4 in float32
+    (locomotion.py:223, dt = 1/60): 2 ulp of the potentials is the reward's own quantisation
+    (bounded by construction: <= 2 ulp of 1e3 / dt).
+Envs whose closest decision is within DECISION_EPS of its threshold may take the other discrete
+branch (any error), but must stay under 2 %. Pure numpy: CPU-testable (tests/test_parity_bounds.py).
+"""
+from __future__ import annotations
+
+from typing import Dict, Optional
+
+import numpy as np
+
+DECISION_EPS = 1e-4          # m or rad: a decision this close to its threshold may flip
+NEAR_MAX_FRAC = 0.02         # envs at a threshold that may differ
+SENS_K = 4.0                 # conditioning allowance: this many times the oracle's 2-ulp response
+SENS_CAP = 1e-2              # ... never above this
+WIDEN_MAX_FRAC = 0.01        # envs per step that may need the conditioning allowance
+CARTPOLE_TOL = 1e-4
+
+# base per-env bound, away from thresholds (see the module docstring for how they were set)
+FAR_TOL = {
+    "Humanoid": {"root": 1e-3, "dof_pos": 4e-4, "dof_vel": 2e-3, "sensors": 2e-3, "actions": 0.0,
+                 "rew": 2e-3},
+    "Ant": {"root": 1e-4, "dof_pos": 1e-5, "dof_vel": 2e-4, "sensors": 4e-4, "actions": 0.0,
+            "rew": 1e-5},
+}
+FAR_TOL["AntSelf"] = FAR_TOL["Humanoid"]   # Ant with self-collision pairs (runtime tables)
+
+# regression detectors: median / 99th percentile of each group's per-env error
+GROUP_TOL = {
+    "Humanoid": {"root": (2e-5, 1e-4), "dof_pos": (1e-5, 5e-5), "dof_vel": (5e-5, 4e-4),
+                 "sensors": (5e-5, 3e-3), "actions": (0.0, 0.0), "rew": (2e-6, 5e-5)},
+    "Ant": {"root": (5e-6, 4e-5), "dof_pos": (1e-6, 3e-6), "dof_vel": (3e-6, 4e-5),
+            "sensors": (1e-5, 1.5e-4), "actions": (0.0, 0.0), "rew": (1e-6, 2e-6)},
+}
+GROUP_TOL["AntSelf"] = GROUP_TOL["Humanoid"]
+
+
+def group_slices(num_dof: int, num_sensors: int) -> Dict[str, slice]:
+    D, S = num_dof, num_sensors
+    return {"root": slice(0, 12), "dof_pos": slice(12, 12 + D), "dof_vel": slice(12 + D, 12 + 2 * D),
+            "sensors": slice(12 + 2 * D, 12 + 2 * D + 6 * S), "actions": slice(12 + 2 * D + 6 * S, None)}
+
+
+def evaluate(name: str, groups: Dict[str, slice], obs, rew, obs_ref, rew_ref, margin,
+             sens: Optional[np.ndarray] = None, pot: Optional[np.ndarray] = None) -> dict:
+    """Per-env errors and bounds of one step; no assertion (check() asserts, the stats tool
+    reports). Returns the per-group errors, the base and applied bounds, which envs are near a
+    threshold, which needed the conditioning allowance and the widest bound applied."""
+    n = len(rew)
+    near = np.asarray(margin) < DECISION_EPS
+    widen = np.zeros(n) if sens is None else np.minimum(SENS_K * np.asarray(sens, np.float64), SENS_CAP)
+    err = {g: np.abs(obs[:, sl] - obs_ref[:, sl]).max(axis=1) for g, sl in groups.items()}
+    err["rew"] = np.abs(np.asarray(rew, np.float64) - np.asarray(rew_ref, np.float64))
+    out = {"err": err, "near": near, "base": {}, "bound": {}, "over": {}, "needed_widening": {}}
+    pot_allow = None
+    if pot is not None:
+        pot_allow = 2.0 * np.spacing(np.asarray(pot, np.float32)).astype(np.float64)
+    any_needed = np.zeros(n, bool)
+    widest = 0.0
+    for g, e in err.items():
+        base = np.full(n, FAR_TOL[name][g])
+        if g == "rew" and pot_allow is not None:
+            base = np.maximum(base, pot_allow)
+        bound = np.maximum(base, widen)
+        needed = (e > base) & (e <= bound) & ~near
+        over = (e > bound) & ~near
+        out["base"][g], out["bound"][g] = base, bound
+        out["over"][g], out["needed_widening"][g] = over, needed
+        any_needed |= needed
+        if needed.any():
+            widest = max(widest, float(bound[needed].max()))
+    out["any_needed"] = any_needed
+    out["widest_applied"] = widest
+    out["near_differ"] = near & np.any(np.stack([e > out["bound"][g] for g, e in err.items()]), axis=0)
+    return out
+
+
+def check(name: str, groups: Dict[str, slice], obs, rew, obs_ref, rew_ref, margin,
+          sens=None, pot=None, quantiles: bool = True, log=print) -> dict:
+    """Assert the one-step parity of a locomotion task (see the module docstring); prints the
+    number of envs that needed the conditioning allowance and the widest bound applied."""
+    r = evaluate(name, groups, obs, rew, obs_ref, rew_ref, margin, sens, pot)
+    n = len(rew)
+    for g, e in r["err"].items():
+        if quantiles:
+            q50, q99 = GROUP_TOL[name][g]
+            assert np.quantile(e, 0.5) <= q50, f"{name} {g}: median error {np.quantile(e, 0.5):.3g} > {q50}"
+            assert np.quantile(e, 0.99) <= q99, f"{name} {g}: q99 error {np.quantile(e, 0.99):.3g} > {q99}"
+        bad = r["over"][g]
+        assert not bad.any(), (
+            f"{name} {g}: env {np.nonzero(bad)[0][0]} error {e[bad][0]:.3g} > {r['bound'][g][bad][0]:.3g} "
+            f"(base {r['base'][g][bad][0]:.3g})")
+    k = int(r["any_needed"].sum())
+    if log is not None:
+        log(f"[parity] {name}: {n} envs, {k} needed the conditioning allowance, widest bound applied "
+            f"{r['widest_applied']:.3g}, {int(r['near'].sum())} at a threshold "
+            f"({int(r['near_differ'].sum())} differ)")
+    assert k < max(1.0, WIDEN_MAX_FRAC * n), f"{name}: {k} of {n} envs needed the conditioning allowance"
+    assert r["near_differ"].mean() < NEAR_MAX_FRAC, f"{name}: {int(r['near_differ'].sum())} envs at a threshold differ"
+    return r

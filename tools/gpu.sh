@@ -20,6 +20,7 @@
 #   stamps       phase stamps (per-phase s_memtime accumulators)          -> stamps_<task>.log
 #   patha        INTEGRATION path (A): reference call sequence over ArticulationView -> path_a_humanoid.json
 #   train        PPO frames/s (tools/bench_train.py)                       -> bench_train_*.log
+#   curve        reference training schedule, per-epoch curve (tools/train_curve.py) -> train_curve_*.jsonl
 #   sizes        env-count sweep of the fused step (tools/bw_sweep.py)     -> bw_sweep_*.json
 #   ab           bench A/B: default library vs LIB_B (alternating passes)  -> DESIGN perf log
 # Environment knobs: TASK (Humanoid), NS (env counts), BARGS (extra bench.py args), TAG (log suffix).
@@ -89,6 +90,8 @@ recipe() {
     run path_a 200 python -u tools/path_a_timing.py ;;
   train)
     for T in ${TASKS:-Humanoid}; do run train_${T}_$TAG 600 python -u tools/bench_train.py --task $T; done ;;
+  curve)
+    for T in ${TASKS:-Ant Humanoid}; do run curve_${T}_$TAG 900 python -u tools/train_curve.py --task $T ${CARGS:-}; done ;;
   sizes)
     run sizes_${TASK}_$TAG 300 python -u tools/bw_sweep.py $TASK ${NS// /,} ;;
   ab)   # A/B of the default library against LIB_B (another build of libmi_sim.so), alternating
