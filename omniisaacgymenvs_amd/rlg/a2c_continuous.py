@@ -48,7 +48,7 @@ import torch.distributed as dist
 import torch.nn as nn
 
 from . import ops
-from .models import ModelA2CContinuousLogStd
+from .models import ModelA2CContinuousLogStd, RunningMeanStd
 
 
 def _f(x) -> float:
@@ -147,20 +147,30 @@ class A2CAgent:
         self.actions_high = torch.as_tensor(np.asarray(info["action_space"].high, np.float32), device=self.device)
         self.num_actors = int(cfg["num_actors"])
         self.horizon = int(cfg["horizon_length"])
-        # multi-GPU (multi_gpu: True under torch.distributed.run): one process per
-        # GPU steps its env shard with a policy replica; every horizon is gathered to the learner
-        # (rank 0) in ONE collective (utils.distributed.RolloutGather), the learner trains on all
-        # ranks' actors and broadcasts the weights back. (rl_games' multi_gpu runs a learner per
-        # rank and averages gradients instead; here each rollout crosses xGMI once and there is
-        # one optimizer.) num_actors stays the per-rank count, batch_size is the learner's.
+        # multi-GPU (multi_gpu: True under torch.distributed.run), one process per
+        # GPU stepping its env shard; two learner modes (`multi_gpu_mode`):
+        #  * "data_parallel" (default; rl_games' multi_gpu): every rank runs GAE and the PPO
+        #    epochs on its own shard (num_actors and minibatch_size per rank); per minibatch the
+        #    gradients and the policy KL are averaged over the ranks in ONE all-reduce (RCCL)
+        #    before the optimizer step, so every replica takes the same step with the same
+        #    adaptive LR; the obs / value normalisation statistics merge the ranks' batch moments
+        #    (all-reduce), so replicas stay identical; weights broadcast once at start;
+        #  * "central": every horizon is gathered to the learner (rank 0) in ONE collective
+        #    (utils.distributed.RolloutGather), the learner trains on all ranks' actors (world x
+        #    the batch, world x the minibatches) and broadcasts the weights back.
         # `distributed` also holds at world size 1 under an initialised process group (the
-        # single-GPU rehearsal of config 5's gather / broadcast path, tests/test_gpu_nccl.py)
+        # single-GPU rehearsal of config 5's collectives, tests/test_gpu_nccl.py)
         self.distributed = (bool(cfg.get("multi_gpu", False)) and dist.is_available()
                             and dist.is_initialized())
         self.world = dist.get_world_size() if self.distributed else 1
         self.rank = dist.get_rank() if self.distributed else 0
-        self.is_learner = self.rank == 0
-        self.batch_size = self.horizon * self.num_actors * self.world
+        mode = str(cfg.get("multi_gpu_mode", "data_parallel"))
+        if mode not in ("data_parallel", "central"):
+            raise ValueError(f"multi_gpu_mode must be 'data_parallel' or 'central', got {mode!r}")
+        self.dp = self.distributed and mode == "data_parallel"
+        self.central = self.distributed and mode == "central"
+        self.is_learner = self.rank == 0 or not self.central
+        self.batch_size = self.horizon * self.num_actors * (self.world if self.central else 1)
         self.minibatch_size = int(cfg["minibatch_size"])
         if self.batch_size % self.minibatch_size != 0:
             raise ValueError(f"minibatch_size {self.minibatch_size} must divide horizon x actors = "
@@ -197,6 +207,10 @@ class A2CAgent:
             _use_shipped_gemm_tunings()
         self.model = ModelA2CContinuousLogStd(self.num_obs, self.num_actions, params["network"],
                                               self.normalize_input, self.normalize_value).to(self.device)
+        if self.dp:   # merged batch moments over the ranks (replicas keep identical statistics)
+            for m in self.model.modules():
+                if isinstance(m, RunningMeanStd):
+                    m.all_reduce = True
         wd = float(cfg.get("weight_decay", 0.0))
         if self.device.type == "cuda":
             # LR lives on the device and the legacy adaptive schedule updates it there (no
@@ -224,7 +238,7 @@ class A2CAgent:
         H, N, O, A = self.horizon, self.num_actors, self.num_obs, self.num_actions
         dev, f32 = self.device, torch.float32
         self.rollout = None
-        if self.distributed:
+        if self.central:
             # the rollout buffers ARE the gather slab's fields (zero copy; one slab, so the
             # captured rollout graph keeps writing the same addresses)
             from ..utils.distributed import RolloutGather
@@ -260,6 +274,11 @@ class A2CAgent:
         # minibatch updates: one captured graph per (obs-statistics mode, minibatch index)
         self.graph_update = self.device.type == "cuda" and bool(cfg.get("graph_update", True))
         self.upd_graphs: Dict = {}
+        # data-parallel: gradients (+ the policy KL) of a minibatch in one flat buffer, averaged
+        # over the ranks by one all-reduce between the two captured halves of the update
+        self._params = [p for p in self.model.parameters()]
+        self._flat = (torch.zeros(sum(p.numel() for p in self._params) + 1, device=dev, dtype=f32)
+                      if self.dp else None)
         self._data: Optional[Dict[str, torch.Tensor]] = None
         self._mb_out = torch.zeros((self.num_minibatches, 5), device=dev, dtype=f32)
         self._mb_stats = torch.zeros((self.mini_epochs, self.num_minibatches, 5), device=dev, dtype=f32)
@@ -376,7 +395,9 @@ class A2CAgent:
                 self.graph.replay()
             else:
                 self._rollout_body()
-        self._global = self._gather_horizon() if self.distributed else None
+        self._global = self._gather_horizon() if self.central else None
+        if self.dp:                                     # global episode statistics in the logs
+            dist.all_reduce(self.episode_sums)
         ep = self.episode_sums.cpu().numpy()           # the rollout's one host sync
         for cnt, rsum, lsum in ep:
             if cnt > 0:
@@ -400,7 +421,7 @@ class A2CAgent:
     # ------------------------------------------------------------------ training
     def prepare_dataset(self) -> Dict[str, torch.Tensor]:
         b, last_values, dones = self.buf, self.last_values, self.dones
-        if self.distributed:             # the learner: every rank's actors, gathered
+        if self.central:                 # the learner: every rank's actors, gathered
             b, last_values, dones = self._global
         adv, ret = ops.gae(b["rewards"], b["values"], b["dones"], last_values, dones,
                            self.gamma, self.tau)
@@ -439,30 +460,75 @@ class A2CAgent:
     def _minibatch_device(self, i: int) -> None:
         """One minibatch update on the device, without host syncs (graph-capturable): PPO loss,
         backward, GradScaler + fused Adam, mu / sigma write-back, adaptive LR, stats row i."""
+        self._mb_grad(i)
+        self._mb_apply(i)
+
+    def _mb_grad(self, i: int) -> None:
+        """First half of a minibatch update: PPO loss and gradients (p.grad), mu / sigma
+        write-back; data-parallel: gradients and KL packed into the flat all-reduce buffer."""
         s, e = i * self.minibatch_size, (i + 1) * self.minibatch_size
         data = self._data
         mb = {k: v[s:e] for k, v in data.items()}
         if self.fused_loss:        # mu / sigma written back by the loss kernel itself
-            a_loss, c_loss, ent, kl, b_loss = self._calc_gradients_fused(mb)
+            a_loss, c_loss, ent, kl, b_loss = self._calc_gradients_fused(mb, step=False)
         else:
-            a_loss, c_loss, ent, kl, cmu, csigma, b_loss = self.calc_gradients(mb)
+            a_loss, c_loss, ent, kl, cmu, csigma, b_loss = self.calc_gradients(mb, step=False)
             data["mu"][s:e].copy_(cmu)
             data["sigma"][s:e].copy_(csigma)
-        if self.scheduler is not None:
-            self._lr_update_device(kl)
         self._mb_out[i].copy_(torch.stack([a_loss.float(), c_loss.float(), ent.float(), kl.float(),
                                            b_loss.float()]))
+        if self.dp:
+            torch.cat([p.grad.reshape(-1) for p in self._params] + [self._mb_out[i, 3:4]], out=self._flat)
+
+    def _mb_apply(self, i: int) -> None:
+        """Second half: (data-parallel: the all-reduced flat buffer / world back into p.grad and
+        the KL) GradScaler + Adam step, adaptive LR on the (averaged) KL."""
+        if self.dp:
+            self._flat.mul_(1.0 / self.world)
+            o = 0
+            views = []
+            for p in self._params:
+                views.append(self._flat[o:o + p.numel()].view_as(p))
+                o += p.numel()
+            torch._foreach_copy_([p.grad for p in self._params], views)
+            self._mb_out[i, 3].copy_(self._flat[o])
+        self._optimizer_step()
+        if self.scheduler is not None:
+            self._lr_update_device(self._mb_out[i, 3])
+
+    def _allreduce_flat(self) -> None:
+        dist.all_reduce(self._flat)
 
     def _minibatch_graphed(self, mode: int, i: int) -> None:
+        """Replay the captured update of (obs-statistics mode, minibatch i), capturing it on first
+        use. Data-parallel: two graphs with the gradient all-reduce between them."""
         key = (mode, i)
         g = self.upd_graphs.get(key)
         if g is None:
             torch.cuda.synchronize(self.device)
-            g = torch.cuda.CUDAGraph()
-            with torch.cuda.graph(g):        # records the launches without running them
-                self._minibatch_device(i)
+            if self.dp:
+                ga, gb = torch.cuda.CUDAGraph(), torch.cuda.CUDAGraph()
+                with torch.cuda.graph(ga):   # records the launches without running them
+                    self._mb_grad(i)
+                with torch.cuda.graph(gb, pool=ga.pool()):
+                    self._mb_apply(i)
+                g = (ga, gb)
+            else:
+                g = torch.cuda.CUDAGraph()
+                with torch.cuda.graph(g):
+                    self._minibatch_device(i)
             self.upd_graphs[key] = g
-        g.replay()
+        if self.dp:
+            g[0].replay()
+            self._allreduce_flat()
+            g[1].replay()
+        else:
+            g.replay()
+
+    def _minibatch_eager_dp(self, i: int) -> None:
+        self._mb_grad(i)
+        self._allreduce_flat()
+        self._mb_apply(i)
 
     def _optimizer_step(self) -> None:
         if self.truncate_grads:
@@ -471,7 +537,7 @@ class A2CAgent:
         self.scaler.step(self.optimizer)
         self.scaler.update()
 
-    def _calc_gradients_fused(self, mb: Dict[str, torch.Tensor]):
+    def _calc_gradients_fused(self, mb: Dict[str, torch.Tensor], step: bool = True):
         """calc_gradients with the loss and its head gradients in one HIP launch
         (mi_rl_ppo_loss): the MLP forward under autocast, the fused loss, autograd from the
         heads down, then the same GradScaler / clip / Adam step. Writes mu / sigma into mb."""
@@ -488,11 +554,12 @@ class A2CAgent:
             p.grad = None
         torch.autograd.backward([mu, value], [g_mu, g_val])
         net.sigma.grad = g_ls        # logstd = mu * 0 + sigma: the rows' log-std grads sum here
-        self._optimizer_step()
+        if step:
+            self._optimizer_step()
         b_loss = sums[3] if self.bounds_loss_coef is not None else sums[3] * 0.0
         return sums[0], sums[1], sums[2], sums[4], b_loss
 
-    def calc_gradients(self, mb: Dict[str, torch.Tensor]):
+    def calc_gradients(self, mb: Dict[str, torch.Tensor], step: bool = True):
         # autocast's weight cast cache off: every cast is a recorded launch (graph replay)
         with torch.autocast(device_type=self.device.type, dtype=torch.float16, enabled=self.mixed_precision,
                             cache_enabled=False):
@@ -521,10 +588,24 @@ class A2CAgent:
         for p in self.model.parameters():
             p.grad = None
         self.scaler.scale(loss).backward()
-        self._optimizer_step()
         with torch.no_grad():
             kl = policy_kl(mu.detach().float(), sigma.detach().float(), mb["mu"], mb["sigma"])
+        if step:
+            if self.dp:        # eager (CPU / gloo) data-parallel step: average grads and KL first
+                kl = self._allreduce_grads_kl(kl)
+            self._optimizer_step()
         return a_loss.detach(), c_loss.detach(), entropy.detach(), kl, mu.detach().float(), sigma.detach().float(), b_loss.detach()
+
+    def _allreduce_grads_kl(self, kl: torch.Tensor) -> torch.Tensor:
+        """Data-parallel, eager: p.grad and the KL averaged over the ranks in one all-reduce."""
+        flat = torch.cat([p.grad.reshape(-1) for p in self._params] + [kl.reshape(1).float()])
+        dist.all_reduce(flat)
+        flat.mul_(1.0 / self.world)
+        o = 0
+        for p in self._params:
+            p.grad.copy_(flat[o:o + p.numel()].view_as(p))
+            o += p.numel()
+        return flat[o].to(kl.dtype)
 
     def update_lr(self, lr: float) -> None:
         if self.lr_t is not None:      # device LR: one tensor shared by every param group
@@ -556,8 +637,21 @@ class A2CAgent:
             graphed = self.graph_update and self.epoch_num >= 2
             for mini_ep in range(self.mini_epochs):
                 mode = int(self.normalize_input and mini_ep == 0)   # obs statistics update on
+                if self.dp and self.normalize_input:
+                    # data-parallel: the obs statistics update (merged over the ranks: a
+                    # collective) runs eagerly before each minibatch's captured halves, which
+                    # then see the statistics frozen — the order of the in-forward update
+                    self.model.running_mean_std.eval()
                 for i in range(self.num_minibatches):
-                    if graphed:
+                    if self.dp:
+                        if mode:
+                            s, e = i * self.minibatch_size, (i + 1) * self.minibatch_size
+                            self.model.running_mean_std._update(self._data["obs"][s:e])
+                        if graphed:
+                            self._minibatch_graphed(0, i)
+                        else:
+                            self._minibatch_eager_dp(i)
+                    elif graphed:
                         self._minibatch_graphed(mode, i)
                     else:
                         self._minibatch_device(i)
@@ -587,7 +681,7 @@ class A2CAgent:
             a_loss_m, c_loss_m = torch.stack(a_l).mean().item(), torch.stack(c_l).mean().item()
             b_loss_m, ent_m = torch.stack(b_l).mean().item(), torch.stack(ents).mean().item()
             kl_m = torch.stack(kls).mean().item()
-        if self.distributed:
+        if self.central:
             self._broadcast_weights()
         update_time = time.perf_counter() - t0
         self.frame += self.batch_size
@@ -615,12 +709,12 @@ class A2CAgent:
                     f"{st['fps_total']:.0f} epoch: {st['epoch']}/{max_epochs} "
                     f"mean reward: {st['mean_rewards']:.3f} mean length: {st['mean_lengths']:.1f}")
             mean_rewards = st["mean_rewards"]
-            if self.is_learner and self.save_frequency > 0 and self.epoch_num % self.save_frequency == 0:
+            if self.rank == 0 and self.save_frequency > 0 and self.epoch_num % self.save_frequency == 0:
                 self.save(os.path.join(self.run_dir, "nn", f"last_{self.name}_ep_{self.epoch_num}"))
             if (self.game_rewards.current_size > 0 and mean_rewards > self.last_mean_rewards
                     and self.epoch_num >= self.save_best_after):
                 self.last_mean_rewards = mean_rewards
-                if self.is_learner:
+                if self.rank == 0:
                     self.save(os.path.join(self.run_dir, "nn", str(self.name)))
                 if mean_rewards > self.score_to_win:
                     break

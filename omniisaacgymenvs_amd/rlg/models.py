@@ -62,6 +62,23 @@ def linear_train(x: torch.Tensor, layer: nn.Linear, splits: int = 32) -> torch.T
     return _LinearSplitK.apply(x, w, b, splits)
 
 
+def _merge_moments(mean: torch.Tensor, var: torch.Tensor, n: float):
+    """(mean, unbiased var, count) of the union of every rank's batch of n rows (equal n), from
+    each rank's own: two all-reduces (parallel-variance merge)."""
+    import torch.distributed as dist
+
+    w = dist.get_world_size()
+    if w == 1:
+        return mean, var, n
+    gmean = mean.clone()
+    dist.all_reduce(gmean)
+    gmean /= w
+    m2 = var * (n - 1.0) + n * (mean - gmean) ** 2
+    dist.all_reduce(m2)
+    tot = n * w
+    return gmean, m2 / (tot - 1.0), tot
+
+
 class RunningMeanStd(nn.Module):
     """Running mean / variance of a batch stream (parallel-variance merge), f64 buffers;
     forward normalises (clamped to ±5) or un-normalises. Statistics update only in
@@ -75,6 +92,9 @@ class RunningMeanStd(nn.Module):
         self.register_buffer("running_mean", torch.zeros(shape, dtype=torch.float64))
         self.register_buffer("running_var", torch.ones(shape, dtype=torch.float64))
         self.register_buffer("count", torch.ones((), dtype=torch.float64))
+        # data-parallel learner: the batch moments are those of the union of the ranks' batches
+        # (equal batch sizes), merged by all-reduce, so every replica keeps the same statistics
+        self.all_reduce = False
 
     @torch.no_grad()
     def _update(self, x: torch.Tensor) -> None:
@@ -84,6 +104,8 @@ class RunningMeanStd(nn.Module):
         batch_mean = bm.double()
         batch_var = bv.double()
         batch_count = float(x.shape[0])
+        if self.all_reduce:
+            batch_mean, batch_var, batch_count = _merge_moments(batch_mean, batch_var, batch_count)
         delta = batch_mean - self.running_mean
         tot = self.count + batch_count
         new_mean = self.running_mean + delta * batch_count / tot

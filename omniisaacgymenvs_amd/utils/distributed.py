@@ -138,11 +138,17 @@ class RolloutGather:
     def field(self, name: str, h: int) -> torch.Tensor:
         return self.slabs[self.active].views[name][h]
 
-    def record(self, h: int, obs: torch.Tensor, rew: torch.Tensor, done: torch.Tensor) -> None:
+    def record(self, h: int, obs: torch.Tensor, rew: torch.Tensor,
+               done: Optional[torch.Tensor] = None) -> None:
+        """Copy one step into row h. A slab built with_done=False has no done field: `done`
+        must then be None (its consumer keeps its own dones)."""
         o, r, d = self.slot(h)
         o.copy_(obs)
         r.copy_(rew)
-        d.copy_(done)
+        if d is not None:
+            d.copy_(done)
+        elif done is not None:
+            raise ValueError("this slab has no done field (with_done=False): pass done=None")
 
     def _join(self, k: int) -> None:
         w = self._work[k]

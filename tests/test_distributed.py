@@ -214,3 +214,23 @@ def _rollout_tail(world):
     out[0, :, tp.num_obs] = b["rew"]
     out[0, :, tp.num_obs + 1] = b["reset"]
     return out
+
+
+def test_slab_without_done_field():
+    """RolloutGather(with_done=False) (the learner's slab: its dones are f32 learner fields):
+    slot() has no done, record() stores obs / rew and refuses a done it cannot hold."""
+    import pytest
+
+    from omniisaacgymenvs_amd.utils.distributed import RolloutGather
+
+    g = RolloutGather(4, 8, 3, "cpu", 1, buffers=1, with_done=False)
+    o, r, d = g.slot(1)
+    assert d is None and "done" not in g.slabs[0].views
+    obs = torch.arange(24, dtype=torch.float32).view(8, 3)
+    rew = torch.arange(8, dtype=torch.float32)
+    g.record(1, obs, rew)
+    assert torch.equal(g.slabs[0].obs[1], obs) and torch.equal(g.slabs[0].rew[1], rew)
+    with pytest.raises(ValueError, match="no done field"):
+        g.record(2, obs, rew, torch.zeros(8, dtype=torch.int64))
+    out = g.gather()
+    assert torch.equal(out.obs[0, 1], obs)

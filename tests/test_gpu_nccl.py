@@ -78,7 +78,7 @@ def test_shard_loop_rccl_gather_equals_twin_env(nccl_group):
     twin.close()
 
 
-def _agent(n, seed, multi_gpu, tag):
+def _agent(n, seed, multi_gpu, tag, mode="central", graph_update=False):
     from omniisaacgymenvs_amd.rlg.a2c_continuous import A2CAgent
     from omniisaacgymenvs_amd.utils.rlgames.rlgames_utils import RLGPUEnv, register_env
     from omniisaacgymenvs_amd.utils.task_util import make_env
@@ -89,8 +89,9 @@ def _agent(n, seed, multi_gpu, tag):
     register_env(name, lambda **kw: env)
     params = env.task_cfg["train"]["params"]
     params["config"]["multi_gpu"] = multi_gpu
+    params["config"]["multi_gpu_mode"] = mode
     params["config"]["graph_rollout"] = False
-    params["config"]["graph_update"] = False
+    params["config"]["graph_update"] = graph_update
     params["config"]["save_frequency"] = 0
     params["config"]["save_best_after"] = 10 ** 9
     params["seed"] = seed
@@ -121,4 +122,30 @@ def test_multi_gpu_learner_epoch_over_rccl(nccl_group):
         assert abs(st_m[k] - st_s[k]) <= 1e-5 * max(1.0, abs(st_s[k])), (k, st_m[k], st_s[k])
     for (k, a), b in zip(ag_m.model.state_dict().items(), ag_s.model.state_dict().values()):
         torch.testing.assert_close(a, b, rtol=1e-5, atol=1e-6, msg=k)
+    env_m.close(); env_s.close()
+
+
+@pytest.mark.parametrize("graphed", [False, True])
+def test_data_parallel_learner_over_rccl(nccl_group, graphed):
+    """multi_gpu_mode data_parallel (rl_games' multi_gpu) at world 1 over RCCL: per minibatch the
+    gradients + KL go through one all-reduce between the two captured halves of the update (or
+    eagerly), the obs / value statistics merge through all-reduces; the result equals the single
+    learner's (cfg/train/HumanoidPPO.yaml:43)."""
+    n = 512
+    epochs = 3 if graphed else 1          # updates are captured from epoch 2 on
+    env_m, ag_m = _agent(n, 5, True, f"dp{int(graphed)}", mode="data_parallel", graph_update=graphed)
+    env_s, ag_s = _agent(n, 5, False, f"dps{int(graphed)}", graph_update=graphed)
+    assert ag_m.dp and not ag_m.central and ag_m.rollout is None and ag_m.is_learner
+    assert ag_m.batch_size == ag_s.batch_size == 32 * n
+    ag_m.env_reset(); ag_s.env_reset()
+    for _ in range(epochs):
+        st_m = ag_m.train_epoch()
+        st_s = ag_s.train_epoch()
+    torch.cuda.synchronize()
+    if graphed:
+        assert all(isinstance(g, tuple) for g in ag_m.upd_graphs.values()) and ag_m.upd_graphs
+    for k in ("a_loss", "c_loss", "kl"):
+        assert abs(st_m[k] - st_s[k]) <= 1e-4 * max(1.0, abs(st_s[k])), (k, st_m[k], st_s[k])
+    for (k, a), b in zip(ag_m.model.state_dict().items(), ag_s.model.state_dict().values()):
+        torch.testing.assert_close(a, b, rtol=1e-4, atol=1e-5, msg=k)
     env_m.close(); env_s.close()

@@ -94,10 +94,11 @@ recipe() {
     for T in ${TASKS:-Ant Humanoid}; do run curve_${T}_$TAG 900 python -u tools/train_curve.py --task $T ${CARGS:-}; done ;;
   sizes)
     run sizes_${TASK}_$TAG 300 python -u tools/bw_sweep.py $TASK ${NS// /,} ;;
-  ab)   # A/B of the default library against LIB_B (another build of libmi_sim.so), alternating
+  ab)   # A/B of the default library against LIB_B (another build of libmi_sim.so) or, with
+        # ENV_B="VAR=value ...", against the default library under those variables; alternating
     for k in 1 2 3; do
       run ab_a_${TASK}_$k 200 python -u bench.py --task $TASK --steps 300 --warmup 30 --no-cpu-baseline --no-side --fuse-envs 0 ${BARGS:-}
-      run ab_b_${TASK}_$k 200 env MI_SIM_LIB=$LIB_B python -u bench.py --task $TASK --steps 300 --warmup 30 --no-cpu-baseline --no-side --fuse-envs 0 ${BARGS:-}
+      run ab_b_${TASK}_$k 200 env ${ENV_B:-MI_SIM_LIB=$LIB_B} python -u bench.py --task $TASK --steps 300 --warmup 30 --no-cpu-baseline --no-side --fuse-envs 0 ${BARGS:-}
     done
     for f in gpurun_out/ab_[ab]_${TASK}_*.log; do echo "$f $(grep -o '"kernel_ms": [0-9.]*\|"ms_per_step": [0-9.]*\|"lds_bytes_per_env": [0-9]*' $f | head -3 | tr '\n' ' ')"; done ;;
   *)

@@ -49,7 +49,9 @@ def main():
         st = agent.stats
         row = {"epoch": st["epoch"], "frames": st["frames"], "mean_reward": round(st["mean_rewards"], 4),
                "mean_length": round(st["mean_lengths"], 2), "games": st["games"],
-               "lr": st.get("lr"), "kl": st.get("kl"), "fps_total": round(st["fps_total"], 1),
+               "lr": st.get("lr"), "kl": st.get("kl"), "a_loss": st.get("a_loss"), "c_loss": st.get("c_loss"),
+               "grad_scale": agent.scaler.get_scale() if agent.mixed_precision else None,
+               "fps_total": round(st["fps_total"], 1),
                "wall_s": round(time.perf_counter() - t0, 3)}
         rows.append(row)
         f.write(json.dumps(row) + "\n")
