@@ -14,9 +14,11 @@ per horizon (HumanoidPPO.yaml:66, 32 steps), asynchronously while the next horiz
 timed window starts a fresh horizon and ends by gathering any partial one, so every window
 holds at least one complete gather whatever --steps is.
 
-Prints ONE JSON line (rank 0). `roofline` is for the dominant kernel (k_env_step_wave), timed
-with HIP events on the stream it is launched on; `cpu_baseline` times the CPU oracle (the
-build's C restatement; the reference's PhysX CPU path is closed and absent) on host cores.
+Prints ONE JSON line (rank 0). `roofline` is for the dominant kernel — the launch the fused
+step runs, named in the line (Humanoid / Ant: k_env_step_pair<TopoCT<Robot*>>, two envs per
+wavefront; Cartpole: k_env_step) — timed with HIP events carried by its own dispatch on the
+stream it is launched on; `cpu_baseline` times the CPU oracle (the build's C restatement; the
+reference's PhysX CPU path is closed and absent) on host cores.
 """
 from __future__ import annotations
 

@@ -154,6 +154,7 @@ typedef struct mi_sim mi_sim;
 int mi_sim_create(const mi_model_desc* model, const mi_sim_params* params, int32_t num_envs,
                   int64_t env_id_offset, int32_t device_id, const float* env_origins /*[N,3]*/,
                   uint64_t seed, mi_sim** out);
+/* Issues any deferred substeps, waits for the device, frees everything. */
 int mi_sim_destroy(mi_sim* sim);
 /* ArticulationView.num_dof / count / get_dof_limits (humanoid.py:110, ant.py:81) */
 int mi_sim_info(const mi_sim* sim, int32_t* num_envs, int32_t* num_dof, int32_t* num_links,
@@ -178,7 +179,11 @@ int mi_set_root_state(mi_sim* sim, const float* pos /*[n,3]|NULL*/, const float*
  * mi_get_state_mirror issues any deferred substeps and refreshes every stale mirror in ONE launch
  * (none when nothing wrote the state since the last refresh), so the five getter calls of one
  * get_observations cost at most one gather launch. Every entry point that writes the state marks
- * the mirrors stale; mi_set_dof_efforts does not (efforts are not mirrored). */
+ * the mirrors stale; mi_set_dof_efforts does not (efforts are not mirrored). A call on another
+ * stream than the last refresh's waits for that refresh (stream-ordered, no host sync).
+ * Contract: the mirrors are the library's copies — a caller must not write them (an in-place
+ * edit would persist into later getters until the state changes; the reference's task code only
+ * reads them, locomotion.py:81-89). */
 int mi_sim_set_mirror(mi_sim* sim, float* pos /*[N,3]*/, float* quat /*[N,4]*/, float* vel /*[N,6]*/,
                       float* q /*[N,D]*/, float* qd /*[N,D]*/, float* sens /*[N,S,6]*/);
 int mi_get_state_mirror(mi_sim* sim, void* stream);
@@ -188,7 +193,8 @@ int mi_get_state_mirror(mi_sim* sim, void* stream);
  * other call touching the state in between (the reference's controlFrequencyInv x World.step
  * loop) run as ONE launch, issued by the next entry point that reads or writes the state (or by
  * mi_sim_flush); results are identical to separate launches. Inside a stream capture, and with
- * the environment variable MI_SIM_DEFER=0, every call launches at once. */
+ * the environment variable MI_SIM_DEFER=0, every call launches at once. substeps in [0, 64];
+ * one launch never carries more than 64 (a call that would pass 64 issues the pending ones first). */
 int mi_sim_step(mi_sim* sim, int32_t substeps, void* stream);
 /* Issue any deferred substeps now (stream-ordered; no host sync). */
 int mi_sim_flush(mi_sim* sim, void* stream);
@@ -286,7 +292,8 @@ int mi_get_reset_count(mi_sim* sim, uint32_t* out /*[N] host*/);
  * so the next reset draws the same Philox noise; no reference counterpart: torch's global
  * generator state plays this role there, locomotion.py:120-124). Blocks the host. */
 int mi_set_reset_count(mi_sim* sim, const uint32_t* in /*[N] host*/);
-/* Number of env-steps whose physics produced a non-finite state and were forced to reset. */
+/* Number of env-steps whose physics produced a non-finite state and were forced to reset
+ * (issues deferred substeps first and waits for them: blocks the host). */
 int mi_sim_nan_count(mi_sim* sim, int64_t* count);
 /* Diagnostics: which physics kernel runs. path: 0 one-lane-per-env, 1 wavefront-per-env,
  * 2 two envs per wavefront (the compiled topologies' default; MI_WAVE_PAIR=0 selects path 1);
@@ -294,6 +301,10 @@ int mi_sim_nan_count(mi_sim* sim, int64_t* count);
  * lds_bytes: LDS per env (= per workgroup) of the wave path. Any output may be NULL. */
 int mi_sim_kernel_path(const mi_sim* sim, int32_t* path, int32_t* topology, int32_t* lds_bytes);
 int mi_abi_version(void);
+/* SHA-256 (hex) of the sources this library was compiled from: csrc/mi_sim.hip, csrc/*.hpp and
+ * include/*.h in name order (__graft_entry__.source_hash); "unknown" when built without it. A
+ * stale binary shows up as a mismatch against the tree (smoke(), tests/test_host.py). */
+const char* mi_build_id(void);
 const char* mi_last_error(void);
 
 #ifdef __cplusplus

@@ -113,6 +113,9 @@ MI_D void sdof_loop(const float* Ss, const float* R, F&& fn) {
 #ifndef MI_PAIR_WIDE_PD
 #define MI_PAIR_WIDE_PD 4   // W-row prefetch depth of the wide Delassus set-up (1-4 all spill: see DESIGN)
 #endif
+#ifndef MI_PAIR_WIDE_AP
+#define MI_PAIR_WIDE_AP 8   // Delassus rows streamed ahead of the wide sweeps' chain
+#endif
 #ifndef MI_PAIR_SDOF_PD
 #define MI_PAIR_SDOF_PD 4   // DOF-loop prefetch depth (sdof_loop): 2 -> 0.1609 ms, 4 -> 0.1592 (A/B)
 #endif
@@ -152,8 +155,80 @@ MI_D void pair_jrow(const MC& mc, const WaveTabs& t, const float* sm, int r, int
 // with the slab path of the same expression into flat loads
 typedef const float __attribute__((address_space(3)))* lds_cf;
 MI_D lds_cf lds_ptr(const float* p) { return (lds_cf)p; }
-MI_D const float* pair_wrow(const WaveTabs& t, const float* sm, const float* gW, int r, int nv) {
-    return r < t.w_rows_lds ? sm + t.s_W + r * nv : gW + (size_t)r * WNV;
+// The LDS W rows of the paired kernels sit in groups of four rows, DOF-major inside a group:
+// entry (r, c) at s_W + (r & ~3) nv + 4 c + (r & 3). One ds_read_b128 then returns rows
+// 4g..4g+3 of one DOF — the Delassus set-up's four row chains (one uniform address for the
+// wave) and the u update's four rows of the lane's DOF — instead of four ds_read_b32.
+// w_rows_lds is a multiple of 4 (host), so a group is wholly in LDS or wholly in the slab.
+typedef float pv4 __attribute__((ext_vector_type(4)));
+typedef const pv4 __attribute__((address_space(3)))* lds_cf4;
+MI_D int pw_idx(int r, int c, int nv) { return (r & ~3) * nv + 4 * c + (r & 3); }
+MI_D lds_cf4 pw_group(const WaveTabs& t, const float* sm, int g0, int nv) {
+    return (lds_cf4)(sm + t.s_W + g0 * nv);
+}
+// slab row r (rows >= w_rows_lds; row-major, stride WNV)
+MI_D const float* pair_srow(const float* gW, int r) { return gW + (size_t)r * WNV; }
+
+// Delassus entries A[r][g0 + q] = J_r . W_{g0+q}, q < 4, of this lane's row r (the PGS set-up of
+// both widths), the loads of DOF c + PD issued before DOF c's FMAs (a ring indexed at compile
+// time, see sdof_loop). The env has n rows; group rows past them are 0 in LDS (they hold stale
+// data there, finite or not, and the sweeps only ever scale them by a zero lambda change) and
+// repeat row n - 1 in the slab.
+template <class TP, int PD>
+MI_D void pair_dgroup(const WaveTabs& t, const float* sm, const float* gW, int g0, int n,
+                      const float (&Jr)[TP::nvc], float (&a)[4]) {
+    constexpr int NV = TP::nv, NB = PD + 1;
+    const int last = max(n - 1, 0);
+    float a0 = 0.0f, a1 = 0.0f, a2 = 0.0f, a3 = 0.0f;
+    if (g0 + 3 < t.w_rows_lds) {   // uniform: the group in LDS, one ds_read_b128 per DOF
+        const lds_cf4 W = pw_group(t, sm, g0, NV);
+        pv4 wb[NB];
+        sfor<0, (PD < NV ? PD : NV)>([&](auto C) { wb[C % NB] = W[C]; });
+        sfor<0, NV>([&](auto C) {
+            constexpr int c = C;
+            if constexpr (c + PD < NV) wb[(c + PD) % NB] = W[c + PD];
+            a0 += Jr[C] * wb[c % NB].x;
+            a1 += Jr[C] * wb[c % NB].y;
+            a2 += Jr[C] * wb[c % NB].z;
+            a3 += Jr[C] * wb[c % NB].w;
+        });
+        a[0] = g0 < n ? a0 : 0.0f;
+        a[1] = g0 + 1 < n ? a1 : 0.0f;
+        a[2] = g0 + 2 < n ? a2 : 0.0f;
+        a[3] = g0 + 3 < n ? a3 : 0.0f;
+    } else {                       // the slab (rows clamped to the env's last row)
+        const float* w0 = pair_srow(gW, min(g0, last));
+        const float* w1 = pair_srow(gW, min(g0 + 1, last));
+        const float* w2 = pair_srow(gW, min(g0 + 2, last));
+        const float* w3 = pair_srow(gW, min(g0 + 3, last));
+        float wb[NB][4];
+        auto ld = [&](auto C) {
+            constexpr int c = C;
+            wb[c % NB][0] = w0[c]; wb[c % NB][1] = w1[c]; wb[c % NB][2] = w2[c]; wb[c % NB][3] = w3[c];
+        };
+        sfor<0, (PD < NV ? PD : NV)>([&](auto C) { ld(C); });
+        sfor<0, NV>([&](auto C) {
+            constexpr int c = C;
+            if constexpr (c + PD < NV) ld(std::integral_constant<int, c + PD>{});
+            a0 += Jr[C] * wb[c % NB][0];
+            a1 += Jr[C] * wb[c % NB][1];
+            a2 += Jr[C] * wb[c % NB][2];
+            a3 += Jr[C] * wb[c % NB][3];
+        });
+        a[0] = a0; a[1] = a1; a[2] = a2; a[3] = a3;
+    }
+}
+
+// W entries of rows g0..g0+3 at this lane's DOF kc (the u update of both PGS widths)
+MI_D void pair_wcol(const WaveTabs& t, const float* sm, const float* gW, int g0, int last, int kc,
+                    int nv, float (&wq)[4]) {
+    if (g0 + 3 < t.w_rows_lds) {
+        const pv4 w = pw_group(t, sm, g0, nv)[kc];
+        wq[0] = w.x; wq[1] = w.y; wq[2] = w.z; wq[3] = w.w;
+    } else {
+#pragma unroll
+        for (int q = 0; q < 4; ++q) wq[q] = pair_srow(gW, min(g0 + q, last))[kc];
+    }
 }
 
 // One articulated substep of the env of this lane's half (env i, LDS region sm, W slab gW).
@@ -421,7 +496,7 @@ MI_D void pair_artic_substep(const DevModel& m, const WaveTabs& t, const DevStat
         if (lane == 0) {
 #pragma unroll
             for (int c = 0; c < NR; ++c)
-                if (c < nv) us[c] = us[c] + dt * res[c];
+                if (c < TP::nv) us[c] = us[c] + dt * res[c];
         }
         wave_sync();
         bool act = false;
@@ -471,10 +546,10 @@ MI_D void pair_artic_substep(const DevModel& m, const WaveTabs& t, const DevStat
         if (slot >= 0) {
             sm[t.s_ad + slot] = a > 1e-12f ? a : 1e-12f;
             if (slot < t.w_rows_lds) {
-                float* wl = sm + t.s_W + slot * nv;
+                float* wl = sm + t.s_W + (slot & ~3) * nv + (slot & 3);
 #pragma unroll
                 for (int c = 0; c < NR; ++c)
-                    if (c < nv) wl[c] = res[c] * sc;
+                    if (c < TP::nv) wl[4 * c] = res[c] * sc;
             } else {
 #pragma unroll
                 for (int c = 0; c < WNV; ++c) gW[(size_t)slot * WNV + c] = c < NR ? res[c] * sc : 0.0f;
@@ -548,36 +623,9 @@ MI_D void pair_artic_substep(const DevModel& m, const WaveTabs& t, const DevStat
         static_assert(RMAX % 4 == 0, "Delassus rows are built four at a time");
         sfor<0, RMAX / 4>([&](auto G) {
             constexpr int g0 = 4 * G;
-            float a0 = 0.0f, a1 = 0.0f, a2 = 0.0f, a3 = 0.0f;
-            if (g0 < nrows_max) {
-                auto dots = [&](auto w0, auto w1, auto w2, auto w3) {
-                    // W entries of DOF C + MI_PAIR_SDOF_PD loaded before DOF C's FMAs (a ring
-                    // indexed at compile time; see sdof_loop)
-                    constexpr int PD = MI_PAIR_SDOF_PD, NB = PD + 1;
-                    float wb[NB][4];
-                    auto ld = [&](auto C) {
-                        constexpr int c = C;
-                        wb[c % NB][0] = w0[c]; wb[c % NB][1] = w1[c]; wb[c % NB][2] = w2[c]; wb[c % NB][3] = w3[c];
-                    };
-                    sfor<0, (PD < NV ? PD : NV)>([&](auto C) { ld(C); });
-                    sfor<0, NV>([&](auto C) {
-                        constexpr int c = C;
-                        if constexpr (c + PD < NV) ld(std::integral_constant<int, c + PD>{});
-                        a0 += Jr[C] * wb[c % NB][0];
-                        a1 += Jr[C] * wb[c % NB][1];
-                        a2 += Jr[C] * wb[c % NB][2];
-                        a3 += Jr[C] * wb[c % NB][3];
-                    });
-                };
-                if (g0 + 3 < t.w_rows_lds) {   // uniform: all four rows in LDS (ds_read)
-                    const lds_cf W = lds_ptr(sm + t.s_W);
-                    dots(W + min(g0, last) * NV, W + min(g0 + 1, last) * NV,
-                         W + min(g0 + 2, last) * NV, W + min(g0 + 3, last) * NV);
-                } else
-                    dots(pair_wrow(t, sm, gW, min(g0, last), NV), pair_wrow(t, sm, gW, min(g0 + 1, last), NV),
-                         pair_wrow(t, sm, gW, min(g0 + 2, last), NV), pair_wrow(t, sm, gW, min(g0 + 3, last), NV));
-            }
-            Ar[g0] = a0; Ar[g0 + 1] = a1; Ar[g0 + 2] = a2; Ar[g0 + 3] = a3;
+            float a[4] = {0.0f, 0.0f, 0.0f, 0.0f};
+            if (g0 < nrows_max) pair_dgroup<TP, MI_PAIR_SDOF_PD>(t, sm, gW, g0, nrows, Jr, a);
+            Ar[g0] = a[0]; Ar[g0 + 1] = a[1]; Ar[g0 + 2] = a[2]; Ar[g0 + 3] = a[3];
         });
         // lane r's own row: bias, 1 / A_rr, kind (contact rows are (normal, friction, friction)
         // triples 3c..3c+2, then the limit rows)
@@ -626,27 +674,40 @@ MI_D void pair_artic_substep(const DevModel& m, const WaveTabs& t, const DevStat
             constexpr int g0 = 4 * G;
             if (g0 < nrows_max) {
                 float wq[4];
-#pragma unroll
-                for (int q = 0; q < 4; ++q)
-                    wq[q] = g0 + 3 < t.w_rows_lds ? lds_ptr(sm + t.s_W)[min(g0 + q, last) * NV + kc]
-                                                  : pair_wrow(t, sm, gW, min(g0 + q, last), NV)[kc];
+                pair_wcol(t, sm, gW, g0, last, kc, NV, wq);
 #pragma unroll
                 for (int q = 0; q < 4; ++q) u = g0 + q < nrows ? u + wq[q] * lamv[g0 + q] : u;
             }
         });
         if (lane < NV) us[lane] = u;
         wave_sync();
+        {   // reuse: lambda of row rr, written by lane rr (one select chain, one store)
+            float lo = 0.0f;
 #pragma unroll
-        for (int rr = 0; rr < RMAX; ++rr)            // reuse: lambda of row rr
-            if (lane == rr && rr < nrows) sm[t.s_ad + rr] = lamv[rr];
+            for (int rr = 0; rr < RMAX; ++rr) lo = lane_here(lane) == rr ? lamv[rr] : lo;
+            if (lane < nrows) sm[t.s_ad + lane] = lo;
+        }
     } else if (nrows_max <= 64) {
+#ifndef MI_EXP_NO_WIDE
         // Wide Delassus (a half with 33..64 rows: 0.4 % of Humanoid substeps, but they set the
         // launch's slowest waves): the two envs one after the other, each on all 64 lanes, lane
         // r = row r of that env. Per row: the owner lane projects, one v_readlane hands the new
         // lambda to the wave (its old one is read off the chain), one FMA per lane updates v.
+        // The Delassus block does not stay in registers (64 per lane would set the kernel's
+        // register peak and spill it): the set-up stores it to the wave's global scratch t.g_wa
+        // as A[s][r] (lane-contiguous rows, coalesced; A is symmetric, so row s holds every
+        // lane's A[r][s]), and the sweeps stream it back MI_PAIR_WIDE_AP rows ahead of the chain
+        // (L2-resident, off the dependency chain).
         constexpr int NV = TP::nv;
+        constexpr int PA = MI_PAIR_WIDE_AP;
         const int l64 = pair_l64(), me = l64 >> 5;
         const int kc = l64 < NV ? l64 : 0;
+        // this wave's scratch (i >> 1: the same for both halves), addressed through a buffer
+        // resource: one lane offset register for every row (row s at soffset 256 s)
+        const int wv = __builtin_amdgcn_readfirstlane(i >> 1);
+        const __amdgpu_buffer_rsrc_t ars = __builtin_amdgcn_make_buffer_rsrc(
+            (void*)(t.g_wa + (size_t)wv * (64 * 64)), (short)0, 64 * 64 * (int)sizeof(float), 0x00020000);
+        const int avo = l64 * (int)sizeof(float);
         STAMP(29);
         for (int h = 0; h < 2; ++h) {
             const int nrh = __builtin_amdgcn_readlane(nrows, 32 * h);
@@ -662,39 +723,18 @@ MI_D void pair_artic_substep(const DevModel& m, const WaveTabs& t, const DevStat
             float v = 0.0f;
             sfor<0, NV>([&](auto C) { v += Jr[C] * ush[C]; });
             STAMP(30);
-            float Ar[64];
             sfor<0, 16>([&](auto G) {
                 constexpr int g0 = 4 * G;
-                float a0 = 0.0f, a1 = 0.0f, a2 = 0.0f, a3 = 0.0f;
                 if (g0 < nrh) {
-                    auto dots = [&](auto w0, auto w1, auto w2, auto w3) {
-                        constexpr int PD = MI_PAIR_WIDE_PD, NB = PD + 1;   // prefetch ring, as above
-                        float wb[NB][4];
-                        auto ld = [&](auto C) {
-                            constexpr int c = C;
-                            wb[c % NB][0] = w0[c]; wb[c % NB][1] = w1[c]; wb[c % NB][2] = w2[c]; wb[c % NB][3] = w3[c];
-                        };
-                        sfor<0, (PD < NV ? PD : NV)>([&](auto C) { ld(C); });
-                        sfor<0, NV>([&](auto C) {
-                            constexpr int c = C;
-                            if constexpr (c + PD < NV) ld(std::integral_constant<int, c + PD>{});
-                            a0 += Jr[C] * wb[c % NB][0];
-                            a1 += Jr[C] * wb[c % NB][1];
-                            a2 += Jr[C] * wb[c % NB][2];
-                            a3 += Jr[C] * wb[c % NB][3];
-                        });
-                    };
-                    if (g0 + 3 < t.w_rows_lds) {
-                        const lds_cf W = lds_ptr(smh + t.s_W);
-                        dots(W + min(g0, last) * NV, W + min(g0 + 1, last) * NV,
-                             W + min(g0 + 2, last) * NV, W + min(g0 + 3, last) * NV);
-                    } else {
-                        dots(pair_wrow(t, smh, gWh, min(g0, last), NV), pair_wrow(t, smh, gWh, min(g0 + 1, last), NV),
-                             pair_wrow(t, smh, gWh, min(g0 + 2, last), NV), pair_wrow(t, smh, gWh, min(g0 + 3, last), NV));
-                    }
+                    float a[4];
+                    pair_dgroup<TP, MI_PAIR_WIDE_PD>(t, smh, gWh, g0, nrh, Jr, a);
+#pragma unroll
+                    for (int q = 0; q < 4; ++q)
+                        __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(unsigned, a[q]), ars, avo,
+                                                              (g0 + q) * 256, 0);
                 }
-                Ar[g0] = a0; Ar[g0 + 1] = a1; Ar[g0 + 2] = a2; Ar[g0 + 3] = a3;
             });
+            wave_sync();
             STAMP(27);
             float b = 0.0f, ia = 0.0f, lam = 0.0f;    // ia 0: a dead row keeps its lambda 0
             int kd = 0;
@@ -708,10 +748,25 @@ MI_D void pair_artic_substep(const DevModel& m, const WaveTabs& t, const DevStat
                 int nrow_it = nrh;
                 asm volatile("" : "+s"(nrow_it));
                 float lamn = 0.0f;
+                // rows rr .. rr + PA - 1 of A in flight (rows past the env's count are loaded but
+                // never used: the scratch is allocated for 64 rows and zeroed at creation)
+                // a fresh pointer each sweep: the loads must not be hoisted out of the sweep loop
+                // (they would all stay live: the register peak this scratch is here to remove)
+                int vo = avo, lw = l64;
+                // per-sweep copies: the loads and the 64 `lane == row` masks must not be hoisted
+                // out of the sweep loop (64 SGPR-pair masks would spill and reload per row)
+                asm volatile("" : "+v"(vo), "+v"(lw));
+                auto ald = [&](int r) {
+                    return __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(ars, vo, r * 256, 0));
+                };
+                float ab[PA];
+                sfor<0, PA>([&](auto Q) { ab[Q] = ald(Q); });
                 sfor<0, 64>([&](auto RR) {
                     constexpr int rr = RR;
                     if (rr < nrow_it) {
                         __builtin_amdgcn_sched_barrier(0);
+                        const float arr = ab[rr % PA];
+                        if constexpr (rr + PA < 64) ab[rr % PA] = ald(rr + PA);
                         const bool fric = kd == 1 || kd == 2;
                         const float lim = mu * lamn;
                         const float mine = __builtin_amdgcn_fmed3f(lam + (b - v) * ia, fric ? -lim : 0.0f,
@@ -719,8 +774,8 @@ MI_D void pair_artic_substep(const DevModel& m, const WaveTabs& t, const DevStat
                         const float l0 = readlane(lam, rr);
                         const float ln = readlane(mine, rr);
                         if constexpr (rr % 3 == 0) lamn = rr < nnh ? ln : lamn;
-                        v += Ar[rr] * (ln - l0);
-                        lam = l64 == rr ? ln : lam;
+                        v += arr * (ln - l0);
+                        lam = lw == rr ? ln : lam;
                     }
                 });
             }
@@ -731,10 +786,7 @@ MI_D void pair_artic_substep(const DevModel& m, const WaveTabs& t, const DevStat
                 constexpr int g0 = 4 * G;
                 if (g0 < nrh) {
                     float wq[4];
-#pragma unroll
-                    for (int q = 0; q < 4; ++q)
-                        wq[q] = g0 + 3 < t.w_rows_lds ? lds_ptr(smh + t.s_W)[min(g0 + q, last) * NV + kc]
-                                                      : pair_wrow(t, smh, gWh, min(g0 + q, last), NV)[kc];
+                    pair_wcol(t, smh, gWh, g0, last, kc, NV, wq);
 #pragma unroll
                     for (int q = 0; q < 4; ++q) {
                         const float lq = readlane(lam, g0 + q);
@@ -748,7 +800,9 @@ MI_D void pair_artic_substep(const DevModel& m, const WaveTabs& t, const DevStat
             wave_sync();
             STAMP(11);
         }
+#endif
     } else {
+#ifndef MI_EXP_NO_FALLBACK
         // fallback (a half with more rows than the Delassus registers hold, 0.4 % of Humanoid
         // substeps): u-space sweeps, lane = DOF. Rows 0..63 as the wave kernel's one-bank
         // sweeps with 32-lane banks: row r's data in lane r & 31 of bank r >> 5 (J rebuilt per row
@@ -784,12 +838,13 @@ MI_D void pair_artic_substep(const DevModel& m, const WaveTabs& t, const DevStat
         if (lane < nrows) load_row(lane, b0, ia0, k0, fa, ma, ma2);
         if (lane + 32 < nrows) load_row(lane + 32, b1, ia1, k1, fb, mb, mb2);
         const int nnorm = 3 * ncon;
-        float Wr[64];
-#pragma unroll
-        for (int rr = 0; rr < 64; ++rr) {   // uniform branch per row: LDS rows, then the slab
-            if (rr < t.w_rows_lds) Wr[rr] = sm[t.s_W + rr * nv + kc] * kin;
-            else Wr[rr] = gW[(size_t)rr * WNV + kc] * kin;
-        }
+        // W entry of row rr at the lane's DOF (uniform branch: LDS rows, then the slab); read
+        // per row (a handful of substeps in a million: registers matter more than latency here)
+        const float* wsm = sm;
+        const float* wgW = gW;
+        auto wrow = [&](int rr) {
+            return (rr < t.w_rows_lds ? wsm[t.s_W + pw_idx(rr, kc, nv)] : wgW[(size_t)rr * WNV + kc]) * kin;
+        };
         for (int r = 64 + lane; r < nrows; r += 32) gW[(size_t)r * WNV + (WNV - 1)] = 0.0f;
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
@@ -797,12 +852,16 @@ MI_D void pair_artic_substep(const DevModel& m, const WaveTabs& t, const DevStat
         for (int it = 0; it < p.iters; ++it) {
             asm volatile("" : "+v"(b0), "+v"(b1), "+v"(ia0), "+v"(ia1),
                          "+v"(ma), "+v"(mb), "+v"(ma2), "+v"(mb2));
+            int lfb = lane, nrl = nrows;
+            // per-row W reads and lane / row-count masks stay inside the sweep (hoisted, 64 masks
+            // of each would spill SGPRs)
+            asm volatile("" : "+v"(wsm), "+v"(wgW), "+v"(lfb), "+v"(nrl));
             int nrow_it = nrows_max;
             asm volatile("" : "+s"(nrow_it));
             float lamn = 0.0f;
 #pragma unroll
             for (int rr = 0; rr < 64; ++rr) {
-                if (rr >= nrow_it) continue;   // no early exit: Wr stays register-indexed
+                if (rr >= nrow_it) continue;
                 __builtin_amdgcn_sched_barrier(0);
                 const int bank = rr >> 5, w = rr & 31;
                 float fr[6];
@@ -823,10 +882,10 @@ MI_D void pair_artic_substep(const DevModel& m, const WaveTabs& t, const DevStat
                 const float lim = mu * lamn;
                 ln = fmaxf(ln, fric ? -lim : 0.0f);
                 ln = fric ? fminf(ln, lim) : ln;
-                const bool live_row = rr < nrows;
+                const bool live_row = rr < nrl;
                 lamn = (live_row && kind == 0) ? ln : lamn;
-                u = live_row ? u + Wr[rr] * (ln - l0) : u;
-                const bool own = live_row && lane_here(lane) == w;
+                u = live_row ? u + wrow(rr) * (ln - l0) : u;
+                const bool own = live_row && lfb == w;
                 if (bank) lam1 = own ? ln : lam1;
                 else lam0 = own ? ln : lam0;
             }
@@ -872,11 +931,78 @@ MI_D void pair_artic_substep(const DevModel& m, const WaveTabs& t, const DevStat
         if (lane < nrows) sm[t.s_ad + lane] = lam0;          // reuse: lambda of row lane
         if (lane + 32 < nrows) sm[t.s_ad + lane + 32] = lam1;
         for (int r = 64 + lane; r < nrows; r += 32) sm[t.s_ad + r] = gW[(size_t)r * WNV + (WNV - 1)];
+#endif
     }
     wave_sync();
     STAMP(11);
-    // ---- P11a: force sensors (lane s)
-    if (lane < m.S) {
+    // ---- P11a: force sensors. Contact-parallel when the buffer fits the dead W rows
+    // (t.sens_par): lane = contact computes its force and, for every sensor whose link it
+    // touches, its torque about the sensor, into [contact][sensor][6] at s_W; then lane =
+    // (sensor, component) sums its component over the contacts in contact order — the serial
+    // loop's terms and summation order (a non-touching contact adds a signed zero, which leaves
+    // a sum started at +0 unchanged), without its per-contact latency chain.
+    if (t.sens_par) {
+        const int S = m.S;
+        float* sb = sm + t.s_W;
+        float* sums = sb + 6 * S * t.ncmax;
+        const int nc_max = pmax(ncon);
+        for (int c0 = 0; c0 < nc_max; c0 += 32) {
+            const int c = c0 + lane;
+            if (c < ncon) {
+#pragma clang fp contract(off)
+                const int la = (int)sm[t.s_cl + c];
+                const int lb = TP::kSelf ? (int)sm[t.s_cl2 + c] : -1;
+                const float* lamp = sm + t.s_ad;
+                const float fn = lamp[3 * c] / dt, f1 = lamp[3 * c + 1] / dt, f2 = lamp[3 * c + 2] / dt;
+                float d[9];
+                contact_dirs<TP::kSelf>(sm, t, c, d);
+                const float cp[3] = {sm[t.s_cp + 3 * c], sm[t.s_cp + 3 * c + 1], sm[t.s_cp + 3 * c + 2]};
+                for (int si = 0; si < S; ++si) {
+                    const int l = (int)mc.sf(MS_LINK, si);
+                    const float sgn = la == l ? 1.0f : ((TP::kSelf && lb == l) ? -1.0f : 0.0f);
+                    float R[9], xs[3];
+#pragma unroll
+                    for (int q = 0; q < 9; ++q) R[q] = sm[t.s_R + 9 * l + q];
+                    const float sp[3] = {mc.sf(MS_X, si), mc.sf(MS_X + 1, si), mc.sf(MS_X + 2, si)};
+                    m3_vec(R, sp, xs);
+#pragma unroll
+                    for (int q = 0; q < 3; ++q) xs[q] += sm[t.s_o + 3 * l + q];
+                    float fc[3], rr[3], tc[3];
+#pragma unroll
+                    for (int q = 0; q < 3; ++q) fc[q] = sgn * (fn * d[q] + f1 * d[3 + q] + f2 * d[6 + q]);
+#pragma unroll
+                    for (int q = 0; q < 3; ++q) rr[q] = cp[q] - xs[q];
+                    cross3(rr, fc, tc);
+                    float* o = sb + 6 * (S * c + si);
+#pragma unroll
+                    for (int q = 0; q < 3; ++q) { o[q] = sgn == 0.0f ? 0.0f : fc[q]; o[3 + q] = sgn == 0.0f ? 0.0f : tc[q]; }
+                }
+            }
+        }
+        wave_sync();
+        if (lane < 6 * S) {
+            const int si = lane / 6, q = lane - 6 * si;
+            float acc = 0.0f;
+            for (int c = 0; c < ncon; ++c) acc += sb[6 * (S * c + si) + q];
+            sums[lane] = acc;
+        }
+        wave_sync();
+        if (lane < S) {
+            const int si = lane, l = (int)mc.sf(MS_LINK, si);
+            float R[9], F[3], T[3], Fl[3], Tl[3];
+#pragma unroll
+            for (int q = 0; q < 9; ++q) R[q] = sm[t.s_R + 9 * l + q];
+#pragma unroll
+            for (int q = 0; q < 3; ++q) { F[q] = sums[6 * si + q]; T[q] = sums[6 * si + 3 + q]; }
+            m3_tvec(R, F, Fl);
+            m3_tvec(R, T, Tl);
+#pragma unroll
+            for (int q = 0; q < 3; ++q) {
+                sm[t.s_rb + 6 * si + q] = Fl[q];
+                sm[t.s_rb + 6 * si + 3 + q] = Tl[q];
+            }
+        }
+    } else if (lane < m.S) {
         const int si = lane, l = (int)mc.sf(MS_LINK, si);
         float R[9], xs[3], F[3] = {0, 0, 0}, T[3] = {0, 0, 0};
 #pragma unroll

@@ -216,6 +216,14 @@ __global__ __launch_bounds__(256) void k_ppo_loss(
 extern "C" {
 
 int32_t mi_rl_abi_version(void) { return MI_RL_ABI_VERSION; }
+#ifndef MI_BUILD_ID
+#define MI_BUILD_ID "unknown"
+#endif
+// the string carries a marker prefix so the build id can be found in the binary file
+const char* mi_rl_build_id(void) {
+    static const char id[] = MI_BUILD_ID;
+    return (sizeof(id) > 12 && id[0] == 'M' && id[11] == ':') ? id + 12 : id;
+}
 
 int32_t mi_rl_ppo_loss(const void* mu, int32_t mu_half, const float* logstd, const void* value,
                        int32_t value_half, const float* actions, const float* old_logp,

@@ -84,6 +84,8 @@ struct mi_sim {
     // mirror equals the state (set by mi_get_state_mirror, cleared by every state write)
     float* mir[6] = {nullptr, nullptr, nullptr, nullptr, nullptr, nullptr};
     bool mir_valid = false;
+    hipStream_t mir_stream = nullptr;   // stream of the last refresh; a reader on another stream
+    hipEvent_t mir_ev = nullptr;        // waits on mir_ev (recorded after that refresh)
     std::vector<float> lower, upper;  // host copy for mi_sim_info
     std::vector<void*> allocs;
     // launch timing (mi_sim_time_launches): every tev_every-th mi_env_step launch carries a
@@ -94,6 +96,7 @@ struct mi_sim {
     int tev_rec = 0;
 };
 static hipError_t timed_launch(mi_sim* s, void* stream, hipEvent_t* ev0, hipEvent_t* ev1);
+static int flush_pending(mi_sim* s, void* stream);
 
 static int dev_alloc(mi_sim* s, void** p, size_t bytes) {
     if (bytes == 0) bytes = 16;
@@ -419,8 +422,12 @@ template <class F>
 static void with_topo(int id, F&& f) {
     switch (id) {
         case RobotHumanoid::id: f(TopoCT<RobotHumanoid>{}); break;
+#ifndef MI_DEV_ONLY_HUMANOID   // register / spill inspection builds (tools/regs.sh): one topology
         case RobotAnt::id: f(TopoCT<RobotAnt>{}); break;
         default: f(TopoRuntime{}); break;
+#else
+        default: break;
+#endif
     }
 }
 
@@ -909,6 +916,14 @@ __global__ void k_fill_uniform(int N, int64_t off, float* out, int cols, uint64_
 extern "C" {
 
 int mi_abi_version(void) { return MI_ABI_VERSION; }
+#ifndef MI_BUILD_ID
+#define MI_BUILD_ID "unknown"
+#endif
+// the string carries a marker prefix so the build id can be found in the binary file
+const char* mi_build_id(void) {
+    static const char id[] = MI_BUILD_ID;
+    return (sizeof(id) > 12 && id[0] == 'M' && id[11] == ':') ? id + 12 : id;
+}
 
 #ifdef MI_STAMPS
 // diagnostic build only: phase stamps of workgroup MI_STAMP_BLOCK's last substep
@@ -1277,7 +1292,10 @@ int mi_sim_create(const mi_model_desc* md, const mi_sim_params* prm, int32_t N, 
             t.s_W = ro;
             int w = std::min(64, (t.s_R + env_budget - ro) / m.nv);
             while (w > 0 && ro + al4(w * m.nv) > t.s_R + env_budget) --w;
+            w &= ~3;   // whole 4-row groups (mi_pair.hpp pw_idx: DOF-major inside a group)
             t.w_rows_lds = t.w_rows_a = std::max(0, w);
+            const char* spe = getenv("MI_SENS_PAR");
+            t.sens_par = (!spe || atoi(spe) != 0) && 6 * m.S * (C + 1) <= t.w_rows_lds * m.nv ? 1 : 0;
             t.s_W2 = 0;
             so = std::max(span1, ro + al4(t.w_rows_lds * m.nv));
         } else {
@@ -1425,6 +1443,13 @@ int mi_sim_create(const mi_model_desc* md, const mi_sim_params* prm, int32_t N, 
     if (s->wave) {
         if ((rc = dev_alloc(s, &p, sizeof(float) * (size_t)N * s->wt.g_row_stride))) return cleanup(rc);
         s->rows = (float*)p;
+        s->wt.g_wa = nullptr;
+        if (s->pair) {   // wide-PGS Delassus scratch, one 64 x 64 block per wave (mi_pair.hpp)
+            const size_t nb = sizeof(float) * (size_t)(N / 2) * 64 * 64;
+            if ((rc = dev_alloc(s, &p, nb))) return cleanup(rc);
+            if (hipMemset(p, 0, nb) != hipSuccess) return cleanup(fail(MI_E_HIP, "hipMemset (Delassus scratch)"));
+            s->wt.g_wa = (float*)p;
+        }
         AL(ws, float, 64);
     } else {
         AL(ws, float, (size_t)((N + 63) / 64) * 64 * (m.slots > 0 ? m.slots : 1));
@@ -1467,8 +1492,13 @@ int mi_sim_create(const mi_model_desc* md, const mi_sim_params* prm, int32_t N, 
 int mi_sim_destroy(mi_sim* s) {
     if (!s) return MI_OK;
     (void)hipSetDevice(s->device);
+    // deferred substeps are issued, not dropped (their state is about to be freed, but a
+    // mirror or a caller's event may still order after them), then everything drains
+    if (s->pending) (void)flush_pending(s, s->pending_stream);
+    (void)hipDeviceSynchronize();
     for (hipEvent_t e : s->tev) (void)hipEventDestroy(e);
     if (s->pending_ev) (void)hipEventDestroy(s->pending_ev);
+    if (s->mir_ev) (void)hipEventDestroy(s->mir_ev);
     for (void* p : s->allocs) (void)hipFree(p);
     delete s;
     return MI_OK;
@@ -1654,7 +1684,11 @@ int mi_get_state_mirror(mi_sim* s, void* stream) {
     if (!s->mir[0]) return fail(MI_E_STATE, "mi_get_state_mirror: no mirrors registered (mi_sim_set_mirror)");
     HIP_TRY(hipSetDevice(s->device));
     FLUSH(s, stream);
-    if (s->mir_valid) return MI_OK;
+    if (s->mir_valid) {
+        if (STREAM(stream) != s->mir_stream)    // the refresh ran on another stream: order after it
+            HIP_TRY(hipStreamWaitEvent(STREAM(stream), s->mir_ev, 0));
+        return MI_OK;
+    }
     GFields f{};
     int nf = 0;
     const int fs = s->ds.fs, es = s->ds.es;
@@ -1666,6 +1700,9 @@ int mi_get_state_mirror(mi_sim* s, void* stream) {
     if (s->dm.S > 0) f.f[nf++] = {s->ds.sens, s->mir[5], 6 * s->dm.S, s->ds.sfs, s->ds.ses};
     const int rc = gather_fields(s, f, nf, stream);
     if (rc) return rc;
+    if (!s->mir_ev) HIP_TRY(hipEventCreateWithFlags(&s->mir_ev, hipEventDisableTiming));
+    HIP_TRY(hipEventRecord(s->mir_ev, STREAM(stream)));
+    s->mir_stream = STREAM(stream);
     s->mir_valid = true;
     return MI_OK;
 }
@@ -1683,10 +1720,11 @@ int mi_sim_step(mi_sim* s, int32_t substeps, void* stream) {
         FLUSH(s, stream);
         return launch_sim(s, substeps, STREAM(stream));
     }
-    if (s->pending && s->pending_stream != STREAM(stream)) FLUSH(s, stream);
+    if (s->pending && (s->pending_stream != STREAM(stream) || s->pending + substeps > 64))
+        FLUSH(s, stream);                  // one launch never carries more than 64 substeps
     s->pending += substeps;
     s->pending_stream = STREAM(stream);
-    if (s->pending >= 64) FLUSH(s, stream);
+    if (s->pending == 64) FLUSH(s, stream);
     return MI_OK;
 }
 
@@ -2088,6 +2126,8 @@ int mi_set_reset_count(mi_sim* s, const uint32_t* in) {
 int mi_sim_nan_count(mi_sim* s, int64_t* count) {
     NEED(s); NEED(count);
     HIP_TRY(hipSetDevice(s->device));
+    FLUSH(s, s->pending_stream);           // deferred substeps count too
+    HIP_TRY(hipStreamSynchronize(s->pending_stream));
     unsigned long long v = 0;
     HIP_TRY(hipMemcpy(&v, s->ds.nan_total, sizeof v, hipMemcpyDeviceToHost));
     *count = (int64_t)v;

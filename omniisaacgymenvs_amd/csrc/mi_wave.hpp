@@ -138,6 +138,11 @@ struct WaveTabs {
     int ngeoms;
     // paired-env kernels (mi_pair.hpp): lambda per constraint row of the u-space fallback sweeps
     int s_lam;
+    // paired-env kernels: contact-parallel force sensors (buffer [ncmax][S][6] + sums in the
+    // dead W rows; 0: the serial per-sensor loop)
+    int sens_par;
+    // paired-env kernels: per-wave Delassus scratch of the wide PGS ([N / 2][64][64] floats)
+    float* g_wa;
 };
 
 // Per-model constants in the LDS block, structure-of-arrays so lane-indexed reads (lane = link,
@@ -368,7 +373,7 @@ MI_D void ct_publish_factor(int lane, int dj, const float (&Mc)[T::nvc], float d
         sfor<0, T::nv>([&](auto I) {
             constexpr int i = I;
             constexpr int na = T::dof.anc_start[i + 1] - T::dof.anc_start[i];
-            if ((T::dof.anc_mask[i] >> lane) & 1u) Lr[T::dof.lrow[i] + na - 1 - dj] = Mc[i];
+            if ((T::dof.anc_mask[i] >> lane_here(lane)) & 1u) Lr[T::dof.lrow[i] + na - 1 - dj] = Mc[i];
         });
         Lr[T::dof.lrow[T::nv] + lane] = dvec;
     }

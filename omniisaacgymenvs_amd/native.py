@@ -133,6 +133,7 @@ _SIGS = {
     "mi_sim_nan_count": (C.c_int, [C.c_void_p, _i64p]),
     "mi_sim_kernel_path": (C.c_int, [C.c_void_p, _i32p, _i32p, _i32p]),
     "mi_abi_version": (C.c_int, []),
+    "mi_build_id": (C.c_char_p, []),
     "mi_last_error": (C.c_char_p, []),
 }
 

@@ -41,6 +41,8 @@ def load_library() -> C.CDLL:
         lib.mi_rl_abi_version.argtypes = []
         lib.mi_rl_last_error.restype = C.c_char_p
         lib.mi_rl_last_error.argtypes = []
+        lib.mi_rl_build_id.restype = C.c_char_p
+        lib.mi_rl_build_id.argtypes = []
         lib.mi_rl_gae.restype = i32
         lib.mi_rl_gae.argtypes = [vp, vp, vp, vp, vp, i32, i32, f, f, vp, vp, vp]
         lib.mi_rl_sample_gauss.restype = i32

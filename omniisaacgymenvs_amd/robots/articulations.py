@@ -162,7 +162,10 @@ class ArticulationView:
     # launch after the state changed, include/mi_sim.h mi_get_state_mirror): with clone=False the
     # mirror itself, which the next physics step overwrites — Isaac's clone=False returns its
     # internal buffer the same way (locomotion.py:81-88 reads them before stepping again); with
-    # clone=True (the default) a copy.
+    # clone=True (the default) a copy. Contract (include/mi_sim.h): a clone=False result, and
+    # get_force_sensor_forces', is read-only — an in-place edit would persist into later getters
+    # until the state changes (the reference only reads them, locomotion.py:81-89). A read on
+    # another stream than the refresh's is ordered after it by the library (event wait).
     def _empty(self, *shape) -> torch.Tensor:
         return torch.empty(shape, dtype=torch.float32, device=self.device)
 

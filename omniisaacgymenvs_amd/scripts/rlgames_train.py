@@ -14,8 +14,10 @@ Multi-GPU (one process per GPU):
         -m omniisaacgymenvs_amd.scripts.rlgames_train task=Humanoid train.params.config.multi_gpu=True
 
 Rank r drives device LOCAL_RANK and owns envs [r n, (r + 1) n) of the global grid (num_envs per
-rank); the learner is rank 0 (rlg.a2c_continuous: one rollout gather per horizon, weights
-broadcast back); only rank 0 writes run files.
+rank). train.params.config.multi_gpu_mode picks the learner (rlg.a2c_continuous):
+data_parallel (default, rl_games' multi_gpu: a learner per rank, gradients + KL all-reduced per
+minibatch) or central (rank 0 learns on one rollout gather per horizon, weights broadcast back).
+Only rank 0 writes run files.
 """
 from __future__ import annotations
 

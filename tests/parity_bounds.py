@@ -8,8 +8,10 @@ profiles/r04/parity_stats_<task>.log). Two allowances may widen it, both compute
 side, never from the device's own error:
   * conditioning: SENS_K x the oracle's response to a 2-ulp perturbation of its own input
     state (tests/helpers.py oracle_sensitivity) — stacked contacts and near-singular Delassus
-    blocks amplify rounding. Capped at SENS_CAP, and fewer than WIDEN_MAX_FRAC of the envs of a
-    step may NEED it (error above the base bound); the widest bound applied is reported;
+    blocks amplify rounding. Capped at SENS_CAP x max(1, |oracle value|) (1 % of the entry's
+    magnitude: the force sensors read up to ~10 after contactForceScale), and fewer than
+    WIDEN_MAX_FRAC of the envs of a step may NEED it (error above the base bound); the widest
+    bound applied is reported;
   * the reward carries potentials - prev_potentials with |potentials| ~ 6e4 in float32
     (locomotion.py:223, dt = 1/60): 2 ulp of the potentials is the reward's own quantisation
     (bounded by construction: <= 2 ulp of 1e3 / dt).
@@ -25,16 +27,18 @@ import numpy as np
 DECISION_EPS = 1e-4          # m or rad: a decision this close to its threshold may flip
 NEAR_MAX_FRAC = 0.02         # envs at a threshold that may differ
 SENS_K = 4.0                 # conditioning allowance: this many times the oracle's 2-ulp response
-SENS_CAP = 1e-2              # ... never above this
+SENS_CAP = 1e-2              # ... never above this x max(1, |oracle value|)
 WIDEN_MAX_FRAC = 0.01        # envs per step that may need the conditioning allowance
 CARTPOLE_TOL = 1e-4
 
 # base per-env bound, away from thresholds (see the module docstring for how they were set)
+# (Humanoid sensors keep the round-1 one-step bar 2e-3, under the measured 2.6e-3 maximum: the
+# few envs above it are the ones the conditioning allowance is for)
 FAR_TOL = {
-    "Humanoid": {"root": 1e-3, "dof_pos": 4e-4, "dof_vel": 2e-3, "sensors": 2e-3, "actions": 0.0,
-                 "rew": 2e-3},
-    "Ant": {"root": 1e-4, "dof_pos": 1e-5, "dof_vel": 2e-4, "sensors": 4e-4, "actions": 0.0,
-            "rew": 1e-5},
+    "Humanoid": {"root": 2.5e-4, "dof_pos": 6e-4, "dof_vel": 2.6e-3, "sensors": 2e-3, "actions": 0.0,
+                 "rew": 4e-4},
+    "Ant": {"root": 8e-5, "dof_pos": 6e-6, "dof_vel": 8e-5, "sensors": 2.5e-4, "actions": 0.0,
+            "rew": 3e-6},
 }
 FAR_TOL["AntSelf"] = FAR_TOL["Humanoid"]   # Ant with self-collision pairs (runtime tables)
 
@@ -61,9 +65,11 @@ def evaluate(name: str, groups: Dict[str, slice], obs, rew, obs_ref, rew_ref, ma
     threshold, which needed the conditioning allowance and the widest bound applied."""
     n = len(rew)
     near = np.asarray(margin) < DECISION_EPS
-    widen = np.zeros(n) if sens is None else np.minimum(SENS_K * np.asarray(sens, np.float64), SENS_CAP)
     err = {g: np.abs(obs[:, sl] - obs_ref[:, sl]).max(axis=1) for g, sl in groups.items()}
     err["rew"] = np.abs(np.asarray(rew, np.float64) - np.asarray(rew_ref, np.float64))
+    mag = {g: np.abs(obs_ref[:, sl]).max(axis=1) for g, sl in groups.items()}
+    mag["rew"] = np.abs(np.asarray(rew_ref, np.float64))
+    sk = np.zeros(n) if sens is None else SENS_K * np.asarray(sens, np.float64)
     out = {"err": err, "near": near, "base": {}, "bound": {}, "over": {}, "needed_widening": {}}
     pot_allow = None
     if pot is not None:
@@ -74,6 +80,7 @@ def evaluate(name: str, groups: Dict[str, slice], obs, rew, obs_ref, rew_ref, ma
         base = np.full(n, FAR_TOL[name][g])
         if g == "rew" and pot_allow is not None:
             base = np.maximum(base, pot_allow)
+        widen = np.minimum(sk, SENS_CAP * np.maximum(1.0, mag[g]))
         bound = np.maximum(base, widen)
         needed = (e > base) & (e <= bound) & ~near
         over = (e > bound) & ~near

@@ -448,3 +448,37 @@ def test_modular_step_roctx_ranges(gpu, monkeypatch):
     assert names == ["pre_physics_step", "physics (controlFrequencyInv x World.step)", "post_physics_step"]
     assert sum(c[0] == "pop" for c in calls) == 3
     env.close()
+
+
+@pytest.mark.parametrize("name", ["Humanoid", "Cartpole"])
+def test_returned_obs_contract(gpu, name):
+    """The returned obs vs the reference's `_process_data` (vec_env_rlgames.py:43:
+    `clamp(obs_buf).clone()`, a tensor independent of the task's obs_buf). Documented deviation
+    (LocomotionTask.fused_step, RLTask.cleanup): with clip_obs = inf and fresh outputs, the fused
+    launch writes the obs row once and task.obs_buf IS the returned tensor; the env never writes
+    a tensor it has handed out (every step returns a new one), so a caller that keeps step k's
+    obs sees it unchanged after step k + 1. With a finite clip (Cartpole) or caller buffers
+    (out=...), obs_buf is a buffer of its own, as in the reference."""
+    env = make_env(name, num_envs=64, device="cuda:0", seed=3)
+    t = env.task
+    env.reset()
+    o1, _, _, _ = env.step(rand_actions(64, t.num_actions, 1).to("cuda:0"))
+    obs1 = o1["obs"]
+    kept = obs1.clone()
+    assert torch.equal(obs1, torch.clamp(t.obs_buf, -t.clip_obs, t.clip_obs))   # the reference's values
+    if name == "Humanoid":
+        assert obs1.data_ptr() == t.obs_buf.data_ptr()          # the deviation: aliased, not cloned
+    else:
+        assert obs1.data_ptr() != t.obs_buf.data_ptr()          # finite clip: an independent copy
+    o2, _, _, _ = env.step(rand_actions(64, t.num_actions, 2).to("cuda:0"))
+    torch.cuda.synchronize()
+    assert o2["obs"].data_ptr() != obs1.data_ptr()              # a new tensor every step
+    assert torch.equal(obs1, kept)                              # step k's obs untouched by step k + 1
+    # caller buffers: obs_buf stays separate (the launch writes both)
+    out = (torch.empty_like(kept), torch.empty(64, device="cuda:0"), torch.empty(64, dtype=torch.int64, device="cuda:0"))
+    if env.fused:
+        o3, _, _, _ = env.step(rand_actions(64, t.num_actions, 3).to("cuda:0"), out=out)
+        torch.cuda.synchronize()
+        assert o3["obs"].data_ptr() == out[0].data_ptr() != t.obs_buf.data_ptr()
+        assert torch.equal(o3["obs"], torch.clamp(t.obs_buf, -t.clip_obs, t.clip_obs))
+    env.close()

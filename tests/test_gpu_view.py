@@ -133,15 +133,39 @@ def test_indexed_efforts_through_a_substep(gpu, name):
     env.close()
 
 
+# kernel variants the deferred / mirror tests run on: (envs, MI_WAVE_PAIR, expected physics path
+# of the locomotion tasks): the default paired kernel (even N), the one-env-per-wave kernel by
+# choice (MI_WAVE_PAIR=0) and by an odd N (the paired kernel needs both halves of a wave)
+KERNELS = [(256, None, 2), (256, "0", 1), (NENV, None, 1)]
+
+
+def _make(name, n, pair, monkeypatch, **kw):
+    if pair is not None:
+        monkeypatch.setenv("MI_WAVE_PAIR", pair)
+    env = make_env(name, num_envs=n, device="cuda:0", **kw)
+    monkeypatch.delenv("MI_WAVE_PAIR", raising=False)
+    return env
+
+
+def _check_path(env, name, path):
+    got = env.task.get_robot().sim_kernel_path()[0]
+    assert got == (0 if name == "Cartpole" else path), (name, got)
+
+
+@pytest.mark.parametrize("n,pair,path", KERNELS)
 @pytest.mark.parametrize("name", ["Humanoid", "Ant", "Cartpole"])
-def test_deferred_substeps_equal_immediate_launches(gpu, name, monkeypatch):
+def test_deferred_substeps_equal_immediate_launches(gpu, name, n, pair, path, monkeypatch):
     """World.step() twice (vec_env_rlgames.py:64-66) is one launch of two substeps, issued by the
     next call that touches the state (include/mi_sim.h mi_sim_step): bit-identical to one launch
-    per World.step (MI_SIM_DEFER=0) through the method-by-method step and the getters."""
-    ea = make_env(name, num_envs=NENV, device="cuda:0", seed=4)
+    per World.step (MI_SIM_DEFER=0) through the method-by-method step and the getters — on every
+    physics kernel (first / last-substep flags of coalesced launches), and past the 64-substep
+    cap of one launch."""
+    NENV = n
+    ea = _make(name, n, pair, monkeypatch, seed=4)
     monkeypatch.setenv("MI_SIM_DEFER", "0")
-    eb = make_env(name, num_envs=NENV, device="cuda:0", seed=4)
+    eb = _make(name, n, pair, monkeypatch, seed=4)
     monkeypatch.delenv("MI_SIM_DEFER")
+    _check_path(ea, name, path)
     for e in (ea, eb):
         e.use_fused(False)
         e.reset()
@@ -157,6 +181,13 @@ def test_deferred_substeps_equal_immediate_launches(gpu, name, monkeypatch):
         v.set_joint_efforts(torch.ones((NENV, v.num_dof), device="cuda:0"))
         e._world.step()
         e._world.step()
+    sa, sb = _state(ea.task.get_robot()), _state(eb.task.get_robot())
+    for key in sa:
+        assert np.array_equal(sa[key], sb[key]), key
+    # 70 World.step()s in a row: two launches (64 + 6) when deferred, 70 when not
+    for e in (ea, eb):
+        for _ in range(70):
+            e._world.step()
     sa, sb = _state(ea.task.get_robot()), _state(eb.task.get_robot())
     for key in sa:
         assert np.array_equal(sa[key], sb[key]), key
@@ -188,14 +219,18 @@ def _mirrored(view):
     return {k: v.cpu().numpy() for k, v in out.items()}
 
 
+@pytest.mark.parametrize("n,pair,path", KERNELS)
 @pytest.mark.parametrize("name", ["Humanoid", "Ant", "Cartpole"])
-def test_state_mirrors_track_every_state_write(gpu, name):
+def test_state_mirrors_track_every_state_write(gpu, name, n, pair, path, monkeypatch):
     """The getters' state mirrors (include/mi_sim.h mi_sim_set_mirror / mi_get_state_mirror) equal
     the per-call gathers bit for bit after every kind of state write: deferred World.step()s,
     indexed setters (reset_idx's shapes), the fused env step (its mask-driven resets included) and
     the method-by-method step; clone=False hands out the mirror itself (a view the next step
-    overwrites, as Isaac's clone=False), clone=True a copy."""
-    env = make_env(name, num_envs=NENV, device="cuda:0", seed=12)
+    overwrites, as Isaac's clone=False), clone=True a copy; a read on another stream is ordered
+    after the refresh."""
+    NENV = n
+    env = _make(name, n, pair, monkeypatch, seed=12)
+    _check_path(env, name, path)
     env.reset()
     view = env.task.get_robot()
     D = view.num_dof
@@ -227,4 +262,14 @@ def test_state_mirrors_track_every_state_write(gpu, name):
         for _ in range(3):
             env.step((torch.rand((NENV, env.num_actions), generator=g) * 2 - 1).cuda())
             same()
+    # refresh on the default stream, read on a side stream: the library orders the side stream
+    # after the refresh (event wait), so the side copy sees the refreshed mirror
+    env._world.step()
+    q = view.get_joint_positions(clone=False)            # refresh (default stream)
+    side = torch.cuda.Stream()
+    with torch.cuda.stream(side):
+        q2 = view.get_joint_positions(clone=False)       # valid mirror: event wait only
+        copy = q2.clone()
+    side.synchronize()
+    assert q2 is q and np.array_equal(copy.cpu().numpy(), _direct(view)["q"])
     env.close()

@@ -153,3 +153,15 @@ def test_generated_topologies_up_to_date():
     r = subprocess.run([sys.executable, os.path.join(root, "tools", "gen_topologies.py"), "--check"],
                        capture_output=True, text=True)
     assert r.returncode == 0, r.stdout + r.stderr
+
+
+def test_libraries_are_built_from_this_tree():
+    """The shipped .so files embed the SHA-256 of the sources they were compiled from
+    (__graft_entry__.source_hash, mi_build_id / mi_rl_build_id): a stale or restored binary
+    fails here (and in smoke()) instead of silently testing other code."""
+    import __graft_entry__ as g
+    from omniisaacgymenvs_amd.rlg import ops
+
+    assert N.load_library().mi_build_id().decode() == g.source_hash()
+    assert ops.load_library().mi_rl_build_id().decode() == g.source_hash("mi_rl.hip")
+    assert g.built_id(g.LIB) == g.source_hash() and g.built_id(g.LIB_RL) == g.source_hash("mi_rl.hip")

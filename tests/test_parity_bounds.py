@@ -27,7 +27,8 @@ def test_clean_step_passes_without_widening():
 
 def test_allowance_counted_and_widest_reported():
     ref, rr, obs, rew, margin, sens = _case()
-    obs[5, 20] += 5e-3                  # dof_pos: above its base bound (4e-4)
+    ref[5, 20] = 0.5
+    obs[5, 20] = 0.5 + 5e-3             # dof_pos: above its base bound (6e-4)
     sens[5] = 2e-3                      # the oracle says this env's step is ill-conditioned
     logs = []
     r = PB.check("Humanoid", G, obs, rew, ref, rr, margin, sens=sens, quantiles=False, log=logs.append)
@@ -37,16 +38,32 @@ def test_allowance_counted_and_widest_reported():
 
 def test_allowance_is_capped():
     ref, rr, obs, rew, margin, sens = _case()
+    ref[7, 0] = obs[7, 0] = 0.5
     obs[7, 0] += 0.05
     sens[7] = 1.0                       # 4 x sens = 4 would allow it: the cap (1e-2) does not
     with pytest.raises(AssertionError, match="root"):
         PB.check("Humanoid", G, obs, rew, ref, rr, margin, sens=sens, quantiles=False, log=None)
 
 
+def test_allowance_cap_scales_with_magnitude():
+    ref, rr, obs, rew, margin, sens = _case()
+    sl = G["sensors"]
+    ref[4, sl] = 0.0
+    ref[4, sl.start] = 5.0              # a 5-unit force reading: the cap is 1 % of it
+    obs[4, sl] = ref[4, sl]
+    obs[4, sl.start] += 0.04
+    sens[4] = 1.0
+    r = PB.check("Humanoid", G, obs, rew, ref, rr, margin, sens=sens, quantiles=False, log=None)
+    assert r["widest_applied"] == pytest.approx(0.05)
+    obs[4, sl.start] += 0.02            # 0.06 > 1 % of 5
+    with pytest.raises(AssertionError, match="sensors"):
+        PB.check("Humanoid", G, obs, rew, ref, rr, margin, sens=sens, quantiles=False, log=None)
+
+
 def test_too_many_envs_needing_the_allowance_fail():
     ref, rr, obs, rew, margin, sens = _case()
     idx = np.arange(0, 1000, 50)[:15]   # 1.5 % of the envs
-    obs[idx, 20] += 1e-3
+    obs[idx, 20] += 2e-3
     sens[idx] = 1e-3
     with pytest.raises(AssertionError, match="needed the conditioning allowance"):
         PB.check("Humanoid", G, obs, rew, ref, rr, margin, sens=sens, quantiles=False, log=None)
@@ -54,7 +71,7 @@ def test_too_many_envs_needing_the_allowance_fail():
 
 def test_ant_bounds_are_tighter_than_humanoid():
     ref, rr, obs, rew, margin, sens = _case(name="Ant")
-    obs[3, 20] += 1e-4                  # fine for Humanoid dof_pos, not for Ant (1e-5)
+    obs[3, 20] += 1e-4                  # fine for Humanoid dof_pos, not for Ant (6e-6)
     PB.check("Humanoid", G, obs, rew, ref, rr, margin, sens=sens, quantiles=False, log=None)
     with pytest.raises(AssertionError, match="dof_pos"):
         PB.check("Ant", G, obs, rew, ref, rr, margin, sens=sens, quantiles=False, log=None)
@@ -62,7 +79,8 @@ def test_ant_bounds_are_tighter_than_humanoid():
 
 def test_reward_potential_quantisation_allowance():
     ref, rr, obs, rew, margin, sens = _case()
-    rew[9] += 5e-3                      # 2 ulp of a 6e4 potential is 7.8e-3
+    rr[9] = 0.5
+    rew[9] = 0.5 + 5e-3                 # 2 ulp of a 6e4 potential is 7.8e-3
     pot = np.full(1000, 10.0)
     with pytest.raises(AssertionError, match="rew"):
         PB.check("Humanoid", G, obs, rew, ref, rr, margin, sens=sens, pot=pot, quantiles=False, log=None)

@@ -18,7 +18,7 @@ def main():
     for n in sizes:
         steps = max(10, min(200, (200 * 4096) // n))
         cmd = [sys.executable, os.path.join(ROOT, "bench.py"), "--task", task, "--num-envs", str(n),
-               "--steps", str(steps), "--warmup", "5", "--no-cpu-baseline", "--fuse-envs", "0"]
+               "--steps", str(steps), "--warmup", "5", "--no-cpu-baseline", "--no-side", "--fuse-envs", "0"]
         r = subprocess.run(cmd, capture_output=True, text=True, timeout=600)
         line = [l for l in r.stdout.splitlines() if l.startswith("{")]
         if r.returncode != 0 or not line:

@@ -18,6 +18,7 @@
 #   pstats       device-vs-oracle error distribution + oracle sensitivity -> parity_stats_<task>.log
 #   freerun      free-running device vs oracle distributions              -> free_run_*.log
 #   stamps       phase stamps (per-phase s_memtime accumulators)          -> stamps_<task>.log
+#   tail         slowest-wave phase stamps of the paired kernel            -> tail/pair_tail_*.log
 #   patha        INTEGRATION path (A): reference call sequence over ArticulationView -> path_a_humanoid.json
 #   train        PPO frames/s (tools/bench_train.py)                       -> bench_train_*.log
 #   curve        reference training schedule, per-epoch curve (tools/train_curve.py) -> train_curve_*.jsonl
@@ -86,6 +87,8 @@ recipe() {
     for T in Humanoid Ant Cartpole; do run free_run_${T}_$TAG 300 python -u tools/free_run.py $T 4096; done ;;
   stamps)
     for T in ${TASKS:-Humanoid Ant}; do run stamps_${T}_$TAG 150 python -u tools/phase_stamps.py $T 4096; done ;;
+  tail)   # slowest-wave phase stamps of the paired kernel (needs libmi_sim_stamps.so on the box)
+    for T in ${TASKS:-Humanoid}; do run tail_${T}_$TAG 150 python -u tools/pair_tail.py $T 4096 3; done ;;
   patha)
     run path_a 200 python -u tools/path_a_timing.py ;;
   train)

@@ -50,8 +50,17 @@ def measure(task_name: str = "Humanoid", n: int = 4096, steps: int = 200) -> dic
 
     ev = []   # (start, stop) HIP events around each backend call when timing the backend alone
     cache = {}  # the reference ops alone: every backend call replaced by its last result
+    host = {}   # host seconds per backend call (name -> [total, calls]) when timing the host side
+    timing_host = False
 
     def backend(fn, *a, **kw):
+        if timing_host:
+            t0 = time.perf_counter()
+            r = fn(*a, **kw)
+            h = host.setdefault(getattr(fn, "__name__", str(fn)), [0.0, 0])
+            h[0] += time.perf_counter() - t0
+            h[1] += 1
+            return r
         if ref_only:
             key = getattr(fn, "__name__", str(fn))
             if key not in cache:
@@ -121,18 +130,29 @@ def measure(task_name: str = "Humanoid", n: int = 4096, steps: int = 200) -> dic
     timed(path_a, 5000)
     torch.cuda.synchronize()
     backend_ms = sum(a.elapsed_time(b) for a, b in ev[-(len(ev) * steps // (steps + 20)):]) / steps
+    timing_backend = False
+    # host cost of each backend call (ctypes, argument checks, launch enqueue): while the host
+    # is inside these the GPU can sit idle (the event intervals above count that idle time)
+    timing_host = True
+    timed(path_a, 7000)
+    timing_host = False
+    host_us = {k: round(1e6 * v[0] / v[1], 2) for k, v in host.items()}
+    host_us_step = round(1e6 * sum(v[0] for v in host.values()) / (steps + 20), 2)
     acts = torch.rand((8, n, t.num_actions), device=dev, generator=g) * 2 - 1
     ms_b_wall, ms_b_dev = timed(lambda k: env.step(acts[k % 8]), 1000)
     rec = {"task": task_name, "num_envs": n, "steps": steps,
            "path_a_ms_per_step": round(ms_a_wall, 4), "path_a_device_ms_per_step": round(ms_a_dev, 4),
            "path_a_backend_device_ms_per_step": round(backend_ms, 4),
+           "backend_host_us_per_call": host_us, "backend_host_us_per_step": host_us_step,
            "reference_ops_only_ms_per_step": round(ms_ref_wall, 4),
            "path_a_launches_per_step": "1 physics (deferred substeps) + 1 state-mirror refresh (the five getters) + efforts "
                                        "+ 4 reset scatters when any env is due",
            "path_b_fused_ms_per_step": round(ms_b_wall, 4), "path_b_device_ms_per_step": round(ms_b_dev, 4),
            "note": "path A: the reference's call sequence incl. its reset / termination torch ops and "
                    "nonzero() host sync; jit observation / reward math excluded. backend_device: "
-                   "the libmi_sim calls alone (HIP events around each); reference_ops_only: the same loop with "
+                   "the libmi_sim calls alone (HIP events around each: includes the GPU's idle time while "
+                   "the host enqueues the call; the kernels alone: rocprofv3 kernel trace); backend_host: "
+                   "host time inside each call; reference_ops_only: the same loop with "
                    "every backend call skipped (the reference's own torch ops and host sync)"}
     env.close()
     return rec

@@ -18,6 +18,7 @@ def main():
     cnt = collections.Counter()
     inside = False
     loc = "?"
+    spill_vgprs = set()   # VGPRs that hold SGPR spills (destinations of v_writelane)
     for ln in open(path):
         m = re.match(r"\s*\.file\s+(\d+)\s+\"([^\"]*)\"(?:\s+\"([^\"]*)\")?", ln)
         if m:
@@ -43,8 +44,10 @@ def main():
             cnt[("vload", loc)] += 1
         elif s.startswith("v_writelane_b32"):
             cnt[("swritelane", loc)] += 1
+            spill_vgprs.add(s.split()[1].rstrip(","))
         elif s.startswith("v_readlane_b32"):
-            cnt[("sreadlane", loc)] += 1
+            src = s.split()[2].rstrip(",")
+            cnt[("sreload" if src in spill_vgprs else "readlane", loc)] += 1
     for (k, l), v in cnt.most_common(top):
         print(f"{k:11s} {l:24s} {v}")
 
