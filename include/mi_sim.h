@@ -218,8 +218,9 @@ int mi_task_post_step(mi_sim* sim, const float* actions /*[N,A]*/, float* obs /*
                       float* rew /*[N]*/, int64_t* reset_buf, int64_t* progress_buf,
                       float* potentials, float* prev_potentials, void* stream);
 /* Which kernel the last mi_task_post_step launched and its grid (diagnostics, no reference
- * counterpart): 0..3 k_loco_post_tiled 64s/64d/32s/32d, 4 k_loco_post_pipe, 5 k_post_step
- * (one lane per env); -1 before the first launch. */
+ * counterpart): 0..3 k_loco_post_tiled 64s/64d/32s/32d, 4 k_loco_post_pipe (32-env tiles),
+ * 5 k_post_step (one lane per env), 6 k_loco_post_pipe with 16-env tiles; -1 before the first
+ * launch. */
 int mi_task_post_kernel(const mi_sim* sim, int32_t* kernel, int32_t* grid);
 /* The three task methods RLTask.post_physics_step calls, as separate kernels
  * (rl_task.py:244-250) for tasks that override some of them in torch:

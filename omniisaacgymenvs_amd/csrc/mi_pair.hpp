@@ -113,6 +113,12 @@ MI_D void sdof_loop(const float* Ss, const float* R, F&& fn) {
 #ifndef MI_PAIR_WIDE_PD
 #define MI_PAIR_WIDE_PD 4   // W-row prefetch depth of the wide Delassus set-up (1-4 all spill: see DESIGN)
 #endif
+#ifndef MI_PAIR_EXACT_ROWS
+#define MI_PAIR_EXACT_ROWS 1   // P9: exact-row passes when the speculative batch needs two (0: always speculative)
+#endif
+#ifndef MI_PAIR_WIDE_AREG
+#define MI_PAIR_WIDE_AREG 32   // wide-PGS Delassus rows in registers (0, 32 or 64); the rest streamed
+#endif
 #ifndef MI_PAIR_WIDE_AP
 #define MI_PAIR_WIDE_AP 8   // Delassus rows streamed ahead of the wide sweeps' chain
 #endif
@@ -484,11 +490,19 @@ MI_D void pair_artic_substep(const DevModel& m, const WaveTabs& t, const DevStat
     }
     wave_sync();
     STAMP(6);
-    // ---- P7+P9: one batch per half, lanes over solve vectors (rhs, limit candidates, contact
-    // rows); passes of 32 to the larger half's count
+    // ---- P7+P9: lanes over solve vectors, passes of 32 to the larger half's count. Two lane
+    // layouts, same vectors, same solves, same row order (bit-identical results):
+    //  * speculative (1 + limit candidates + contact rows fit one pass): lane 0 the rhs, lanes
+    //    1..nlim every limit candidate's unit vector (the limit test runs on lane 0's u* inside
+    //    the pass, the inactive candidates' solves are dropped), then the contact rows;
+    //  * exact (more rows: most Humanoid substeps with >= 4 contacts): the rhs alone first (one
+    //    solve, no J build or filing), the limit test, then passes over exactly the rows —
+    //    contacts, then the active limits (ceil((nc + nact) / 32) passes instead of
+    //    ceil((1 + nlim + nc) / 32) with the unused candidates).
     const int nlim = t.nlimc;
     const int total = 1 + nlim + nc;
     const int total_max = pmax(total);
+    const bool spec = !MI_PAIR_EXACT_ROWS || total_max <= 32;  // uniform
     int nrows = nc;
     unsigned limact = 0u;
     auto limit_rows = [&](const auto& res) {
@@ -556,11 +570,28 @@ MI_D void pair_artic_substep(const DevModel& m, const WaveTabs& t, const DevStat
             }
         }
     };
-    for (int base = 0; base < total_max; base += 32) {
+    int pass_total = total_max;
+    if (!spec) {   // exact layout: u* = u + dt M~^-1 rhs first (every lane solves the rhs), limit test
+        float x[TP::nvc];
+        sfor<0, TP::nv>([&](auto C) { x[C] = rhs[C]; });
+        float a;
+        ct_solve_l<TP, MI_PAIR_SOLVE_PD>(sm + t.s_L, x, a);
+        limit_rows(x);
+        pass_total = pmax(nrows);
+    }
+    for (int base = 0; base < pass_total; base += 32) {
         const int bv = base + lane;
-        const bool on = bv < total;
-        const int r = bv - 1 - nlim;
-        const int kd = (on && bv > 0 && r < 0) ? nr + mc.lim(bv - 1) : -1;
+        bool on;
+        int r, kd;
+        if (spec) {
+            on = bv < total;
+            r = bv - 1 - nlim;
+            kd = (on && bv > 0 && r < 0) ? nr + mc.lim(bv - 1) : -1;
+        } else {      // rows in their final order: contacts, then the active limits (s_rl: -(k + 1))
+            on = bv < nrows;
+            r = bv < nc ? bv : -1;
+            kd = (on && bv >= nc) ? (int)(-sm[t.s_rl + bv] - 1.0f) : -1;
+        }
         float x[TP::nvc];
         const bool crow = on && r >= 0;
         float f[6] = {0.0f, 0.0f, 0.0f, 0.0f, 0.0f, 0.0f};
@@ -579,13 +610,13 @@ MI_D void pair_artic_substep(const DevModel& m, const WaveTabs& t, const DevStat
             float xc = (ia ? v : 0.0f) - (ib ? v : 0.0f);
             float rc = rcl;
             asm volatile("" : "+v"(xc), "+v"(rc));
-            x[c] = crow ? xc : (bv == 0 ? rc : (kd == c ? 1.0f : 0.0f));
+            x[c] = crow ? xc : ((spec && bv == 0) ? rc : (kd == c ? 1.0f : 0.0f));
         });
         STAMP(7);
         float a;
         ct_solve_l<TP, MI_PAIR_SOLVE_PD>(sm + t.s_L, x, a);
         STAMP(8);
-        if (base == 0) limit_rows(x);
+        if (spec && base == 0) limit_rows(x);
         STAMP(9);
         file_row(x, on, r, kd, a);
         STAMP(10);
@@ -700,6 +731,7 @@ MI_D void pair_artic_substep(const DevModel& m, const WaveTabs& t, const DevStat
         // (L2-resident, off the dependency chain).
         constexpr int NV = TP::nv;
         constexpr int PA = MI_PAIR_WIDE_AP;
+        constexpr int AR = MI_PAIR_WIDE_AREG;   // Delassus rows kept in registers; the rest streamed
         const int l64 = pair_l64(), me = l64 >> 5;
         const int kc = l64 < NV ? l64 : 0;
         // this wave's scratch (i >> 1: the same for both halves), addressed through a buffer
@@ -723,18 +755,22 @@ MI_D void pair_artic_substep(const DevModel& m, const WaveTabs& t, const DevStat
             float v = 0.0f;
             sfor<0, NV>([&](auto C) { v += Jr[C] * ush[C]; });
             STAMP(30);
+            float Ar[AR > 0 ? AR : 1];
             sfor<0, 16>([&](auto G) {
                 constexpr int g0 = 4 * G;
+                float a[4] = {0.0f, 0.0f, 0.0f, 0.0f};
                 if (g0 < nrh) {
-                    float a[4];
                     pair_dgroup<TP, MI_PAIR_WIDE_PD>(t, smh, gWh, g0, nrh, Jr, a);
+                    if constexpr (g0 >= AR) {
 #pragma unroll
-                    for (int q = 0; q < 4; ++q)
-                        __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(unsigned, a[q]), ars, avo,
-                                                              (g0 + q) * 256, 0);
+                        for (int q = 0; q < 4; ++q)
+                            __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(unsigned, a[q]), ars, avo,
+                                                                  (g0 + q) * 256, 0);
+                    }
                 }
+                if constexpr (g0 < AR) { Ar[g0] = a[0]; Ar[g0 + 1] = a[1]; Ar[g0 + 2] = a[2]; Ar[g0 + 3] = a[3]; }
             });
-            wave_sync();
+            if constexpr (AR < 64) wave_sync();
             STAMP(27);
             float b = 0.0f, ia = 0.0f, lam = 0.0f;    // ia 0: a dead row keeps its lambda 0
             int kd = 0;
@@ -759,14 +795,21 @@ MI_D void pair_artic_substep(const DevModel& m, const WaveTabs& t, const DevStat
                 auto ald = [&](int r) {
                     return __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(ars, vo, r * 256, 0));
                 };
+                // rows AR.. streamed: their first PA loads are issued before the sweep, so the
+                // register rows' steps hide their latency
                 float ab[PA];
-                sfor<0, PA>([&](auto Q) { ab[Q] = ald(Q); });
+                if constexpr (AR < 64) sfor<0, PA>([&](auto Q) { ab[Q] = ald(AR + Q); });
                 sfor<0, 64>([&](auto RR) {
                     constexpr int rr = RR;
                     if (rr < nrow_it) {
                         __builtin_amdgcn_sched_barrier(0);
-                        const float arr = ab[rr % PA];
-                        if constexpr (rr + PA < 64) ab[rr % PA] = ald(rr + PA);
+                        float arr;
+                        if constexpr (rr < AR) {
+                            arr = Ar[rr];
+                        } else {
+                            arr = ab[(rr - AR) % PA];
+                            if constexpr (rr + PA < 64) ab[(rr - AR) % PA] = ald(rr + PA);
+                        }
                         const bool fric = kd == 1 || kd == 2;
                         const float lim = mu * lamn;
                         const float mine = __builtin_amdgcn_fmed3f(lam + (b - v) * ia, fric ? -lim : 0.0f,

@@ -328,14 +328,16 @@ static size_t post_tile_lds(int te, bool stage, int es, int A, int O, int D, int
     return sizeof(float) * (size_t)(te * (es + 1) + te * (A + 1) + (stage ? te * O : 0));
 }
 
-// variant of the tiled post-step (MI_POST_TILE=32p|64s|64d|32s|32d, read per launch so a test
-// can compare variants in one process; default 32p = k_loco_post_pipe)
+// variant of the tiled post-step (MI_POST_TILE=32p|16p|64s|64d|32s|32d, read per launch so a
+// test can compare variants in one process; default 32p = k_loco_post_pipe with 32-env tiles,
+// 16p the same kernel with 16-env tiles)
 static int post_tile_variant() {
     const char* e = getenv("MI_POST_TILE");
     if (e && !strcmp(e, "64s")) return 0;
     if (e && !strcmp(e, "64d")) return 1;
     if (e && !strcmp(e, "32s")) return 2;
     if (e && !strcmp(e, "32d")) return 3;
+    if (e && !strcmp(e, "16p")) return 6;
     return 4;   // 32p
 }
 
@@ -524,7 +526,7 @@ __device__ __forceinline__ float* wave_env_lds(const WaveTabs& t, float* smem) {
 // scratch). Action rows: always MI_PIPE_A loads per lane, the index clamped to the tile, the
 // overhang written to a spare float. Host-checked: records (fs = 1), sensors (sfs = 1,
 // ses = 6S, 6S % 4 == 0); 1 <= A <= 32; D, 6S <= 64.
-constexpr int MI_PIPE_A = 16;   // 32 envs x <= 32 actions / 64 lanes
+constexpr int mi_pipe_a(int te) { return te / 2; }   // te envs x <= 32 actions / 64 lanes
 // floor(x / d) for 0 <= x < 4096, 1 <= d <= 128: (x * ceil(2^20 / d)) >> 20 (exact there)
 MI_D int div_small(int x, unsigned magic) { return (int)(((unsigned)x * magic) >> 20); }
 
@@ -543,22 +545,26 @@ __host__ __device__ inline PipeGeo pipe_geo(int es, int D, int S) {
     g.s0 = 4 * g.ne4;                                     // sensors in the LDS record
     return g;
 }
-constexpr int pipe_nr4(int ne4) { return (32 * ne4 + 63) / 64; }
-constexpr int pipe_ns4(int ns4) { return (32 * ns4 + 63) / 64; }
-static size_t post_pipe_lds(int es, int A, int O, int D, int S) {
+constexpr int pipe_nr4(int ne4, int te = 32) { return (te * ne4 + 63) / 64; }
+constexpr int pipe_ns4(int ns4, int te = 32) { return (te * ns4 + 63) / 64; }
+static size_t post_pipe_lds(int es, int A, int O, int D, int S, int te = 32) {
     const PipeGeo g = pipe_geo(es, D, S);
-    // records [32][P] + a spare float4, obs tile [32][O], potentials in / out, spare float (the
-    // reward sums stay in registers: lane pairs). Humanoid 20 128 B: 8 workgroups per CU.
-    return sizeof(float) * (size_t)(32 * g.P + 4 + 32 * O + 2 * 32 + 4);
+    // records [te][P] + a spare float4, obs tile [te][O], potentials in / out, spare float (the
+    // reward sums stay in registers: lane pairs). Humanoid, 32-env tiles: 20 128 B, 8 workgroups
+    // per CU; 16-env tiles: 10 112 B
+    return sizeof(float) * (size_t)(te * g.P + 4 + te * O + 2 * te + 4);
 }
 
-template <int NR4, int NS4>
+// TE envs per tile (32, or 16: half the LDS and prefetch registers per workgroup, so more
+// workgroups stay resident; lanes e + 16 then repeat env e's root / reward chains, writing nothing)
+template <int TE, int NR4, int NS4>
 __global__ __launch_bounds__(64) void k_loco_post_pipe(const KParams* __restrict__ kp_arg,
                                                       const float* __restrict__ actions,
                                                       float* obs, float* rew, int64_t* reset_buf,
                                                       int64_t* progress_buf, float* pot,
                                                       float* prev) {
-    constexpr int TE = 32;
+    static_assert(TE == 32 || TE == 16, "tile of 32 or 16 envs");
+    constexpr int MI_PIPE_A = mi_pipe_a(TE);
     extern __shared__ __attribute__((aligned(16))) float sm[];
     const int lane = threadIdx.x;
     const KParams* kp = opaque_kp(kp_arg);
@@ -651,15 +657,19 @@ __global__ __launch_bounds__(64) void k_loco_post_pipe(const KParams* __restrict
                 sobs[e * O + 12 + 2 * D + sen_c] = srec[e * g.P + g.s0 + sen_c] * cs;
         }
         __syncthreads();
-        // root-frame block and the reward's DOF-order sums: env lane & 31 on both lane halves
+        // root-frame block and the reward's DOF-order sums: env lane & (TE - 1) on both lane
+        // halves (the pair helpers see lane `pl`: with 16-env tiles lanes 16..31 / 48..63 act as
+        // 0..15 / 32..47 and write nothing)
+        const int pl = TE == 32 ? lane : ((lane & 15) | (lane & 32));
+        const bool pw = TE == 32 || (lane & 16) == 0;
         {
             const DevTask& tp = k->tp;
-            const int e = lane & 31;
+            const int e = pl & 31;
             float* R = sobs + (size_t)e * O;
-            loco_obs_root_pair(srec + e * g.P, tp, lane, R, spot, sprev, e < n);
+            loco_obs_root_pair(srec + e * g.P, tp, pl, R, spot, sprev, e < n && pw);
         }
-        const LocoTerms lt = loco_reward_terms_pair(k->tp, D, sobs + (size_t)(lane & 31) * O,
-                                                    sobs + (size_t)(lane & 31) * O + ka, lane);
+        const LocoTerms lt = loco_reward_terms_pair(k->tp, D, sobs + (size_t)(pl & 31) * O,
+                                                    sobs + (size_t)(pl & 31) * O + ka, pl);
         if (lane < n) {
             const int i = e0 + lane;
             const DevTask& tp = k->tp;
@@ -1812,22 +1822,27 @@ int mi_task_post_step(mi_sim* s, const float* actions, float* obs, float* rew, i
     HIP_TRY(hipSetDevice(s->device));
     FLUSH(s, stream);
     int var = post_tile_variant();
-    if (var == 4) {   // 32p: several tiles per resident workgroup, next tile's loads in flight
+    if (var == 4 || var == 6) {   // 32p / 16p: several tiles per resident workgroup, next tile's loads in flight
         const int es = s->ds.es, ns = 6 * s->dm.S;
-        const size_t tile = post_pipe_lds(es, s->tp.A, s->tp.O, s->dm.D, s->dm.S);
+        const int pte = var == 6 ? 16 : 32;
+        const size_t tile = post_pipe_lds(es, s->tp.A, s->tp.O, s->dm.D, s->dm.S, pte);
         const PipeGeo pg = pipe_geo(es, s->dm.D, s->dm.S);
-        // shipped (NR4, NS4) instantiations: Humanoid (7, 2), Ant (4, 3); other models take the
-        // one-tile kernel
-        const int nr4 = pipe_nr4(pg.ne4), ns4 = pipe_ns4(pg.ns4);
-        const int combo = (nr4 == 7 && ns4 == 2) ? 1 : (nr4 == 4 && ns4 == 3) ? 2 : 0;
+        // shipped (TE, NR4, NS4) instantiations: Humanoid (32, 7, 2) / (16, 4, 1), Ant (32, 4, 3) /
+        // (16, 2, 2); other models take the one-tile kernel
+        const int nr4 = pipe_nr4(pg.ne4, pte), ns4 = pipe_ns4(pg.ns4, pte);
+        const int combo = pte == 32 ? ((nr4 == 7 && ns4 == 2) ? 1 : (nr4 == 4 && ns4 == 3) ? 2 : 0)
+                                    : ((nr4 == 4 && ns4 == 1) ? 3 : (nr4 == 2 && ns4 == 2) ? 4 : 0);
         if (s->tp.kind != MI_TASK_CARTPOLE && s->wave && s->kp_dev && s->ds.fs == 1 && es % 32 == 0 &&
             s->ds.sfs == 1 && s->ds.ses == ns && ns % 4 == 0 && combo &&
             s->tp.A >= 1 && s->tp.A <= 32 && s->dm.D >= 1 && s->dm.D <= 64 &&
             ns <= 64 && tile <= 64 * 1024) {
             if (s->num_cu <= 0)
                 HIP_TRY(hipDeviceGetAttribute(&s->num_cu, hipDeviceAttributeMultiprocessorCount, s->device));
-            const int ntiles = (s->N + 31) / 32;
-            const void* fn = combo == 1 ? (const void*)k_loco_post_pipe<7, 2> : (const void*)k_loco_post_pipe<4, 3>;
+            const int ntiles = (s->N + pte - 1) / pte;
+            const void* fn = combo == 1 ? (const void*)k_loco_post_pipe<32, 7, 2>
+                           : combo == 2 ? (const void*)k_loco_post_pipe<32, 4, 3>
+                           : combo == 3 ? (const void*)k_loco_post_pipe<16, 4, 1>
+                                        : (const void*)k_loco_post_pipe<16, 2, 2>;
             // one resident round: workgroups per CU as registers and LDS allow together
             int per_cu = 0;
             HIP_TRY(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, fn, 64, tile));
@@ -1841,17 +1856,19 @@ int mi_task_post_step(mi_sim* s, const float* actions, float* obs, float* rew, i
             const KParams* kp = (const KParams*)s->kp_dev;
             hipEvent_t ev0 = nullptr, ev1 = nullptr;
             HIP_TRY(timed_launch(s, stream, &ev0, &ev1));
-#define POST_PIPE(R, Q) do { if (ev0) hipExtLaunchKernelGGL((k_loco_post_pipe<R, Q>), dim3(grid), dim3(64), (uint32_t)tile, \
+#define POST_PIPE(T, R, Q) do { if (ev0) hipExtLaunchKernelGGL((k_loco_post_pipe<T, R, Q>), dim3(grid), dim3(64), (uint32_t)tile, \
             STREAM(stream), ev0, ev1, 0, kp, actions, obs, rew, reset_buf, progress_buf, potentials, prev_potentials); \
-            else hipLaunchKernelGGL((k_loco_post_pipe<R, Q>), dim3(grid), dim3(64), tile, STREAM(stream), kp, \
+            else hipLaunchKernelGGL((k_loco_post_pipe<T, R, Q>), dim3(grid), dim3(64), tile, STREAM(stream), kp, \
             actions, obs, rew, reset_buf, progress_buf, potentials, prev_potentials); } while (0)
             switch (combo) {
-                case 1: POST_PIPE(7, 2); break;
-                default: POST_PIPE(4, 3); break;
+                case 1: POST_PIPE(32, 7, 2); break;
+                case 2: POST_PIPE(32, 4, 3); break;
+                case 3: POST_PIPE(16, 4, 1); break;
+                default: POST_PIPE(16, 2, 2); break;
             }
 #undef POST_PIPE
             LAUNCH_CHECK();
-            s->post_kernel = 4; s->post_grid = grid;
+            s->post_kernel = var; s->post_grid = grid;
             return MI_OK;
         }
     one_tile:

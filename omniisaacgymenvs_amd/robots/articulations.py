@@ -276,7 +276,8 @@ class ArticulationView:
         return int(p.value), int(t.value), int(b.value)
 
     POST_KERNELS = {0: "k_loco_post_tiled<64s>", 1: "k_loco_post_tiled<64d>", 2: "k_loco_post_tiled<32s>",
-                    3: "k_loco_post_tiled<32d>", 4: "k_loco_post_pipe", 5: "k_post_step"}
+                    3: "k_loco_post_tiled<32d>", 4: "k_loco_post_pipe", 5: "k_post_step",
+                    6: "k_loco_post_pipe<16>"}
 
     def post_kernel(self) -> tuple:
         """(kernel name, grid) of the last mi_task_post_step launch (None before the first)."""

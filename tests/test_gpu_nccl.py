@@ -12,6 +12,7 @@
 Reference anchors: cfg/train/HumanoidPPO.yaml:43 (multi_gpu), :66 (horizon_length 32);
 SURVEY §8(e). The 8-GPU run itself is the driver's (SCALE); this is the same code at world 1.
 """
+import math
 import os
 
 import pytest
@@ -132,7 +133,7 @@ def test_data_parallel_learner_over_rccl(nccl_group, graphed):
     eagerly), the obs / value statistics merge through all-reduces; the result equals the single
     learner's (cfg/train/HumanoidPPO.yaml:43)."""
     n = 512
-    epochs = 3 if graphed else 1          # updates are captured from epoch 2 on
+    epochs = 2 if graphed else 1          # updates are captured from epoch 2 on (rollouts from epoch 3)
     env_m, ag_m = _agent(n, 5, True, f"dp{int(graphed)}", mode="data_parallel", graph_update=graphed)
     env_s, ag_s = _agent(n, 5, False, f"dps{int(graphed)}", graph_update=graphed)
     assert ag_m.dp and not ag_m.central and ag_m.rollout is None and ag_m.is_learner
@@ -144,8 +145,12 @@ def test_data_parallel_learner_over_rccl(nccl_group, graphed):
     torch.cuda.synchronize()
     if graphed:
         assert all(isinstance(g, tuple) for g in ag_m.upd_graphs.values()) and ag_m.upd_graphs
+    # eager: the same launches (all-reduce of one rank is the identity); graphed: the BLAS may
+    # pick other kernels under stream capture (GEMM rounding, as test_graph_update_matches_eager)
+    rel = 1e-3 if graphed else 1e-5
     for k in ("a_loss", "c_loss", "kl"):
-        assert abs(st_m[k] - st_s[k]) <= 1e-4 * max(1.0, abs(st_s[k])), (k, st_m[k], st_s[k])
+        assert math.isclose(st_m[k], st_s[k], rel_tol=rel, abs_tol=1e-6), (k, st_m[k], st_s[k])
+    assert st_m["lr"] == st_s["lr"]
     for (k, a), b in zip(ag_m.model.state_dict().items(), ag_s.model.state_dict().values()):
-        torch.testing.assert_close(a, b, rtol=1e-4, atol=1e-5, msg=k)
+        torch.testing.assert_close(a, b, rtol=1e-4, atol=1e-6, msg=k)
     env_m.close(); env_s.close()

@@ -336,8 +336,9 @@ def test_self_collision_active_on_device(gpu):
 @pytest.mark.parametrize("name", ["Humanoid", "Ant"])
 def test_pipelined_post_step_equals_one_tile(gpu, monkeypatch, name):
     """k_loco_post_pipe (MI_POST_TILE=32p: each workgroup walks several 32-env tiles and holds
-    the next tile's loads in registers) is bit-identical to the one-tile kernel (32s). A grid of
-    7 workgroups over 4113 envs forces many tiles per workgroup and a ragged last tile."""
+    the next tile's loads in registers; 16p: the same with 16-env tiles) is bit-identical to the
+    one-tile kernel (32s). A grid of 7 workgroups over 4113 envs forces many tiles per workgroup
+    and a ragged last tile."""
     env = make_env(name, num_envs=4113, device="cuda:0", seed=5)
     t = env.task
     env.reset()
@@ -351,7 +352,7 @@ def test_pipelined_post_step_equals_one_tile(gpu, monkeypatch, name):
     start = {b: getattr(t, b).clone() for b in bufs}
     h, s = t.get_robot().handle, t.get_robot().stream()
     out = {}
-    for var, grid in (("32s", None), ("32p", "7"), ("32p", None)):
+    for var, grid in (("32s", None), ("32p", "7"), ("32p", None), ("16p", "7")):
         for b in bufs:
             getattr(t, b).copy_(start[b])
         monkeypatch.setenv("MI_POST_TILE", var)
@@ -367,12 +368,13 @@ def test_pipelined_post_step_equals_one_tile(gpu, monkeypatch, name):
         out[(var, grid)] = {b: getattr(t, b).clone() for b in bufs}
         kname, kgrid = t.get_robot().post_kernel()
         # 129 tiles without MI_POST_GRID: under two tiles per resident workgroup, the one-tile kernel
-        assert kname == ("k_loco_post_pipe" if grid else "k_loco_post_tiled<32s>"), (var, grid, kname)
+        want = {"32p": "k_loco_post_pipe", "16p": "k_loco_post_pipe<16>"}.get(var) if grid else "k_loco_post_tiled<32s>"
+        assert kname == want, (var, grid, kname)
         if grid:
             assert kgrid == int(grid)
     ref = out[("32s", None)]
     assert not torch.equal(ref["obs_buf"], start["obs_buf"])
-    for key in (("32p", "7"), ("32p", None)):
+    for key in (("32p", "7"), ("32p", None), ("16p", "7")):
         for b in bufs:
             assert torch.equal(out[key][b], ref[b]), (key, b)
     env.close()

@@ -10,6 +10,7 @@
 #   bench        default bench line (N=1, Humanoid 4096)                 -> bench_default.log
 #   prof         rocprofv3 --kernel-trace --stats of the default bench   -> kernel_stats_bench_default.*
 #   fuse         obs/reward fuse sweeps Humanoid/Ant + rocprof at 1 M    -> fuse_roofline_*.json, kernel_stats_fuse_*
+#   fuseab       fuse tile variants 32p vs 16p at 1 M / 2 M envs (alternating) -> DESIGN §6
 #   fusepmc      FETCH_SIZE / WRITE_SIZE passes of the fuse at 1 M envs   -> traffic_fuse_*.json (tools/pmc_traffic.py)
 #   traffic      env-count FETCH/WRITE sweep of the fused step (TASK=..)  -> traffic_<task>.json (tools/traffic_split.py)
 #   sq           SQ issue / wait / occupancy counters of the fused step   -> sq_counters_<task>.txt
@@ -46,8 +47,8 @@ run() {  # run <name> <timeout> <cmd...>; exit codes 0/1 (test failures) continu
 recipe() {
   case "$1" in
   tests)
-    run pytest_gpu 900 python -u -m pytest tests -m gpu -q ${PYTEST_X--x} --timeout 200 --timeout-method thread ${PYTEST_K:+-k "$PYTEST_K"}
-    grep -E "^FAILED|^E  .*Error|passed|failed" gpurun_out/pytest_gpu.log | head -30 ;;
+    run pytest_gpu${PTAG:-} 900 python -u -m pytest tests -m gpu -q ${PYTEST_X--x} --timeout 200 --timeout-method thread ${PYTEST_K:+-k "$PYTEST_K"}
+    grep -E "^FAILED|^E  .*Error|passed|failed" gpurun_out/pytest_gpu${PTAG:-}.log | head -30 ;;
   smoke)
     run smoke 300 python -u -c "import __graft_entry__ as g; g.smoke()" ;;
   bench)
@@ -58,6 +59,13 @@ recipe() {
     run fuse_h 300 python -u tools/fuse_roofline.py Humanoid 4096,65536,131072,262144,1048576,2097152
     run fuse_a 300 python -u tools/fuse_roofline.py Ant 4096,65536,131072,262144,1048576,2097152
     run prof_fuse 300 $RP --kernel-trace --stats -d gpurun_out/prof_fuse -o run -- python3 tools/fuse_roofline.py Humanoid 1048576 20 ;;
+  fuseab)   # obs/reward fuse tile variants at 1 M envs, alternating (MI_POST_TILE 32p vs 16p)
+    for k in 1 2 3; do
+      for V in 32p 16p; do
+        for T in Humanoid Ant; do run fab_${V}_${T}_$k 120 env MI_POST_TILE=$V python -u tools/fuse_roofline.py $T 1048576,2097152 30; done
+      done
+    done
+    grep -h '"kernel"' gpurun_out/fab_*.log | cut -c1-200 ;;
   fusepmc)
     for T in Humanoid Ant; do
       run fpf_$T 120 timeout -s KILL 100 $RP --pmc FETCH_SIZE --kernel-trace -d gpurun_out/fpf_$T -o run -- python3 tools/fuse_roofline.py $T 1048576 10
@@ -100,10 +108,10 @@ recipe() {
   ab)   # A/B of the default library against LIB_B (another build of libmi_sim.so) or, with
         # ENV_B="VAR=value ...", against the default library under those variables; alternating
     for k in 1 2 3; do
-      run ab_a_${TASK}_$k 200 python -u bench.py --task $TASK --steps 300 --warmup 30 --no-cpu-baseline --no-side --fuse-envs 0 ${BARGS:-}
-      run ab_b_${TASK}_$k 200 env ${ENV_B:-MI_SIM_LIB=$LIB_B} python -u bench.py --task $TASK --steps 300 --warmup 30 --no-cpu-baseline --no-side --fuse-envs 0 ${BARGS:-}
+      run ab_a_${TASK}_${TAG}_$k 200 python -u bench.py --task $TASK --steps 300 --warmup 30 --no-cpu-baseline --no-side --fuse-envs 0 ${BARGS:-}
+      run ab_b_${TASK}_${TAG}_$k 200 env ${ENV_B:-MI_SIM_LIB=$LIB_B} python -u bench.py --task $TASK --steps 300 --warmup 30 --no-cpu-baseline --no-side --fuse-envs 0 ${BARGS:-}
     done
-    for f in gpurun_out/ab_[ab]_${TASK}_*.log; do echo "$f $(grep -o '"kernel_ms": [0-9.]*\|"ms_per_step": [0-9.]*\|"lds_bytes_per_env": [0-9]*' $f | head -3 | tr '\n' ' ')"; done ;;
+    for f in gpurun_out/ab_[ab]_${TASK}_${TAG}_*.log; do echo "$f $(grep -o '"kernel_ms": [0-9.]*\|"ms_per_step": [0-9.]*\|"lds_bytes_per_env": [0-9]*' $f | head -3 | tr '\n' ' ')"; done ;;
   *)
     echo "unknown recipe $1"; exit 2 ;;
   esac
