@@ -113,9 +113,6 @@ MI_D void sdof_loop(const float* Ss, const float* R, F&& fn) {
 #ifndef MI_PAIR_WIDE_PD
 #define MI_PAIR_WIDE_PD 4   // W-row prefetch depth of the wide Delassus set-up (1-4 all spill: see DESIGN)
 #endif
-#ifndef MI_PAIR_EXACT_ROWS
-#define MI_PAIR_EXACT_ROWS 1   // P9: exact-row passes when the speculative batch needs two (0: always speculative)
-#endif
 #ifndef MI_PAIR_WIDE_AREG
 #define MI_PAIR_WIDE_AREG 32   // wide-PGS Delassus rows in registers (0, 32 or 64); the rest streamed
 #endif
@@ -490,19 +487,11 @@ MI_D void pair_artic_substep(const DevModel& m, const WaveTabs& t, const DevStat
     }
     wave_sync();
     STAMP(6);
-    // ---- P7+P9: lanes over solve vectors, passes of 32 to the larger half's count. Two lane
-    // layouts, same vectors, same solves, same row order (bit-identical results):
-    //  * speculative (1 + limit candidates + contact rows fit one pass): lane 0 the rhs, lanes
-    //    1..nlim every limit candidate's unit vector (the limit test runs on lane 0's u* inside
-    //    the pass, the inactive candidates' solves are dropped), then the contact rows;
-    //  * exact (more rows: most Humanoid substeps with >= 4 contacts): the rhs alone first (one
-    //    solve, no J build or filing), the limit test, then passes over exactly the rows —
-    //    contacts, then the active limits (ceil((nc + nact) / 32) passes instead of
-    //    ceil((1 + nlim + nc) / 32) with the unused candidates).
+    // ---- P7+P9: one batch per half, lanes over solve vectors (rhs, limit candidates, contact
+    // rows); passes of 32 to the larger half's count
     const int nlim = t.nlimc;
     const int total = 1 + nlim + nc;
     const int total_max = pmax(total);
-    const bool spec = !MI_PAIR_EXACT_ROWS || total_max <= 32;  // uniform
     int nrows = nc;
     unsigned limact = 0u;
     auto limit_rows = [&](const auto& res) {
@@ -570,28 +559,11 @@ MI_D void pair_artic_substep(const DevModel& m, const WaveTabs& t, const DevStat
             }
         }
     };
-    int pass_total = total_max;
-    if (!spec) {   // exact layout: u* = u + dt M~^-1 rhs first (every lane solves the rhs), limit test
-        float x[TP::nvc];
-        sfor<0, TP::nv>([&](auto C) { x[C] = rhs[C]; });
-        float a;
-        ct_solve_l<TP, MI_PAIR_SOLVE_PD>(sm + t.s_L, x, a);
-        limit_rows(x);
-        pass_total = pmax(nrows);
-    }
-    for (int base = 0; base < pass_total; base += 32) {
+    for (int base = 0; base < total_max; base += 32) {
         const int bv = base + lane;
-        bool on;
-        int r, kd;
-        if (spec) {
-            on = bv < total;
-            r = bv - 1 - nlim;
-            kd = (on && bv > 0 && r < 0) ? nr + mc.lim(bv - 1) : -1;
-        } else {      // rows in their final order: contacts, then the active limits (s_rl: -(k + 1))
-            on = bv < nrows;
-            r = bv < nc ? bv : -1;
-            kd = (on && bv >= nc) ? (int)(-sm[t.s_rl + bv] - 1.0f) : -1;
-        }
+        const bool on = bv < total;
+        const int r = bv - 1 - nlim;
+        const int kd = (on && bv > 0 && r < 0) ? nr + mc.lim(bv - 1) : -1;
         float x[TP::nvc];
         const bool crow = on && r >= 0;
         float f[6] = {0.0f, 0.0f, 0.0f, 0.0f, 0.0f, 0.0f};
@@ -610,13 +582,13 @@ MI_D void pair_artic_substep(const DevModel& m, const WaveTabs& t, const DevStat
             float xc = (ia ? v : 0.0f) - (ib ? v : 0.0f);
             float rc = rcl;
             asm volatile("" : "+v"(xc), "+v"(rc));
-            x[c] = crow ? xc : ((spec && bv == 0) ? rc : (kd == c ? 1.0f : 0.0f));
+            x[c] = crow ? xc : (bv == 0 ? rc : (kd == c ? 1.0f : 0.0f));
         });
         STAMP(7);
         float a;
         ct_solve_l<TP, MI_PAIR_SOLVE_PD>(sm + t.s_L, x, a);
         STAMP(8);
-        if (spec && base == 0) limit_rows(x);
+        if (base == 0) limit_rows(x);
         STAMP(9);
         file_row(x, on, r, kd, a);
         STAMP(10);

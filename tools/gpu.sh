@@ -99,6 +99,8 @@ recipe() {
     for T in ${TASKS:-Humanoid}; do run tail_${T}_$TAG 150 python -u tools/pair_tail.py $T 4096 3; done ;;
   patha)
     run path_a 200 python -u tools/path_a_timing.py ;;
+  pathaprof)   # kernel trace of path (A): every backend launch and its duration
+    run prof_patha 300 $RP --kernel-trace --stats -d gpurun_out/prof_patha -o run -- python3 tools/path_a_timing.py Humanoid 4096 100 ;;
   train)
     for T in ${TASKS:-Humanoid}; do run train_${T}_$TAG 600 python -u tools/bench_train.py --task $T; done ;;
   curve)
