@@ -120,7 +120,7 @@ MI_D void sdof_loop(const float* Ss, const float* R, F&& fn) {
 #define MI_PAIR_WIDE_AP 8   // Delassus rows streamed ahead of the wide sweeps' chain
 #endif
 #ifndef MI_PAIR_SDOF_PD
-#define MI_PAIR_SDOF_PD 4   // DOF-loop prefetch depth (sdof_loop): 2 -> 0.1609 ms, 4 -> 0.1592 (A/B)
+#define MI_PAIR_SDOF_PD 6   // DOF-loop prefetch depth (sdof_loop): 2 -> 0.1609 ms, 4 -> 0.1592 (A/B, round 3); 6: 0.1356 -> 0.1349 (round 4)
 #endif
 
 // J_r[c] of this lane's constraint row r (contact or limit), for every DOF c (lane = row)
@@ -169,19 +169,20 @@ MI_D int pw_idx(int r, int c, int nv) { return (r & ~3) * nv + 4 * c + (r & 3); 
 MI_D lds_cf4 pw_group(const WaveTabs& t, const float* sm, int g0, int nv) {
     return (lds_cf4)(sm + t.s_W + g0 * nv);
 }
-// slab row r (rows >= w_rows_lds; row-major, stride WNV)
-MI_D const float* pair_srow(const float* gW, int r) { return gW + (size_t)r * WNV; }
+// The env's global W slab (rows >= w_rows_lds, up to MI_MAX_ROWS) uses the same 4-row groups,
+// WNV (32) columns: entry (r, c) at (r & ~3) WNV + 4 c + (r & 3), so a slab group is one
+// global_load_dwordx4 per DOF as well (column WNV - 1 is the fallback sweeps' lambda slot)
+MI_D size_t pair_sidx(int r, int c) { return (size_t)(r & ~3) * WNV + 4 * c + (r & 3); }
+typedef const pv4* glb_cf4;
 
 // Delassus entries A[r][g0 + q] = J_r . W_{g0+q}, q < 4, of this lane's row r (the PGS set-up of
 // both widths), the loads of DOF c + PD issued before DOF c's FMAs (a ring indexed at compile
-// time, see sdof_loop). The env has n rows; group rows past them are 0 in LDS (they hold stale
-// data there, finite or not, and the sweeps only ever scale them by a zero lambda change) and
-// repeat row n - 1 in the slab.
+// time, see sdof_loop). The env has n rows; group rows past them are 0 (they hold stale data,
+// finite or not, and the sweeps only ever scale them by a zero lambda change).
 template <class TP, int PD>
 MI_D void pair_dgroup(const WaveTabs& t, const float* sm, const float* gW, int g0, int n,
                       const float (&Jr)[TP::nvc], float (&a)[4]) {
     constexpr int NV = TP::nv, NB = PD + 1;
-    const int last = max(n - 1, 0);
     float a0 = 0.0f, a1 = 0.0f, a2 = 0.0f, a3 = 0.0f;
     if (g0 + 3 < t.w_rows_lds) {   // uniform: the group in LDS, one ds_read_b128 per DOF
         const lds_cf4 W = pw_group(t, sm, g0, NV);
@@ -195,43 +196,32 @@ MI_D void pair_dgroup(const WaveTabs& t, const float* sm, const float* gW, int g
             a2 += Jr[C] * wb[c % NB].z;
             a3 += Jr[C] * wb[c % NB].w;
         });
-        a[0] = g0 < n ? a0 : 0.0f;
-        a[1] = g0 + 1 < n ? a1 : 0.0f;
-        a[2] = g0 + 2 < n ? a2 : 0.0f;
-        a[3] = g0 + 3 < n ? a3 : 0.0f;
-    } else {                       // the slab (rows clamped to the env's last row)
-        const float* w0 = pair_srow(gW, min(g0, last));
-        const float* w1 = pair_srow(gW, min(g0 + 1, last));
-        const float* w2 = pair_srow(gW, min(g0 + 2, last));
-        const float* w3 = pair_srow(gW, min(g0 + 3, last));
-        float wb[NB][4];
-        auto ld = [&](auto C) {
-            constexpr int c = C;
-            wb[c % NB][0] = w0[c]; wb[c % NB][1] = w1[c]; wb[c % NB][2] = w2[c]; wb[c % NB][3] = w3[c];
-        };
-        sfor<0, (PD < NV ? PD : NV)>([&](auto C) { ld(C); });
+    } else {                       // the slab: one global_load_dwordx4 per DOF
+        const glb_cf4 W = (glb_cf4)(gW + (size_t)g0 * WNV);
+        pv4 wb[NB];
+        sfor<0, (PD < NV ? PD : NV)>([&](auto C) { wb[C % NB] = W[C]; });
         sfor<0, NV>([&](auto C) {
             constexpr int c = C;
-            if constexpr (c + PD < NV) ld(std::integral_constant<int, c + PD>{});
-            a0 += Jr[C] * wb[c % NB][0];
-            a1 += Jr[C] * wb[c % NB][1];
-            a2 += Jr[C] * wb[c % NB][2];
-            a3 += Jr[C] * wb[c % NB][3];
+            if constexpr (c + PD < NV) wb[(c + PD) % NB] = W[c + PD];
+            a0 += Jr[C] * wb[c % NB].x;
+            a1 += Jr[C] * wb[c % NB].y;
+            a2 += Jr[C] * wb[c % NB].z;
+            a3 += Jr[C] * wb[c % NB].w;
         });
-        a[0] = a0; a[1] = a1; a[2] = a2; a[3] = a3;
     }
+    a[0] = g0 < n ? a0 : 0.0f;
+    a[1] = g0 + 1 < n ? a1 : 0.0f;
+    a[2] = g0 + 2 < n ? a2 : 0.0f;
+    a[3] = g0 + 3 < n ? a3 : 0.0f;
 }
 
-// W entries of rows g0..g0+3 at this lane's DOF kc (the u update of both PGS widths)
-MI_D void pair_wcol(const WaveTabs& t, const float* sm, const float* gW, int g0, int last, int kc,
-                    int nv, float (&wq)[4]) {
-    if (g0 + 3 < t.w_rows_lds) {
-        const pv4 w = pw_group(t, sm, g0, nv)[kc];
-        wq[0] = w.x; wq[1] = w.y; wq[2] = w.z; wq[3] = w.w;
-    } else {
-#pragma unroll
-        for (int q = 0; q < 4; ++q) wq[q] = pair_srow(gW, min(g0 + q, last))[kc];
-    }
+// W entries of rows g0..g0+3 at this lane's DOF kc (the u update of both PGS widths; rows past
+// the env's count are read but never used: the caller selects them away)
+MI_D void pair_wcol(const WaveTabs& t, const float* sm, const float* gW, int g0, int kc, int nv,
+                    float (&wq)[4]) {
+    const pv4 w = g0 + 3 < t.w_rows_lds ? pw_group(t, sm, g0, nv)[kc]
+                                        : ((glb_cf4)(gW + (size_t)g0 * WNV))[kc];
+    wq[0] = w.x; wq[1] = w.y; wq[2] = w.z; wq[3] = w.w;
 }
 
 // One articulated substep of the env of this lane's half (env i, LDS region sm, W slab gW).
@@ -555,7 +545,7 @@ MI_D void pair_artic_substep(const DevModel& m, const WaveTabs& t, const DevStat
                     if (c < TP::nv) wl[4 * c] = res[c] * sc;
             } else {
 #pragma unroll
-                for (int c = 0; c < WNV; ++c) gW[(size_t)slot * WNV + c] = c < NR ? res[c] * sc : 0.0f;
+                for (int c = 0; c < WNV; ++c) gW[pair_sidx(slot, c)] = c < NR ? res[c] * sc : 0.0f;
             }
         }
     };
@@ -677,7 +667,7 @@ MI_D void pair_artic_substep(const DevModel& m, const WaveTabs& t, const DevStat
             constexpr int g0 = 4 * G;
             if (g0 < nrows_max) {
                 float wq[4];
-                pair_wcol(t, sm, gW, g0, last, kc, NV, wq);
+                pair_wcol(t, sm, gW, g0, kc, NV, wq);
 #pragma unroll
                 for (int q = 0; q < 4; ++q) u = g0 + q < nrows ? u + wq[q] * lamv[g0 + q] : u;
             }
@@ -801,7 +791,7 @@ MI_D void pair_artic_substep(const DevModel& m, const WaveTabs& t, const DevStat
                 constexpr int g0 = 4 * G;
                 if (g0 < nrh) {
                     float wq[4];
-                    pair_wcol(t, smh, gWh, g0, last, kc, NV, wq);
+                    pair_wcol(t, smh, gWh, g0, kc, NV, wq);
 #pragma unroll
                     for (int q = 0; q < 4; ++q) {
                         const float lq = readlane(lam, g0 + q);
@@ -858,9 +848,9 @@ MI_D void pair_artic_substep(const DevModel& m, const WaveTabs& t, const DevStat
         const float* wsm = sm;
         const float* wgW = gW;
         auto wrow = [&](int rr) {
-            return (rr < t.w_rows_lds ? wsm[t.s_W + pw_idx(rr, kc, nv)] : wgW[(size_t)rr * WNV + kc]) * kin;
+            return (rr < t.w_rows_lds ? wsm[t.s_W + pw_idx(rr, kc, nv)] : wgW[pair_sidx(rr, kc)]) * kin;
         };
-        for (int r = 64 + lane; r < nrows; r += 32) gW[(size_t)r * WNV + (WNV - 1)] = 0.0f;
+        for (int r = 64 + lane; r < nrows; r += 32) gW[pair_sidx(r, WNV - 1)] = 0.0f;
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
         STAMP(27);
@@ -925,7 +915,7 @@ MI_D void pair_artic_substep(const DevModel& m, const WaveTabs& t, const DevStat
                 }
                 jc *= kin;
                 const float jv = psum(jc * u);
-                float* lp = gW + (size_t)rs * WNV + (WNV - 1);
+                float* lp = gW + pair_sidx(rs, WNV - 1);
                 const float l0 = live_row ? *lp : 0.0f;
                 float ln = l0 + (br - jv) * (1.0f / ar);
                 const bool fric = kind == 1 || kind == 2;
@@ -934,7 +924,7 @@ MI_D void pair_artic_substep(const DevModel& m, const WaveTabs& t, const DevStat
                 ln = fric ? fminf(ln, lim) : ln;
                 if (live_row) {
                     lamn = kind == 0 ? ln : lamn;
-                    u += gW[(size_t)rs * WNV + kc] * kin * (ln - l0);
+                    u += gW[pair_sidx(rs, kc)] * kin * (ln - l0);
                 }
                 __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
                 if (live_row && lane == 0) *lp = ln;
@@ -945,7 +935,7 @@ MI_D void pair_artic_substep(const DevModel& m, const WaveTabs& t, const DevStat
         if (lane < nv) us[lane] = u;
         if (lane < nrows) sm[t.s_ad + lane] = lam0;          // reuse: lambda of row lane
         if (lane + 32 < nrows) sm[t.s_ad + lane + 32] = lam1;
-        for (int r = 64 + lane; r < nrows; r += 32) sm[t.s_ad + r] = gW[(size_t)r * WNV + (WNV - 1)];
+        for (int r = 64 + lane; r < nrows; r += 32) sm[t.s_ad + r] = gW[pair_sidx(r, WNV - 1)];
 #endif
     }
     wave_sync();

@@ -770,8 +770,13 @@ __device__ __forceinline__ bool pair_live(int N) {
 }
 #define MI_PAIR_OCC __attribute__((amdgpu_waves_per_eu(2, 2)))
 
+// row-major state mirrors (mi_sim_set_mirror) a physics launch refreshes itself: pos, quat, vel,
+// q, qd, sensor wrenches; p[0] == nullptr: none
+struct Mirrors { float* p[6]; };
+
 template <class T>
-__global__ __launch_bounds__(512) MI_PAIR_OCC void k_sim_step_pair(const KParams* __restrict__ kp, int substeps) {
+__global__ __launch_bounds__(512) MI_PAIR_OCC void k_sim_step_pair(const KParams* __restrict__ kp, int substeps,
+                                                    Mirrors mir) {
     extern __shared__ __attribute__((aligned(16))) float smem[];
     const WaveTabs& t = kp->t;
     const int i = pair_env();
@@ -783,6 +788,22 @@ __global__ __launch_bounds__(512) MI_PAIR_OCC void k_sim_step_pair(const KParams
     for (int s = 0; s < substeps; ++s) {
         const KParams* k = opaque_kp(kp);
         pair_artic_substep<T>(k->m, k->t, k->st, k->p, i, smem, sm, gW, s == 0, s == substeps - 1, prio);
+    }
+    // World.step() then the getters (locomotion.py:81-89): the final state is still in LDS, so the
+    // launch writes the getters' row-major mirrors itself (the same values it stored to the
+    // state) and the mirror refresh launch is not needed
+    if (mir.p[0]) {
+        const KParams* k = opaque_kp(kp);
+        const int lane = (int)(threadIdx.x & 31u), D = k->m.D, nr = k->m.nr, S6 = 6 * k->m.S;
+        const WaveTabs& tk = k->t;
+        if (lane < 3) mir.p[0][3 * i + lane] = sm[tk.s_rp + lane];
+        if (lane < 4) mir.p[1][4 * i + lane] = sm[tk.s_rp + 4 + lane];
+        if (lane < 6) mir.p[2][6 * i + lane] = sm[tk.s_us + lane];
+        if (lane < D) {
+            mir.p[3][(size_t)D * i + lane] = sm[tk.s_q + lane];
+            mir.p[4][(size_t)D * i + lane] = sm[tk.s_us + nr + lane];
+        }
+        for (int c = lane; c < S6; c += 32) mir.p[5][(size_t)S6 * i + c] = sm[tk.s_rb + c];
     }
 }
 
@@ -1534,12 +1555,20 @@ int mi_sim_info(const mi_sim* s, int32_t* num_envs, int32_t* num_dof, int32_t* n
 
 static int launch_sim(mi_sim* s, int substeps, hipStream_t stream) {
     s->mir_valid = false;
+    bool mirrored = false;
     if (s->wave)
         with_topo(s->topo, [&](auto T) {
             if constexpr (has_pair<decltype(T)>()) {
                 if (s->pair) {
+                    // the paired kernel refreshes the mirrors itself (free-root models: the
+                    // state it writes is the mirrors' whole content)
+                    Mirrors mir{};
+                    if (s->mir[0] && s->dm.nr == 6 && (s->dm.S == 0 || s->mir[5])) {
+                        for (int k = 0; k < 6; ++k) mir.p[k] = s->mir[k];
+                        mirrored = true;
+                    }
                     hipLaunchKernelGGL(k_sim_step_pair<decltype(T)>, wave_grid(s), wave_block(s), s->lds_bytes,
-                                       stream, (const KParams*)s->kp_dev, substeps);
+                                       stream, (const KParams*)s->kp_dev, substeps, mir);
                     return;
                 }
             }
@@ -1550,6 +1579,12 @@ static int launch_sim(mi_sim* s, int substeps, hipStream_t stream) {
         hipLaunchKernelGGL(k_sim_step, grid_for(s, s->N), dim3(s->block), 0, stream, s->dm, s->ds,
                            s->sp, substeps);
     LAUNCH_CHECK();
+    if (mirrored) {   // valid after this launch, in stream order (mi_get_state_mirror)
+        if (!s->mir_ev) HIP_TRY(hipEventCreateWithFlags(&s->mir_ev, hipEventDisableTiming));
+        HIP_TRY(hipEventRecord(s->mir_ev, stream));
+        s->mir_stream = stream;
+        s->mir_valid = true;
+    }
     return MI_OK;
 }
 
