@@ -29,8 +29,8 @@ extern "C" {
 #define MI_RL_ABI_VERSION 1
 
 int32_t mi_rl_abi_version(void);
-/* SHA-256 (hex) of the sources this library was compiled from (csrc/mi_rl.hip, csrc/*.hpp,
- * include/*.h; __graft_entry__.source_hash), as mi_build_id of libmi_sim.so. */
+/* SHA-256 (hex) of the sources this library was compiled from (csrc/mi_rl.hip, the csrc .hpp headers,
+ * the include headers; __graft_entry__.source_hash), as mi_build_id of libmi_sim.so. */
 const char* mi_rl_build_id(void);
 const char* mi_rl_last_error(void);
 

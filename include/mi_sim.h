@@ -302,8 +302,8 @@ int mi_sim_nan_count(mi_sim* sim, int64_t* count);
  * lds_bytes: LDS per env (= per workgroup) of the wave path. Any output may be NULL. */
 int mi_sim_kernel_path(const mi_sim* sim, int32_t* path, int32_t* topology, int32_t* lds_bytes);
 int mi_abi_version(void);
-/* SHA-256 (hex) of the sources this library was compiled from: csrc/mi_sim.hip, csrc/*.hpp and
- * include/*.h in name order (__graft_entry__.source_hash); "unknown" when built without it. A
+/* SHA-256 (hex) of the sources this library was compiled from: csrc/mi_sim.hip, the csrc .hpp headers and
+ * the include headers in name order (__graft_entry__.source_hash); "unknown" when built without it. A
  * stale binary shows up as a mismatch against the tree (smoke(), tests/test_host.py). */
 const char* mi_build_id(void);
 const char* mi_last_error(void);

@@ -611,7 +611,7 @@ MI_D void pair_artic_substep(const DevModel& m, const WaveTabs& t, const DevStat
         else sfor<0, NV>([&](auto C) { Jr[C] = 0.0f; });
         float v = 0.0f;
         sfor<0, NV>([&](auto C) { v += Jr[C] * us[C]; });
-        const int last = max(nrows - 1, 0);
+        STAMP(24);
         float Ar[RMAX];
         static_assert(RMAX % 4 == 0, "Delassus rows are built four at a time");
         sfor<0, RMAX / 4>([&](auto G) {
@@ -620,6 +620,7 @@ MI_D void pair_artic_substep(const DevModel& m, const WaveTabs& t, const DevStat
             if (g0 < nrows_max) pair_dgroup<TP, MI_PAIR_SDOF_PD>(t, sm, gW, g0, nrows, Jr, a);
             Ar[g0] = a[0]; Ar[g0 + 1] = a[1]; Ar[g0 + 2] = a[2]; Ar[g0 + 3] = a[3];
         });
+        STAMP(25);
         // lane r's own row: bias, 1 / A_rr, kind (contact rows are (normal, friction, friction)
         // triples 3c..3c+2, then the limit rows)
         float b = 0.0f, ia = 0.0f;   // ia 0: a dead row's projection keeps its lambda 0
@@ -709,7 +710,6 @@ MI_D void pair_artic_substep(const DevModel& m, const WaveTabs& t, const DevStat
             if (nrh == 0) continue;
             float* smh = sm + (h - me) * t.env_stride;                 // env of half h
             const float* gWh = gW + (ptrdiff_t)(h - me) * (ptrdiff_t)t.g_row_stride;
-            const int last = nrh - 1;
             const int rl = l64 < nrh ? l64 : 0;
             float Jr[TP::nvc];
             pair_jrow<TP>(mc, t, smh, rl, nr, Jr);
@@ -1220,12 +1220,43 @@ MI_D void pair_loco_post(const DevModel& m, const WaveTabs& t, const DevState& s
     }
     for (int k = lane; k < 6 * S; k += 32) put(12 + 2 * D + k, sm[t.s_rb + k] * tp.contact_force_scale);
     wave_sync();
-    if (lane == 0) {
+    // The three DOF-order reward sums (limit, action, electricity; ref humanoid.py / ant.py
+    // calculate_metrics) run side by side on lanes 0..2 of each half: one instruction stream with
+    // a per-lane base, each sum still accumulated in DOF order. Ant's limit count sums 0/1 floats,
+    // exact far below 2^24, so it equals the reference's integer count.
+    float part = 0.0f;
+    if (lane < 3) {
+        const float* tb = terms + (lane == 0 ? 2 * D : (lane == 1 ? 0 : D));
+        for (int j = 0; j < D; ++j) part += tb[j];
+    }
+    const float limit_cost = __shfl(part, h0), act_cost = __shfl(part, h0 + 1),
+                elec = __shfl(part, h0 + 2);
+    if (lane < 3) {
+        // lanes 0..2 share the root-frame prelude (same LDS words, same arithmetic), then run the
+        // three angle chains of observations 7..9 side by side: yaw, roll and the walk-target
+        // angle each go through one atan2 (+ fmod for the Euler angles) and normalize_angle,
+        // instead of lane 0 running six atan2 and three sin/cos in sequence.
         float rp[3], rq[4], rv[6];
 #pragma unroll
         for (int k = 0; k < 3; ++k) rp[k] = sm[t.s_rp + k];
 #pragma unroll
         for (int k = 0; k < 4; ++k) rq[k] = sm[t.s_rp + 4 + k];
+        const float inv_start[4] = {1.0f, -0.0f, -0.0f, -0.0f};
+        float tq[4];
+        ref_quat_mul(rq, inv_start, tq);
+        float ay, ax;
+        if (lane < 2) {
+            ref_euler_atan2_args(tq, lane, ay, ax);
+        } else {
+            ay = tp.target[2] - rp[2];
+            ax = tp.target[0] - rp[0];
+        }
+        float ang = atan2f(ay, ax);
+        if (lane < 2) ang = ref_fmod_pos(ang, 6.283185307179586f);
+        const float yaw = __shfl(ang, h0);
+        if (lane == 2) ang = ang - yaw;                          // angle_to_target = walk - yaw
+        put(7 + lane, ref_normalize_angle(ang));
+        if (lane != 0) return;
 #pragma unroll
         for (int k = 0; k < 6; ++k) rv[k] = us[k];
         float tt[3] = {tp.target[0] - rp[0], tp.target[1] - rp[1], tp.target[2] - rp[2]};
@@ -1233,9 +1264,6 @@ MI_D void pair_loco_post(const DevModel& m, const WaveTabs& t, const DevState& s
         const float prev_p = potentials[i];
         const float nrm = sqrtf(tt[0] * tt[0] + tt[1] * tt[1] + tt[2] * tt[2]);
         const float new_p = -nrm / tp.task_dt;
-        const float inv_start[4] = {1.0f, -0.0f, -0.0f, -0.0f};
-        float tq[4];
-        ref_quat_mul(rq, inv_start, tq);
         const float b0[3] = {1.0f, 0.0f, 0.0f}, b1[3] = {0.0f, 0.0f, 1.0f};
         float up[3], hd[3];
         ref_quat_rotate<false>(tq, b1, up);
@@ -1247,35 +1275,18 @@ MI_D void pair_loco_post(const DevModel& m, const WaveTabs& t, const DevState& s
         float vl[3], al[3];
         ref_quat_rotate<true>(tq, rv, vl);
         ref_quat_rotate<true>(tq, rv + 3, al);
-        float roll, pitch, yaw;
-        ref_get_euler_xyz(tq, roll, pitch, yaw);
-        const float walk = atan2f(tp.target[2] - rp[2], tp.target[0] - rp[0]);
-        const float angle_to_target = walk - yaw;
         const float o10 = up[2], o11 = heading_proj;
         put(0, rp[2]);
         put(1, vl[0]); put(2, vl[1]); put(3, vl[2]);
         put(4, al[0] * tp.angular_velocity_scale);
         put(5, al[1] * tp.angular_velocity_scale);
         put(6, al[2] * tp.angular_velocity_scale);
-        put(7, ref_normalize_angle(yaw));
-        put(8, ref_normalize_angle(roll));
-        put(9, ref_normalize_angle(angle_to_target));
         put(10, o10);
         put(11, o11);
         potentials[i] = new_p;
         prev_potentials[i] = prev_p;
-        float limit_cost = 0.0f, act_cost = 0.0f, elec = 0.0f;
-        if (tp.kind == MI_TASK_HUMANOID) {
-            for (int j = 0; j < D; ++j) limit_cost += terms[2 * D + j];
-        } else {
-            int64_t cnt = 0;
-            for (int j = 0; j < D; ++j) cnt += terms[2 * D + j] != 0.0f;
-            limit_cost = (float)cnt;
-        }
         const float heading = o11 > 0.8f ? tp.heading_weight : tp.heading_weight * o11 / 0.8f;
         const float upr = o10 > 0.93f ? 0.0f + tp.up_weight : 0.0f;
-        for (int j = 0; j < D; ++j) act_cost += terms[j];
-        for (int j = 0; j < D; ++j) elec += terms[D + j];
         float total = (new_p - prev_p) + tp.alive_reward_scale + upr + heading -
                       tp.actions_cost * act_cost - tp.energy_cost * elec - limit_cost;
         if (rp[2] < tp.termination_height) total = tp.death_cost;

@@ -69,6 +69,20 @@ MI_D void ref_get_euler_xyz(const float* q, float& roll, float& pitch, float& ya
     yaw = ref_fmod_pos(yw, two_pi);
 }
 
+/* The atan2 arguments of get_euler_xyz's yaw (k = 0) and roll (k = 1), evaluated exactly as in
+ * ref_get_euler_xyz, so lanes can run the angle chains side by side (mi_pair.hpp). */
+MI_D void ref_euler_atan2_args(const float* q, int k, float& sy, float& sx) {
+#pragma clang fp contract(off)
+    float w = q[0], x = q[1], y = q[2], z = q[3];
+    if (k == 0) {
+        sy = 2.0f * (w * z + x * y);
+        sx = w * w + x * x - y * y - z * z;
+    } else {
+        sy = 2.0f * (w * x + y * z);
+        sx = w * w - x * x - y * y + z * z;
+    }
+}
+
 MI_D float ref_normalize_angle(float x) { return atan2f(sinf(x), cosf(x)); }
 
 MI_D float ref_unscale(float x, float l, float u) {

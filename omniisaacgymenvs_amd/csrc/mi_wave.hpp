@@ -1170,11 +1170,10 @@ MI_D void wave_artic_substep(const DevModel& m, const WaveTabs& t, const DevStat
             constexpr int NV = TP::nv;
             constexpr int RMAX = TP::kLamRows;                      // rows of this path
             const float* sJ = sm + t.s_J;
-            float b = 0.0f, ia = 1.0f, kd = 0.0f, lam = 0.0f;
+            float b = 0.0f, ia = 1.0f, lam = 0.0f;   // row kinds follow from the row index
             if (lane < nrows) {
                 b = sm[t.s_rb + lane];
                 ia = 1.0f / sm[t.s_ad + lane];
-                kd = sm[t.s_rk + lane];
             }
             const int rl = lane < nrows ? lane : 0;
             float Jr[NV];

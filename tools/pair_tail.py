@@ -57,10 +57,12 @@ def main():
     a = np.concatenate(rows).astype(np.float64)          # [waves x launches, 32]
     phases = dict(PHASES)
     phases[11] = "P10 pgs: u update"
-    phases[27] = "P10 pgs: set-up (Delassus rows / W registers)"
+    phases[27] = "P10 set-up: wide Delassus rows / narrow row data"
     phases[28] = "P10 pgs: sweeps"
     phases[29] = "P10 wide: entry (P9 tail, syncs)"
     phases[30] = "P10 wide: J rows + v"
+    phases[24] = "P10 narrow: J row + v"
+    phases[25] = "P10 narrow: Delassus rows"
     ph = [k for k in phases if k != 5]
     tot = a[:, ph].sum(axis=1)
     order = np.argsort(tot)
