@@ -119,6 +119,9 @@ MI_D void sdof_loop(const float* Ss, const float* R, F&& fn) {
 #ifndef MI_PAIR_WIDE_AP
 #define MI_PAIR_WIDE_AP 8   // Delassus rows streamed ahead of the wide sweeps' chain
 #endif
+#ifndef MI_PAIR_UPD_PD
+#define MI_PAIR_UPD_PD 3   // W-group prefetch depth of the PGS u update (pair_u_update)
+#endif
 #ifndef MI_PAIR_SDOF_PD
 #define MI_PAIR_SDOF_PD 6   // DOF-loop prefetch depth (sdof_loop): 2 -> 0.1609 ms, 4 -> 0.1592 (A/B, round 3); 6: 0.1356 -> 0.1349 (round 4)
 #endif
@@ -216,12 +219,40 @@ MI_D void pair_dgroup(const WaveTabs& t, const float* sm, const float* gW, int g
 }
 
 // W entries of rows g0..g0+3 at this lane's DOF kc (the u update of both PGS widths; rows past
-// the env's count are read but never used: the caller selects them away)
-MI_D void pair_wcol(const WaveTabs& t, const float* sm, const float* gW, int g0, int kc, int nv,
-                    float (&wq)[4]) {
-    const pv4 w = g0 + 3 < t.w_rows_lds ? pw_group(t, sm, g0, nv)[kc]
-                                        : ((glb_cf4)(gW + (size_t)g0 * WNV))[kc];
-    wq[0] = w.x; wq[1] = w.y; wq[2] = w.z; wq[3] = w.w;
+// the env's count are read — in bounds: LDS group or slab — but never used: the caller selects
+// them away)
+MI_D pv4 pair_wcol(const WaveTabs& t, const float* sm, const float* gW, int g0, int kc, int nv) {
+    return g0 + 3 < t.w_rows_lds ? pw_group(t, sm, g0, nv)[kc] : ((glb_cf4)(gW + (size_t)g0 * WNV))[kc];
+}
+
+// u = u* + sum_r W_r lambda_r at this lane's DOF kc, in row order, rows in groups of four
+// (groups below ng_max, wave-uniform; rows from n on selected away), each group's W load issued
+// UP groups ahead of its FMAs: in line, every group exposed a full LDS or slab round trip.
+// lam(R) = lambda of row R (a compile-time row).
+template <int NG, int UP, class LF>
+MI_D float pair_u_update(const WaveTabs& t, const float* sm, const float* gW, int kc, int nv, int n,
+                         int ng_max, float u, LF&& lam) {
+    constexpr int NB = UP + 1;
+    pv4 wb[NB];
+    sfor<0, (UP < NG ? UP : NG)>([&](auto G) {
+        if (G < ng_max) wb[G % NB] = pair_wcol(t, sm, gW, 4 * G, kc, nv);
+    });
+    sfor<0, NG>([&](auto G) {
+        constexpr int g = G, g0 = 4 * g;
+        if (g < ng_max) {
+            if constexpr (g + UP < NG) {
+                if (g + UP < ng_max) wb[(g + UP) % NB] = pair_wcol(t, sm, gW, g0 + 4 * UP, kc, nv);
+            }
+            const pv4 w = wb[g % NB];
+            const float wq[4] = {w.x, w.y, w.z, w.w};
+            sfor<0, 4>([&](auto Q) {
+                constexpr int q = Q;
+                const float lq = lam(std::integral_constant<int, g0 + q>{});
+                u = g0 + q < n ? u + wq[q] * lq : u;
+            });
+        }
+    });
+    return u;
 }
 
 // One articulated substep of the env of this lane's half (env i, LDS region sm, W slab gW).
@@ -477,16 +508,20 @@ MI_D void pair_artic_substep(const DevModel& m, const WaveTabs& t, const DevStat
     }
     wave_sync();
     STAMP(6);
-    // ---- P7+P9: one batch per half, lanes over solve vectors (rhs, limit candidates, contact
-    // rows); passes of 32 to the larger half's count
+    // ---- P7+P9: one batch per half, lanes over solve vectors: the contact rows first (lane =
+    // row in the first pass, as in the P10 Delassus set-up, which then takes their J rows from
+    // this pass's registers instead of rebuilding them), then the rhs, then the limit
+    // candidates; passes of 32 to the larger half's count
     const int nlim = t.nlimc;
     const int total = 1 + nlim + nc;
     const int total_max = pmax(total);
     int nrows = nc;
     unsigned limact = 0u;
-    auto limit_rows = [&](const auto& res) {
+    // res: the rhs lane's solve (unconstrained acceleration); here: the rhs sits in this pass for
+    // this half (half-uniform; the halves' rhs may sit in different passes)
+    auto limit_rows = [&](const auto& res, bool here, bool rhs_lane) {
         constexpr int NR = sizeof(res) / sizeof(res[0]);
-        if (lane == 0) {
+        if (rhs_lane) {
 #pragma unroll
             for (int c = 0; c < NR; ++c)
                 if (c < TP::nv) us[c] = us[c] + dt * res[c];
@@ -494,7 +529,7 @@ MI_D void pair_artic_substep(const DevModel& m, const WaveTabs& t, const DevStat
         wave_sync();
         bool act = false;
         float bl = 0.0f, sg = 0.0f;
-        if (lane < D) {
+        if (here && lane < D) {
             const int l = lane + 1, k = nr + lane;
             const float lo = mc.lf(MC_LO, l), hi = mc.lf(MC_HI, l);
             if (lo < hi) {
@@ -507,7 +542,8 @@ MI_D void pair_artic_substep(const DevModel& m, const WaveTabs& t, const DevStat
                 if (bl > p.max_depen) bl = p.max_depen;
             }
         }
-        limact = hballot(act);
+        const unsigned lb = hballot(act);
+        if (here) limact = lb;
         if (act) {
             const int rl = nc + __popc(limact & lanemask_lt(lane));
             sm[t.s_rl + rl] = -(float)(nr + lane) - 1.0f;
@@ -549,13 +585,14 @@ MI_D void pair_artic_substep(const DevModel& m, const WaveTabs& t, const DevStat
             }
         }
     };
+    float Jc[TP::nvc];   // J rows of contact rows 0..31 (first pass): the narrow PGS set-up's
     for (int base = 0; base < total_max; base += 32) {
         const int bv = base + lane;
         const bool on = bv < total;
-        const int r = bv - 1 - nlim;
-        const int kd = (on && bv > 0 && r < 0) ? nr + mc.lim(bv - 1) : -1;
+        const bool crow = on && bv < nc;
+        const int r = crow ? bv : -1;
+        const int kd = (on && bv > nc) ? nr + mc.lim(bv - nc - 1) : -1;
         float x[TP::nvc];
-        const bool crow = on && r >= 0;
         float f[6] = {0.0f, 0.0f, 0.0f, 0.0f, 0.0f, 0.0f};
         unsigned msk = 0u, msk2 = 0u;
         if (crow) {
@@ -572,13 +609,15 @@ MI_D void pair_artic_substep(const DevModel& m, const WaveTabs& t, const DevStat
             float xc = (ia ? v : 0.0f) - (ib ? v : 0.0f);
             float rc = rcl;
             asm volatile("" : "+v"(xc), "+v"(rc));
-            x[c] = crow ? xc : (bv == 0 ? rc : (kd == c ? 1.0f : 0.0f));
+            x[c] = crow ? xc : (bv == nc ? rc : (kd == c ? 1.0f : 0.0f));
         });
+        if (base == 0) sfor<0, TP::nv>([&](auto C) { Jc[C] = x[C]; });
         STAMP(7);
         float a;
         ct_solve_l<TP, MI_PAIR_SOLVE_PD>(sm + t.s_L, x, a);
         STAMP(8);
-        if (base == 0) limit_rows(x);
+        const bool rhs_here = base <= nc && nc < base + 32;
+        if (pmax(rhs_here ? 1 : 0)) limit_rows(x, rhs_here, bv == nc);
         STAMP(9);
         file_row(x, on, r, kd, a);
         STAMP(10);
@@ -605,10 +644,19 @@ MI_D void pair_artic_substep(const DevModel& m, const WaveTabs& t, const DevStat
         // cross-lane broadcast (v_r) instead of five.
         constexpr int NV = TP::nv;
         constexpr int RMAX = TP::kLamRows;
-        const int rl = lane < nrows ? lane : 0;
+        // J_r: a contact row's from P9's first pass (same lane), a limit row's sg e_k; a dead
+        // lane's 0 (v 0: its projection keeps lambda 0)
         float Jr[TP::nvc];
-        if (nrows > 0) pair_jrow<TP>(mc, t, sm, rl, nr, Jr);
-        else sfor<0, NV>([&](auto C) { Jr[C] = 0.0f; });
+        {
+            int kdof = -1;
+            float sg = 0.0f;
+            if (lane >= nc && lane < nrows) {
+                kdof = (int)(-sm[t.s_rl + lane] - 1.0f);
+                sg = sm[t.s_lsg + kdof - nr];
+            }
+            const bool own = lane < nc;
+            sfor<0, NV>([&](auto C) { Jr[C] = own ? Jc[C] : (kdof == C ? sg : 0.0f); });
+        }
         float v = 0.0f;
         sfor<0, NV>([&](auto C) { v += Jr[C] * us[C]; });
         STAMP(24);
@@ -662,17 +710,10 @@ MI_D void pair_artic_substep(const DevModel& m, const WaveTabs& t, const DevStat
             });
         }
         STAMP(28);
-        float u = lane < NV ? us[lane] : 0.0f;
         const int kc = lane < NV ? lane : 0;
-        sfor<0, RMAX / 4>([&](auto G) {
-            constexpr int g0 = 4 * G;
-            if (g0 < nrows_max) {
-                float wq[4];
-                pair_wcol(t, sm, gW, g0, kc, NV, wq);
-#pragma unroll
-                for (int q = 0; q < 4; ++q) u = g0 + q < nrows ? u + wq[q] * lamv[g0 + q] : u;
-            }
-        });
+        const float u = pair_u_update<RMAX / 4, MI_PAIR_UPD_PD>(
+            t, sm, gW, kc, NV, nrows, (nrows_max + 3) >> 2, lane < NV ? us[lane] : 0.0f,
+            [&](auto R) { return lamv[R]; });
         if (lane < NV) us[lane] = u;
         wave_sync();
         {   // reuse: lambda of row rr, written by lane rr (one select chain, one store)
@@ -786,19 +827,9 @@ MI_D void pair_artic_substep(const DevModel& m, const WaveTabs& t, const DevStat
             }
             STAMP(28);
             // u = u* + sum_r W_r lambda_r, lane = DOF
-            float u = ush[kc];
-            sfor<0, 16>([&](auto G) {
-                constexpr int g0 = 4 * G;
-                if (g0 < nrh) {
-                    float wq[4];
-                    pair_wcol(t, smh, gWh, g0, kc, NV, wq);
-#pragma unroll
-                    for (int q = 0; q < 4; ++q) {
-                        const float lq = readlane(lam, g0 + q);
-                        u = g0 + q < nrh ? u + wq[q] * lq : u;
-                    }
-                }
-            });
+            const float u = pair_u_update<16, MI_PAIR_UPD_PD>(
+                t, smh, gWh, kc, NV, nrh, (nrh + 3) >> 2, ush[kc],
+                [&](auto R) { return readlane(lam, (int)R); });
             wave_sync();
             if (l64 < NV) smh[t.s_us + l64] = u;
             if (l64 < nrh) smh[t.s_ad + l64] = lam;            // reuse: lambda of row l64

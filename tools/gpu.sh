@@ -25,6 +25,7 @@
 #   curve        reference training schedule, per-epoch curve (tools/train_curve.py) -> train_curve_*.jsonl
 #   sizes        env-count sweep of the fused step (tools/bw_sweep.py)     -> bw_sweep_*.json
 #   ab           bench A/B: default library vs LIB_B (alternating passes)  -> DESIGN perf log
+#   abn          bench A/B/C..: default library vs each of LIBS (alternating passes)
 # Environment knobs: TASK (Humanoid), NS (env counts), BARGS (extra bench.py args), TAG (log suffix).
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 export TMPDIR=/tmp
@@ -114,6 +115,16 @@ recipe() {
       run ab_b_${TASK}_${TAG}_$k 200 env ${ENV_B:-MI_SIM_LIB=$LIB_B} python -u bench.py --task $TASK --steps 300 --warmup 30 --no-cpu-baseline --no-side --fuse-envs 0 ${BARGS:-}
     done
     for f in gpurun_out/ab_[ab]_${TASK}_${TAG}_*.log; do echo "$f $(grep -o '"kernel_ms": [0-9.]*\|"ms_per_step": [0-9.]*\|"lds_bytes_per_env": [0-9]*' $f | head -3 | tr '\n' ' ')"; done ;;
+  abn)  # the default library and each of LIBS (space-separated paths to other builds), alternating
+    for k in 1 2 3; do
+      run abn_0_${TASK}_${TAG}_$k 200 python -u bench.py --task $TASK --steps 300 --warmup 30 --no-cpu-baseline --no-side --fuse-envs 0 ${BARGS:-}
+      j=1
+      for L in $LIBS; do
+        run abn_${j}_${TASK}_${TAG}_$k 200 env MI_SIM_LIB=$L python -u bench.py --task $TASK --steps 300 --warmup 30 --no-cpu-baseline --no-side --fuse-envs 0 ${BARGS:-}
+        j=$((j + 1))
+      done
+    done
+    for f in gpurun_out/abn_*_${TASK}_${TAG}_*.log; do echo "$f $(grep -o '"kernel_ms": [0-9.]*' $f | head -1)"; done ;;
   *)
     echo "unknown recipe $1"; exit 2 ;;
   esac

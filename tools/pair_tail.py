@@ -74,6 +74,7 @@ def main():
            "phases_slow2pct_vs_median": {phases[p]: [round(a[slow, p].mean()), round(a[mid, p].mean())] for p in ph},
            "stats_slow2pct_vs_median_per_substep": {STATS[s]: [round(a[slow, s].mean() / 2, 3), round(a[mid, s].mean() / 2, 3)]
                                                     for s in STATS}}
+    out["w_rows_lds"] = float(a[0, 26]) / 2          # LDS W rows per env (the rest: the slab)
     top = order[-5:][::-1]
     out["slowest5"] = [{"cycles": round(tot[w]), "P10": [round(a[w, 29]), round(a[w, 30]), round(a[w, 27]), round(a[w, 28]),
                                                           round(a[w, 11])], "rows": a[w, 15] / 2,
