@@ -172,19 +172,6 @@ int mi_set_dof_state(mi_sim* sim, const float* q /*[n,D]|NULL*/, const float* qd
 int mi_set_root_state(mi_sim* sim, const float* pos /*[n,3]|NULL*/, const float* quat /*[n,4]|NULL*/,
                       const float* vel /*[n,6]|NULL*/, const int64_t* idx /*[n]|NULL*/, int32_t n,
                       void* stream);
-/* Write batching (off by default): with it on, the three setters above queue their fields
- * (at most 8) instead of launching a scatter each, and the queue is applied in call order by ONE
- * launch at the next call that reads or steps the state (every entry point other than these
- * setters, mi_sim_set_mirror, mi_sim_info and the DR / task-parameter calls), before any substep
- * requested after the writes. A setter whose destination field is already queued, a full queue or
- * a setter on another stream applies the queue first; inside a stream capture setters launch at
- * once. The reference's reset_idx (locomotion.py:116-145: four setters, then set_joint_efforts at
- * :111-114 and World.step) thus costs one scatter launch instead of five. Contract: the source
- * and index buffers of a queued write must stay valid and unmodified until the queue is applied;
- * mi_sim_writes_queued reports how many fields are still queued (0: every earlier source buffer
- * may be reused). Turning batching off applies the queue. */
-int mi_sim_set_write_batching(mi_sim* sim, int32_t on);
-int mi_sim_writes_queued(const mi_sim* sim, int32_t* n);
 /* State mirrors: row-major copies of the articulation state in caller-owned device buffers, the
  * tensors ArticulationView getters hand out with clone=False (get_world_poses, get_velocities,
  * get_joint_positions / velocities, _physics_view.get_force_sensor_forces: locomotion.py:81-89;

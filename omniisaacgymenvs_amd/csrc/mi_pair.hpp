@@ -111,7 +111,7 @@ MI_D void sdof_loop(const float* Ss, const float* R, F&& fn) {
     });
 }
 #ifndef MI_PAIR_WIDE_PD
-#define MI_PAIR_WIDE_PD 4   // W-row prefetch depth of the wide Delassus set-up (1-4 all spill: see DESIGN)
+#define MI_PAIR_WIDE_PD 12   // W-row prefetch depth of the wide Delassus set-up (A/B round 4: 4 0.1360, 8 0.1335, 12 0.1331 ms)
 #endif
 #ifndef MI_PAIR_WIDE_AREG
 #define MI_PAIR_WIDE_AREG 32   // wide-PGS Delassus rows in registers (0, 32 or 64); the rest streamed
@@ -119,8 +119,8 @@ MI_D void sdof_loop(const float* Ss, const float* R, F&& fn) {
 #ifndef MI_PAIR_WIDE_AP
 #define MI_PAIR_WIDE_AP 8   // Delassus rows streamed ahead of the wide sweeps' chain
 #endif
-#ifndef MI_PAIR_UPD_PD
-#define MI_PAIR_UPD_PD 3   // W-group prefetch depth of the PGS u update (pair_u_update)
+#ifndef MI_PAIR_JREUSE_MAXNV
+#define MI_PAIR_JREUSE_MAXNV 16   // narrow PGS reuses P9's J rows for models with nv <= this
 #endif
 #ifndef MI_PAIR_SDOF_PD
 #define MI_PAIR_SDOF_PD 6   // DOF-loop prefetch depth (sdof_loop): 2 -> 0.1609 ms, 4 -> 0.1592 (A/B, round 3); 6: 0.1356 -> 0.1349 (round 4)
@@ -219,40 +219,12 @@ MI_D void pair_dgroup(const WaveTabs& t, const float* sm, const float* gW, int g
 }
 
 // W entries of rows g0..g0+3 at this lane's DOF kc (the u update of both PGS widths; rows past
-// the env's count are read — in bounds: LDS group or slab — but never used: the caller selects
-// them away)
-MI_D pv4 pair_wcol(const WaveTabs& t, const float* sm, const float* gW, int g0, int kc, int nv) {
-    return g0 + 3 < t.w_rows_lds ? pw_group(t, sm, g0, nv)[kc] : ((glb_cf4)(gW + (size_t)g0 * WNV))[kc];
-}
-
-// u = u* + sum_r W_r lambda_r at this lane's DOF kc, in row order, rows in groups of four
-// (groups below ng_max, wave-uniform; rows from n on selected away), each group's W load issued
-// UP groups ahead of its FMAs: in line, every group exposed a full LDS or slab round trip.
-// lam(R) = lambda of row R (a compile-time row).
-template <int NG, int UP, class LF>
-MI_D float pair_u_update(const WaveTabs& t, const float* sm, const float* gW, int kc, int nv, int n,
-                         int ng_max, float u, LF&& lam) {
-    constexpr int NB = UP + 1;
-    pv4 wb[NB];
-    sfor<0, (UP < NG ? UP : NG)>([&](auto G) {
-        if (G < ng_max) wb[G % NB] = pair_wcol(t, sm, gW, 4 * G, kc, nv);
-    });
-    sfor<0, NG>([&](auto G) {
-        constexpr int g = G, g0 = 4 * g;
-        if (g < ng_max) {
-            if constexpr (g + UP < NG) {
-                if (g + UP < ng_max) wb[(g + UP) % NB] = pair_wcol(t, sm, gW, g0 + 4 * UP, kc, nv);
-            }
-            const pv4 w = wb[g % NB];
-            const float wq[4] = {w.x, w.y, w.z, w.w};
-            sfor<0, 4>([&](auto Q) {
-                constexpr int q = Q;
-                const float lq = lam(std::integral_constant<int, g0 + q>{});
-                u = g0 + q < n ? u + wq[q] * lq : u;
-            });
-        }
-    });
-    return u;
+// the env's count are read but never used: the caller selects them away)
+MI_D void pair_wcol(const WaveTabs& t, const float* sm, const float* gW, int g0, int kc, int nv,
+                    float (&wq)[4]) {
+    const pv4 w = g0 + 3 < t.w_rows_lds ? pw_group(t, sm, g0, nv)[kc]
+                                        : ((glb_cf4)(gW + (size_t)g0 * WNV))[kc];
+    wq[0] = w.x; wq[1] = w.y; wq[2] = w.z; wq[3] = w.w;
 }
 
 // One articulated substep of the env of this lane's half (env i, LDS region sm, W slab gW).
@@ -585,7 +557,11 @@ MI_D void pair_artic_substep(const DevModel& m, const WaveTabs& t, const DevStat
             }
         }
     };
-    float Jc[TP::nvc];   // J rows of contact rows 0..31 (first pass): the narrow PGS set-up's
+    // J rows of contact rows 0..31 (first pass), kept for the narrow PGS set-up when the model's
+    // J row is short enough to stay live through the second pass without spilling (Ant: 0.0512
+    // -> 0.0498 ms; Humanoid, nv 27: rebuilt in P10 instead, keeping the kernel spill-free)
+    constexpr bool kReuseJ = TP::nv <= MI_PAIR_JREUSE_MAXNV;
+    float Jc[TP::nvc];
     for (int base = 0; base < total_max; base += 32) {
         const int bv = base + lane;
         const bool on = bv < total;
@@ -611,7 +587,9 @@ MI_D void pair_artic_substep(const DevModel& m, const WaveTabs& t, const DevStat
             asm volatile("" : "+v"(xc), "+v"(rc));
             x[c] = crow ? xc : (bv == nc ? rc : (kd == c ? 1.0f : 0.0f));
         });
-        if (base == 0) sfor<0, TP::nv>([&](auto C) { Jc[C] = x[C]; });
+        if constexpr (kReuseJ) {
+            if (base == 0) sfor<0, TP::nv>([&](auto C) { Jc[C] = x[C]; });
+        }
         STAMP(7);
         float a;
         ct_solve_l<TP, MI_PAIR_SOLVE_PD>(sm + t.s_L, x, a);
@@ -644,10 +622,10 @@ MI_D void pair_artic_substep(const DevModel& m, const WaveTabs& t, const DevStat
         // cross-lane broadcast (v_r) instead of five.
         constexpr int NV = TP::nv;
         constexpr int RMAX = TP::kLamRows;
-        // J_r: a contact row's from P9's first pass (same lane), a limit row's sg e_k; a dead
-        // lane's 0 (v 0: its projection keeps lambda 0)
+        // J_r: with kReuseJ a contact row's from P9's first pass (same lane), a limit row's
+        // sg e_k, a dead lane's 0 (v 0: its projection keeps lambda 0); else rebuilt
         float Jr[TP::nvc];
-        {
+        if constexpr (kReuseJ) {
             int kdof = -1;
             float sg = 0.0f;
             if (lane >= nc && lane < nrows) {
@@ -656,6 +634,9 @@ MI_D void pair_artic_substep(const DevModel& m, const WaveTabs& t, const DevStat
             }
             const bool own = lane < nc;
             sfor<0, NV>([&](auto C) { Jr[C] = own ? Jc[C] : (kdof == C ? sg : 0.0f); });
+        } else {
+            if (nrows > 0) pair_jrow<TP>(mc, t, sm, lane < nrows ? lane : 0, nr, Jr);
+            else sfor<0, NV>([&](auto C) { Jr[C] = 0.0f; });
         }
         float v = 0.0f;
         sfor<0, NV>([&](auto C) { v += Jr[C] * us[C]; });
@@ -710,10 +691,17 @@ MI_D void pair_artic_substep(const DevModel& m, const WaveTabs& t, const DevStat
             });
         }
         STAMP(28);
+        float u = lane < NV ? us[lane] : 0.0f;
         const int kc = lane < NV ? lane : 0;
-        const float u = pair_u_update<RMAX / 4, MI_PAIR_UPD_PD>(
-            t, sm, gW, kc, NV, nrows, (nrows_max + 3) >> 2, lane < NV ? us[lane] : 0.0f,
-            [&](auto R) { return lamv[R]; });
+        sfor<0, RMAX / 4>([&](auto G) {
+            constexpr int g0 = 4 * G;
+            if (g0 < nrows_max) {
+                float wq[4];
+                pair_wcol(t, sm, gW, g0, kc, NV, wq);
+#pragma unroll
+                for (int q = 0; q < 4; ++q) u = g0 + q < nrows ? u + wq[q] * lamv[g0 + q] : u;
+            }
+        });
         if (lane < NV) us[lane] = u;
         wave_sync();
         {   // reuse: lambda of row rr, written by lane rr (one select chain, one store)
@@ -827,9 +815,19 @@ MI_D void pair_artic_substep(const DevModel& m, const WaveTabs& t, const DevStat
             }
             STAMP(28);
             // u = u* + sum_r W_r lambda_r, lane = DOF
-            const float u = pair_u_update<16, MI_PAIR_UPD_PD>(
-                t, smh, gWh, kc, NV, nrh, (nrh + 3) >> 2, ush[kc],
-                [&](auto R) { return readlane(lam, (int)R); });
+            float u = ush[kc];
+            sfor<0, 16>([&](auto G) {
+                constexpr int g0 = 4 * G;
+                if (g0 < nrh) {
+                    float wq[4];
+                    pair_wcol(t, smh, gWh, g0, kc, NV, wq);
+#pragma unroll
+                    for (int q = 0; q < 4; ++q) {
+                        const float lq = readlane(lam, g0 + q);
+                        u = g0 + q < nrh ? u + wq[q] * lq : u;
+                    }
+                }
+            });
             wave_sync();
             if (l64 < NV) smh[t.s_us + l64] = u;
             if (l64 < nrh) smh[t.s_ad + l64] = lam;            // reuse: lambda of row l64

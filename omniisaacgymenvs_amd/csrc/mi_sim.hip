@@ -80,13 +80,6 @@ struct mi_sim {
     int pending = 0;
     hipStream_t pending_stream = nullptr;
     hipEvent_t pending_ev = nullptr;
-    // queued state writes (mi_sim_set_write_batching): the setters' fields since the last flush,
-    // applied in call order by ONE launch at the next entry point that reads or steps the state
-    bool batch_writes = false;
-    int wq_n = 0;
-    hipStream_t wq_stream = nullptr;
-    hipEvent_t wq_ev = nullptr;
-    struct QWrite { const float* src; float* dst; const void* idx; int C, n, idx64; } wq[8];
     // state mirrors (mi_sim_set_mirror): row-major pos, quat, vel, q, qd, sens; valid = every
     // mirror equals the state (set by mi_get_state_mirror, cleared by every state write)
     float* mir[6] = {nullptr, nullptr, nullptr, nullptr, nullptr, nullptr};
@@ -924,23 +917,6 @@ __global__ __launch_bounds__(256) void k_rows_to_soa_multi(GFields fs3, int n, c
     if (i < 0 || i >= N) return;                   // out-of-range ids are ignored
     const_cast<float*>(g.dst)[(size_t)c * fs + (size_t)i * es] = g.src[t];
 }
-// The write queue's scatter: up to 8 fields (blockIdx.y), each with its own rows, ids (int32,
-// int64 or none) and column count; the destination is a record field (field stride fs, env
-// stride es). The queue never holds two fields with one destination array (the host flushes
-// first), so the fields are independent and their order inside the launch does not matter.
-struct QField { const float* src; float* dst; const void* idx; int C, n, idx64; };
-struct QFields { QField f[8]; };
-__global__ __launch_bounds__(256) void k_rows_to_soa_queue(QFields q, int N, int fs, int es) {
-    const QField g = q.f[blockIdx.y];
-    const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (t >= (int64_t)g.n * g.C) return;
-    const int r = (int)(t / g.C), c = (int)(t - (int64_t)r * g.C);
-    const int64_t i = !g.idx ? (int64_t)r
-                     : g.idx64 ? static_cast<const int64_t*>(g.idx)[r]
-                               : (int64_t)static_cast<const int32_t*>(g.idx)[r];
-    if (i < 0 || i >= N) return;                   // out-of-range ids are ignored
-    g.dst[(size_t)c * fs + (size_t)i * es] = g.src[t];
-}
 static inline dim3 gather_grid(int N) { return dim3((N + MI_GATHER_TILE - 1) / MI_GATHER_TILE); }
 static inline dim3 scatter_grid(int n, int C) { return dim3((unsigned)(((int64_t)n * C + 255) / 256)); }
 
@@ -1549,12 +1525,11 @@ int mi_sim_destroy(mi_sim* s) {
     (void)hipSetDevice(s->device);
     // deferred substeps are issued, not dropped (their state is about to be freed, but a
     // mirror or a caller's event may still order after them), then everything drains
-    if (s->pending || s->wq_n) (void)flush_pending(s, s->pending ? s->pending_stream : s->wq_stream);
+    if (s->pending) (void)flush_pending(s, s->pending_stream);
     (void)hipDeviceSynchronize();
     for (hipEvent_t e : s->tev) (void)hipEventDestroy(e);
     if (s->pending_ev) (void)hipEventDestroy(s->pending_ev);
     if (s->mir_ev) (void)hipEventDestroy(s->mir_ev);
-    if (s->wq_ev) (void)hipEventDestroy(s->wq_ev);
     for (void* p : s->allocs) (void)hipFree(p);
     delete s;
     return MI_OK;
@@ -1621,41 +1596,7 @@ static bool capturing(hipStream_t st) {
 // Issue the substeps mi_sim_step deferred, on the stream they were requested on; a caller on
 // another stream waits for them. Substeps requested before a stream capture began cannot be
 // issued into it: that is refused loudly (call the step inside the capture, or synchronise).
-// Apply the queued state writes (one launch on the stream they were queued on; a caller on
-// another stream waits for it).
-static int flush_writes(mi_sim* s, void* stream) {
-    if (s->wq_n == 0) return MI_OK;
-    hipStream_t ws = s->wq_stream;
-    if (capturing(ws) || (stream && capturing(STREAM(stream))))
-        return fail(MI_E_STATE, "%d state write(s) queued before a stream capture began are still "
-                                "pending: synchronise before capturing", s->wq_n);
-    QFields q{};
-    int64_t most = 0;
-    for (int k = 0; k < s->wq_n; ++k) {
-        const mi_sim::QWrite& w = s->wq[k];
-        q.f[k] = {w.src, w.dst, w.idx, w.C, w.n, w.idx64};
-        most = std::max(most, (int64_t)w.n * w.C);
-    }
-    dim3 g((unsigned)((most + 255) / 256), (unsigned)s->wq_n);
-    s->wq_n = 0;
-    HIP_TRY(hipSetDevice(s->device));
-    hipLaunchKernelGGL(k_rows_to_soa_queue, g, dim3(256), 0, ws, q, s->N, s->ds.fs, s->ds.es);
-    LAUNCH_CHECK();
-    if (STREAM(stream) != ws) {
-        if (!s->wq_ev) HIP_TRY(hipEventCreateWithFlags(&s->wq_ev, hipEventDisableTiming));
-        HIP_TRY(hipEventRecord(s->wq_ev, ws));
-        HIP_TRY(hipStreamWaitEvent(STREAM(stream), s->wq_ev, 0));
-    }
-    return MI_OK;
-}
-
-// Queued writes first (they were queued before any substep still pending: a setter issues the
-// pending substeps before it queues), then the deferred substeps.
 static int flush_pending(mi_sim* s, void* stream) {
-    if (s->wq_n) {
-        const int rc = flush_writes(s, stream);
-        if (rc) return rc;
-    }
     if (s->pending == 0) return MI_OK;
     const int k = s->pending;
     hipStream_t ps = s->pending_stream;
@@ -1732,50 +1673,14 @@ int mi_get_sensor_wrench(mi_sim* s, float* out, void* stream) {
     return gather_fields(s, f, 1, stream);
 }
 
-// A setter's fields: queued when batching (mi_sim_set_write_batching, outside stream capture),
-// else one scatter launch now. Pending substeps are issued first either way (they precede the
-// write); a queued field whose destination array is already in the queue, a full queue or a
-// queue on another stream is applied before the new fields join.
-extern "C++" template <typename IDX>
-static int write_fields(mi_sim* s, GFields f, int nf, int n, const IDX* idx, void* stream) {
-    if (s->pending) FLUSH(s, stream);
-    if (nf == 0 || n == 0) return MI_OK;
-    if (!s->batch_writes || capturing(STREAM(stream))) {
-        FLUSH(s, stream);
-        return scatter_fields<IDX>(s, f, nf, n, idx, stream);
-    }
-    if (s->wq_n && s->wq_stream != STREAM(stream)) FLUSH(s, stream);
-    for (int k = 0; k < nf; ++k) {
-        bool clash = s->wq_n == 8;
-        for (int j = 0; j < s->wq_n && !clash; ++j) clash = s->wq[j].dst == f.f[k].dst;
-        if (clash) FLUSH(s, stream);
-        s->wq[s->wq_n++] = {f.f[k].src, const_cast<float*>(f.f[k].dst), (const void*)idx, f.f[k].C, n,
-                            (int)(sizeof(IDX) == 8)};
-    }
-    s->wq_stream = STREAM(stream);
-    return MI_OK;
-}
-
-int mi_sim_set_write_batching(mi_sim* s, int32_t on) {
-    NEED(s);
-    if (!on && s->wq_n) FLUSH(s, s->wq_stream);
-    s->batch_writes = on != 0;
-    return MI_OK;
-}
-
-int mi_sim_writes_queued(const mi_sim* s, int32_t* n) {
-    NEED(s); NEED(n);
-    *n = s->wq_n;
-    return MI_OK;
-}
-
 int mi_set_dof_efforts(mi_sim* s, const float* eff, const int32_t* idx, int32_t n, void* stream) {
     NEED(s); NEED(eff);
     if (n < 0 || n > s->N || (!idx && n != s->N)) return fail(MI_E_SHAPE, "mi_set_dof_efforts: bad n=%d", n);
     HIP_TRY(hipSetDevice(s->device));
+    FLUSH(s, stream);
     GFields f{};
     f.f[0] = {eff, s->ds.eff, s->dm.D};
-    return write_fields<int32_t>(s, f, 1, n, idx, stream);
+    return scatter_fields<int32_t>(s, f, 1, n, idx, stream);
 }
 
 int mi_set_dof_state(mi_sim* s, const float* q, const float* qd, const int64_t* idx, int32_t n,
@@ -1783,12 +1688,13 @@ int mi_set_dof_state(mi_sim* s, const float* q, const float* qd, const int64_t* 
     NEED(s);
     if (n < 0 || n > s->N || (!idx && n != s->N)) return fail(MI_E_SHAPE, "mi_set_dof_state: bad n=%d", n);
     HIP_TRY(hipSetDevice(s->device));
+    FLUSH(s, stream);
     GFields f{};
     int nf = 0;
     if (q) f.f[nf++] = {q, s->ds.q, s->dm.D};
     if (qd) f.f[nf++] = {qd, s->ds.qd, s->dm.D};
     if (nf && n) s->mir_valid = false;
-    return write_fields<int64_t>(s, f, nf, n, idx, stream);
+    return scatter_fields<int64_t>(s, f, nf, n, idx, stream);
 }
 
 int mi_set_root_state(mi_sim* s, const float* pos, const float* quat, const float* vel,
@@ -1796,13 +1702,14 @@ int mi_set_root_state(mi_sim* s, const float* pos, const float* quat, const floa
     NEED(s);
     if (n < 0 || n > s->N || (!idx && n != s->N)) return fail(MI_E_SHAPE, "mi_set_root_state: bad n=%d", n);
     HIP_TRY(hipSetDevice(s->device));
+    FLUSH(s, stream);
     GFields f{};
     int nf = 0;
     if (pos) f.f[nf++] = {pos, s->ds.root_pos, 3};
     if (quat) f.f[nf++] = {quat, s->ds.root_quat, 4};
     if (vel) f.f[nf++] = {vel, s->ds.root_vel, 6};
     if (nf && n) s->mir_valid = false;
-    return write_fields<int64_t>(s, f, nf, n, idx, stream);
+    return scatter_fields<int64_t>(s, f, nf, n, idx, stream);
 }
 
 int mi_sim_set_mirror(mi_sim* s, float* pos, float* quat, float* vel, float* q, float* qd, float* sens) {
@@ -1860,7 +1767,6 @@ int mi_sim_step(mi_sim* s, int32_t substeps, void* stream) {
     }
     if (s->pending && (s->pending_stream != STREAM(stream) || s->pending + substeps > 64))
         FLUSH(s, stream);                  // one launch never carries more than 64 substeps
-    if (s->wq_n && s->wq_stream != STREAM(stream)) FLUSH(s, stream);   // queued writes: same stream
     s->pending += substeps;
     s->pending_stream = STREAM(stream);
     if (s->pending == 64) FLUSH(s, stream);

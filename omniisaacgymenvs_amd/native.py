@@ -93,8 +93,6 @@ class NativeUnavailable(RuntimeError):
 
 
 _LIB = None
-# entry points an A/B build named by MI_SIM_LIB may predate (callers check hasattr)
-_NEWER = ("mi_build_id", "mi_sim_set_write_batching", "mi_sim_writes_queued")
 
 _SIGS = {
     "mi_sim_create": (C.c_int, [C.POINTER(MiModelDesc), C.POINTER(MiSimParams), C.c_int32,
@@ -113,8 +111,6 @@ _SIGS = {
     "mi_get_state_mirror": (C.c_int, [C.c_void_p, C.c_void_p]),
     "mi_sim_step": (C.c_int, [C.c_void_p, C.c_int32, C.c_void_p]),
     "mi_sim_flush": (C.c_int, [C.c_void_p, C.c_void_p]),
-    "mi_sim_set_write_batching": (C.c_int, [C.c_void_p, C.c_int32]),
-    "mi_sim_writes_queued": (C.c_int, [C.c_void_p, _i32p]),
     "mi_task_configure": (C.c_int, [C.c_void_p, C.POINTER(MiTaskParams)]),
     "mi_task_pre_step": (C.c_int, [C.c_void_p] + [C.c_void_p] * 7),
     "mi_task_reset_idx": (C.c_int, [C.c_void_p, C.c_void_p, C.c_int32] + [C.c_void_p] * 5),
@@ -160,7 +156,7 @@ def load_library(path: str = LIB_PATH) -> C.CDLL:
         try:
             fn = getattr(lib, name)
         except AttributeError:
-            if lenient and name in _NEWER:
+            if lenient and name == "mi_build_id":
                 continue
             raise
         fn.restype = res

@@ -15,7 +15,6 @@
 from __future__ import annotations
 
 import ctypes as C
-import os
 from typing import Optional
 
 import numpy as np
@@ -121,22 +120,11 @@ class ArticulationView:
                                       self._mir_vel.data_ptr(), self._mir_q.data_ptr(),
                                       self._mir_qd.data_ptr(),
                                       self._mir_sens.data_ptr() if S else None), "mi_sim_set_mirror")
-        # write batching (include/mi_sim.h mi_sim_set_write_batching): the setters of one
-        # reset_idx plus set_joint_efforts become one scatter launch, applied in call order before
-        # the next step or read. Their source / index tensors are held here until the library
-        # reports the queue applied (MI_SIM_BATCH_WRITES=0: one launch per setter, nothing held).
-        self._held = []
-        self._nq = C.c_int32()
-        self._batch = (os.environ.get("MI_SIM_BATCH_WRITES", "1") != "0"
-                       and hasattr(lib, "mi_sim_set_write_batching"))
-        if self._batch:
-            N.check(lib.mi_sim_set_write_batching(self.handle, 1), "mi_sim_set_write_batching")
 
     def close(self) -> None:
         if self.handle:
-            N.lib().mi_sim_destroy(self.handle)   # applies queued writes, then drains
+            N.lib().mi_sim_destroy(self.handle)
             self.handle = None
-            self._held = []
 
     def __del__(self):
         try:
@@ -229,17 +217,6 @@ class ArticulationView:
     def _idx64(self, indices) -> (Optional[torch.Tensor], int):
         return self._idx(indices, torch.int64)
 
-    def _hold(self, *ts) -> None:
-        """After a setter: keep its tensors while the library still queues writes (a queued
-        write reads them when the queue is applied); drop every held tensor once it is empty."""
-        if not self._batch:
-            return
-        self._lib.mi_sim_writes_queued(self.handle, C.byref(self._nq))
-        if self._nq.value == 0:
-            self._held.clear()
-        else:
-            self._held.extend(t for t in ts if t is not None)
-
     def set_joint_efforts(self, efforts: torch.Tensor, indices=None) -> None:
         e = self._f32(efforts)
         idx, n = self._idx(indices, torch.int32)
@@ -249,7 +226,6 @@ class ArticulationView:
                                           n, self.stream())
         if rc:
             N.check(rc, "mi_set_dof_efforts")
-        self._hold(e, idx)
 
     def set_joint_positions(self, positions: torch.Tensor, indices=None) -> None:
         q = self._f32(positions)
@@ -259,7 +235,6 @@ class ArticulationView:
         rc = self._lib.mi_set_dof_state(self.handle, q.data_ptr(), None, N.ptr(idx), n, self.stream())
         if rc:
             N.check(rc, "mi_set_dof_state")
-        self._hold(q, idx)
 
     def set_joint_velocities(self, velocities: torch.Tensor, indices=None) -> None:
         qd = self._f32(velocities)
@@ -269,7 +244,6 @@ class ArticulationView:
         rc = self._lib.mi_set_dof_state(self.handle, None, qd.data_ptr(), N.ptr(idx), n, self.stream())
         if rc:
             N.check(rc, "mi_set_dof_state")
-        self._hold(qd, idx)
 
     def set_world_poses(self, positions=None, orientations=None, indices=None) -> None:
         p, r = self._f32(positions), self._f32(orientations)
@@ -279,7 +253,6 @@ class ArticulationView:
         rc = self._lib.mi_set_root_state(self.handle, N.ptr(p), N.ptr(r), None, N.ptr(idx), n, self.stream())
         if rc:
             N.check(rc, "mi_set_root_state")
-        self._hold(p, r, idx)
 
     def set_velocities(self, velocities: torch.Tensor, indices=None) -> None:
         v = self._f32(velocities)
@@ -289,7 +262,6 @@ class ArticulationView:
         rc = self._lib.mi_set_root_state(self.handle, None, None, v.data_ptr(), N.ptr(idx), n, self.stream())
         if rc:
             N.check(rc, "mi_set_root_state")
-        self._hold(v, idx)
 
     # ---- physics ----
     def sim_step(self, substeps: int = 1) -> None:

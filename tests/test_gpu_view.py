@@ -273,69 +273,3 @@ def test_state_mirrors_track_every_state_write(gpu, name, n, pair, path, monkeyp
     side.synchronize()
     assert q2 is q and np.array_equal(copy.cpu().numpy(), _direct(view)["q"])
     env.close()
-
-
-@pytest.mark.parametrize("name", ["Humanoid", "Ant", "Cartpole"])
-def test_write_batching_equals_one_launch_per_setter(gpu, name, monkeypatch):
-    """Queued setters (include/mi_sim.h mi_sim_set_write_batching, on in the ArticulationView)
-    equal one scatter launch per setter (MI_SIM_BATCH_WRITES=0), bit for bit: the reference's
-    path (A) order — reset_idx's four setters (locomotion.py:130-134) on random env ids, then
-    set_joint_efforts (:111-114), two World.step, the getters — plus a field written twice before
-    the queue is applied (the later write wins on overlapping ids), a setter on a side stream and
-    a state read right after the setters. The view holds the queued tensors until the library
-    reports the queue applied."""
-    n = 257
-    ea = make_env(name, num_envs=n, device="cuda:0", seed=6)
-    monkeypatch.setenv("MI_SIM_BATCH_WRITES", "0")
-    eb = make_env(name, num_envs=n, device="cuda:0", seed=6)
-    monkeypatch.delenv("MI_SIM_BATCH_WRITES")
-    va, vb = ea.task.get_robot(), eb.task.get_robot()
-    assert va._batch and not vb._batch
-    for e in (ea, eb):
-        e.reset()
-    D = va.num_dof
-    g = torch.Generator().manual_seed(3)
-    q_cnt = ctypes_int()
-    side = torch.cuda.Stream()
-    for k in range(6):
-        ids = torch.randperm(n, generator=g)[: 5 + 7 * k].cuda()
-        ids2 = torch.randperm(n, generator=g)[:20].cuda()
-        vals = [(torch.rand((len(ids), c), generator=g) * 0.2 - 0.1).cuda() for c in (D, D, 3, 4, 6)]
-        vals[3] = torch.nn.functional.normalize(vals[3] + torch.tensor([1.0, 0, 0, 0]).cuda(), dim=-1)
-        q2 = (torch.rand((20, D), generator=g) * 0.1).cuda()
-        eff = (torch.rand((n, D), generator=g) * 2 - 1).cuda()
-        for v in (va, vb):
-            v.set_joint_positions(vals[0], indices=ids)
-            v.set_joint_velocities(vals[1], indices=ids)
-            if name != "Cartpole":                            # fixed base: no root setters
-                v.set_world_poses(vals[2], vals[3], indices=ids)
-                v.set_velocities(vals[4], indices=ids)
-            v.set_joint_positions(q2, indices=ids2)          # same field again: later wins
-            if k % 2:
-                with torch.cuda.stream(side):                 # a setter on another stream
-                    side.wait_stream(torch.cuda.current_stream())
-                    v.set_joint_efforts(eff, indices=torch.arange(n, dtype=torch.int32, device="cuda:0"))
-                torch.cuda.current_stream().wait_stream(side)
-            else:
-                v.set_joint_efforts(eff, indices=torch.arange(n, dtype=torch.int32, device="cuda:0"))
-        va._lib.mi_sim_writes_queued(va.handle, q_cnt)
-        assert q_cnt.value > 0 and va._held, k                # queued, tensors held
-        if k == 3:                                            # a read right after the setters
-            sa, sb = _state(va), _state(vb)
-            for key in sa:
-                assert np.array_equal(sa[key], sb[key]), (k, key)
-        for e in (ea, eb):
-            e._world.step()
-            e._world.step()
-        sa, sb = _state(va), _state(vb)
-        for key in sa:
-            assert np.array_equal(sa[key], sb[key]), (k, key)
-        va._lib.mi_sim_writes_queued(va.handle, q_cnt)
-        assert q_cnt.value == 0, k
-    ea.close()
-    eb.close()
-
-
-def ctypes_int():
-    import ctypes
-    return ctypes.c_int32()

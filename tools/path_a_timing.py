@@ -145,11 +145,8 @@ def measure(task_name: str = "Humanoid", n: int = 4096, steps: int = 200) -> dic
            "path_a_backend_device_ms_per_step": round(backend_ms, 4),
            "backend_host_us_per_call": host_us, "backend_host_us_per_step": host_us_step,
            "reference_ops_only_ms_per_step": round(ms_ref_wall, 4),
-           "path_a_launches_per_step": ("1 physics (deferred substeps; the paired kernel writes the five getters' "
-                                        "state mirrors itself) + 1 scatter (set_joint_efforts and, when any env "
-                                        "is due, the four reset setters, queued and applied together)"
-                                        if os.environ.get("MI_SIM_BATCH_WRITES", "1") != "0" else
-                                        "1 physics + efforts + 4 reset scatters when any env is due"),
+           "path_a_launches_per_step": "1 physics (deferred substeps; the paired kernel writes the five getters' "
+                                       "state mirrors itself) + efforts + 4 reset scatters when any env is due",
            "path_b_fused_ms_per_step": round(ms_b_wall, 4), "path_b_device_ms_per_step": round(ms_b_dev, 4),
            "note": "path A: the reference's call sequence incl. its reset / termination torch ops and "
                    "nonzero() host sync; jit observation / reward math excluded. backend_device: "
