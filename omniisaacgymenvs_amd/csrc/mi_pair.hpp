@@ -365,7 +365,6 @@ MI_D void pair_artic_substep(const DevModel& m, const WaveTabs& t, const DevStat
                     const int r = 3 * ci + tt;
                     sm[t.s_rl + r] = (float)l;
                     sm[t.s_rb + r] = tt == 0 ? bn : 0.0f;
-                    sm[t.s_rk + r] = (float)tt;
                 }
             }
             ncon += __popc(mask);
@@ -462,7 +461,6 @@ MI_D void pair_artic_substep(const DevModel& m, const WaveTabs& t, const DevStat
                         const int r = 3 * ci + tt;
                         sm[t.s_rl + r] = (float)la;
                         sm[t.s_rb + r] = tt == 0 ? bn : 0.0f;
-                        sm[t.s_rk + r] = (float)tt;
                     }
                 }
                 const int took = budget > 0 ? min(__popc(mask), budget) : 0;
@@ -521,7 +519,6 @@ MI_D void pair_artic_substep(const DevModel& m, const WaveTabs& t, const DevStat
             sm[t.s_rl + rl] = -(float)(nr + lane) - 1.0f;
             sm[t.s_lsg + lane] = sg;
             sm[t.s_rb + rl] = bl;
-            sm[t.s_rk + rl] = 3.0f;
         }
         nrows = nc + __popc(limact);
         wave_sync();
@@ -657,7 +654,7 @@ MI_D void pair_artic_substep(const DevModel& m, const WaveTabs& t, const DevStat
         if (lane < nrows) {
             b = sm[t.s_rb + lane];
             ia = 1.0f / sm[t.s_ad + lane];
-            kd = (int)sm[t.s_rk + lane];
+            kd = lane < nc ? lane % 3 : 3;   // row kind from the row index (no LDS array)
         }
         const int nnorm = 3 * ncon;   // rows below this with r % 3 == 0 are normal rows
         STAMP(27);
@@ -856,7 +853,7 @@ MI_D void pair_artic_substep(const DevModel& m, const WaveTabs& t, const DevStat
                             unsigned& msk2) {
             b = sm[t.s_rb + r];
             ia = 1.0f / sm[t.s_ad + r];
-            k = sm[t.s_rk + r];
+            k = (float)(r < nc ? r % 3 : 3);
             const float lk = sm[t.s_rl + r];
             if (lk >= 0.0f) {
                 contact_row_f<TP::kSelf>(sm, t, r, f);
@@ -927,7 +924,7 @@ MI_D void pair_artic_substep(const DevModel& m, const WaveTabs& t, const DevStat
                 const bool live_row = r < nrows;
                 const int rs = live_row ? r : 0;
                 const float br = sm[t.s_rb + rs], ar = sm[t.s_ad + rs];
-                const int kind = (int)sm[t.s_rk + rs];
+                const int kind = rs < nc ? rs % 3 : 3;
                 const float lk = sm[t.s_rl + rs];
                 float jc;
                 if (lk >= 0.0f) {

@@ -1318,7 +1318,10 @@ int mi_sim_create(const mi_model_desc* md, const mi_sim_params* prm, int32_t N, 
             ro = span0;
             auto take_r = [&](int n) { const int at = ro; ro += al4(n); return at; };
             t.s_cp = take_r(3 * C); t.s_cl = take_r(C); t.s_cl2 = take_r(C); t.s_cn = take_r(3 * C);
-            t.s_rl = take_r(R); t.s_rb = take_r(R); t.s_rk = take_r(R); t.s_ad = take_r(R);
+            // no row-kind array: the paired kernels derive a row's kind from its index (contact
+            // rows are (normal, friction, friction) triples, then the limit rows); its R floats
+            // buy W rows (Humanoid: 28 -> 32 LDS rows, so the narrow PGS never reads the slab)
+            t.s_rl = take_r(R); t.s_rb = take_r(R); t.s_rk = -1; t.s_ad = take_r(R);
             t.s_lsg = take_r(WNV);
             t.s_W = ro;
             int w = std::min(64, (t.s_R + env_budget - ro) / m.nv);
