@@ -67,6 +67,20 @@ MI_D unsigned hballot(bool p) {
     return (unsigned)(m >> (pair_l64() & 32));
 }
 MI_D unsigned lanemask_lt(int lane) { return (1u << lane) - 1u; }
+// index of the j-th (0-based) set bit of m, j < popc(m): binary search on popcounts
+MI_D int nth_bit(unsigned m, int j) {
+    int b = 0;
+#pragma unroll
+    for (int w = 16; w >= 1; w >>= 1) {
+        const int c = __popc((m >> b) & ((1u << w) - 1u));
+        if (j >= c) { j -= c; b += w; }
+    }
+    return b;
+}
+// the k lowest set bits of m
+MI_D unsigned low_bits(unsigned m, int k) {
+    return k >= __popc(m) ? m : (m & ((1u << nth_bit(m, k)) - 1u));
+}
 // larger of the two halves' (half-uniform) values: wave-uniform
 MI_D int pmax(int v) { return max(__builtin_amdgcn_readlane(v, 0), __builtin_amdgcn_readlane(v, 32)); }
 // sum over each 32-lane half, returned to every lane of the half
@@ -118,6 +132,12 @@ MI_D void sdof_loop(const float* Ss, const float* R, F&& fn) {
 #endif
 #ifndef MI_PAIR_WIDE_AP
 #define MI_PAIR_WIDE_AP 8   // Delassus rows streamed ahead of the wide sweeps' chain
+#endif
+#ifndef MI_PAIR_LIM_NEAR
+#define MI_PAIR_LIM_NEAR 0.05f   // rad / m: a joint this close to a limit is speculated on first
+#endif
+#ifndef MI_PAIR_LIM_SPEC_MIN_D
+#define MI_PAIR_LIM_SPEC_MIN_D 16   // speculative limit-candidate lanes for models with >= this many DOFs
 #endif
 #ifndef MI_PAIR_JREUSE_MAXNV
 #define MI_PAIR_JREUSE_MAXNV 16   // narrow PGS reuses P9's J rows for models with nv <= this
@@ -479,12 +499,39 @@ MI_D void pair_artic_substep(const DevModel& m, const WaveTabs& t, const DevStat
     wave_sync();
     STAMP(6);
     // ---- P7+P9: one batch per half, lanes over solve vectors: the contact rows first (lane =
-    // row in the first pass, as in the P10 Delassus set-up, which then takes their J rows from
-    // this pass's registers instead of rebuilding them), then the rhs, then the limit
-    // candidates; passes of 32 to the larger half's count
-    const int nlim = t.nlimc;
-    const int total = 1 + nlim + nc;
-    const int total_max = pmax(total);
+    // row in the first pass, as in the P10 Delassus set-up, which may then take their J rows
+    // from this pass's registers), then the rhs, then limit candidates; passes of 32 to the
+    // larger half's count.
+    // Limit candidates: only the rhs's solve tells which limits are active, so the pass holding
+    // the rhs fills its spare lanes with candidates speculatively — joints near a limit first
+    // (q or q + dt u within MI_PAIR_LIM_NEAR of it), then the others in joint order — and later
+    // passes take only the active candidates that were not among them. Which lane solves a
+    // candidate changes neither its solve nor its filing (slot by joint index): the results of
+    // solving every candidate, with a pass fewer whenever the spare lanes hold the active ones
+    // (Humanoid: 1 + 21 + 14 solve vectors were two passes; 14 contact rows, the rhs and 17
+    // candidates are one).
+    // (models with few limited joints, e.g. Ant's 8, never need the second pass for them: there
+    // every candidate follows the rhs, no speculation bookkeeping)
+    constexpr bool kSpec = TP::D >= MI_PAIR_LIM_SPEC_MIN_D;
+    unsigned cmask = 0u, nmask = 0u;
+    if constexpr (kSpec) {
+        bool cand = false, near = false;
+        if (lane < D) {
+            const float lo = mc.lf(MC_LO, lane + 1), hi = mc.lf(MC_HI, lane + 1);
+            const float qj = sm[t.s_q + lane], qp = qj + dt * us[nr + lane];
+            const float mg = MI_PAIR_LIM_NEAR;
+            cand = lo < hi;
+            near = cand && (qj < lo + mg || qp < lo + mg || qj > hi - mg || qp > hi - mg);
+        }
+        cmask = hballot(cand);
+        nmask = hballot(near);
+    }
+    const unsigned fmask = cmask & ~nmask;
+    const int nN = __popc(nmask);
+    const int nspec = kSpec ? min(__popc(cmask), 31 - (nc & 31)) : t.nlimc;   // spare lanes of the rhs's pass
+    int total = nc + 1 + nspec;
+    int total_max = pmax(total);
+    unsigned rem = 0u;                   // active candidates the spare lanes did not solve
     int nrows = nc;
     unsigned limact = 0u;
     // res: the rhs lane's solve (unconstrained acceleration); here: the rhs sits in this pass for
@@ -564,7 +611,15 @@ MI_D void pair_artic_substep(const DevModel& m, const WaveTabs& t, const DevStat
         const bool on = bv < total;
         const bool crow = on && bv < nc;
         const int r = crow ? bv : -1;
-        const int kd = (on && bv > nc) ? nr + mc.lim(bv - nc - 1) : -1;
+        int kd = -1;
+        if (on && bv > nc) {
+            const int sl = bv - nc - 1;
+            if constexpr (kSpec)
+                kd = nr + (sl < nspec ? (sl < nN ? nth_bit(nmask, sl) : nth_bit(fmask, sl - nN))
+                                      : nth_bit(rem, sl - nspec));
+            else
+                kd = nr + mc.lim(sl);
+        }
         float x[TP::nvc];
         float f[6] = {0.0f, 0.0f, 0.0f, 0.0f, 0.0f, 0.0f};
         unsigned msk = 0u, msk2 = 0u;
@@ -592,7 +647,15 @@ MI_D void pair_artic_substep(const DevModel& m, const WaveTabs& t, const DevStat
         ct_solve_l<TP, MI_PAIR_SOLVE_PD>(sm + t.s_L, x, a);
         STAMP(8);
         const bool rhs_here = base <= nc && nc < base + 32;
-        if (pmax(rhs_here ? 1 : 0)) limit_rows(x, rhs_here, bv == nc);
+        if (pmax(rhs_here ? 1 : 0)) {
+            limit_rows(x, rhs_here, bv == nc);
+            if (kSpec && rhs_here) {
+                const unsigned spec = nspec <= nN ? low_bits(nmask, nspec) : (nmask | low_bits(fmask, nspec - nN));
+                rem = limact & ~spec;
+                total += __popc(rem);
+            }
+            total_max = pmax(total);
+        }
         STAMP(9);
         file_row(x, on, r, kd, a);
         STAMP(10);
