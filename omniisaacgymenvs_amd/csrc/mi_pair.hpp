@@ -865,11 +865,14 @@ MI_D void pair_artic_substep(const DevModel& m, const WaveTabs& t, const DevStat
                         const float lim = mu * lamn;
                         const float mine = __builtin_amdgcn_fmed3f(lam + (b - v) * ia, fric ? -lim : 0.0f,
                                                                    fric ? lim : __builtin_huge_valf());
-                        const float l0 = readlane(lam, rr);
-                        const float ln = readlane(mine, rr);
-                        if constexpr (rr % 3 == 0) lamn = rr < nnh ? ln : lamn;
-                        v += arr * (ln - l0);
-                        lam = lw == rr ? ln : lam;
+                        // the owner forms the lambda change itself (mine - lam there is exactly
+                        // ln - l0) and keeps mine as its lambda: one v_readlane per row (two for
+                        // the normal rows, whose lambda bounds the next two), no SGPR pair to
+                        // move back for the subtraction
+                        const float dl = readlane(mine - lam, rr);
+                        if constexpr (rr % 3 == 0) lamn = rr < nnh ? readlane(mine, rr) : lamn;
+                        v += arr * dl;
+                        lam = lw == rr ? mine : lam;
                     }
                 });
             }
