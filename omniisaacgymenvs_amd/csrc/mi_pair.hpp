@@ -731,7 +731,9 @@ MI_D void pair_artic_substep(const DevModel& m, const WaveTabs& t, const DevStat
             float lamn = 0.0f;
             sfor<0, RMAX>([&](auto RR) {   // fully unrolled: Ar / lamv stay register-indexed
                 constexpr int rr = RR;
-                if (rr < nrow_it) {           // uniform
+                // uniform, per group of four rows: rows past the count in the last group run as
+                // dead rows (owner ia 0, A entries 0: lambda and v unchanged), one branch per group
+                if ((rr & ~3) < nrow_it) {
                     __builtin_amdgcn_sched_barrier(0);
                     // the row's owner (lane rr of each half) holds v_rr, b, 1 / A_rr and its kind:
                     // it alone projects, and one broadcast hands the new lambda to its half
@@ -852,7 +854,7 @@ MI_D void pair_artic_substep(const DevModel& m, const WaveTabs& t, const DevStat
                 if constexpr (AR < 64) sfor<0, PA>([&](auto Q) { ab[Q] = ald(AR + Q); });
                 sfor<0, 64>([&](auto RR) {
                     constexpr int rr = RR;
-                    if (rr < nrow_it) {
+                    if ((rr & ~3) < nrow_it) {   // per group of four rows, as in the narrow sweeps
                         __builtin_amdgcn_sched_barrier(0);
                         float arr;
                         if constexpr (rr < AR) {
