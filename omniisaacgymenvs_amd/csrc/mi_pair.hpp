@@ -91,7 +91,8 @@ template <class T>
 MI_D void ct_ltdl_pair(int lane, float (&Mc)[T::nvc]) {
     sfor_down<0, T::nv>([&](auto K) {
         constexpr int k = K;
-        __builtin_amdgcn_sched_barrier(0);
+        // no scheduling barrier per pivot: pivots of different limbs overlap (0.1262 -> 0.1254
+        // ms A/B; a barrier every 2 or 4 pivots the same; no spills either way)
         const int ln = lane_here(lane);
         const float inv = __builtin_amdgcn_rcpf(pbcc<k>(Mc[k]));
         sfor<T::dof.anc_start[k], T::dof.anc_start[k + 1]>([&](auto A) {
@@ -340,6 +341,7 @@ MI_D void pair_artic_substep(const DevModel& m, const WaveTabs& t, const DevStat
     float Mc[TP::nvc];
     ct_load_columns<TP>(Mx, lane, Mc);
     ct_ltdl_pair<TP>(lane, Mc);
+    STAMP(5);
     const float dvec = ct_dinv<TP>(lane, Mc);
     {
         const int dj = lane < nr ? lane : __builtin_popcount(mc.mask(lane < nv ? lane - nr + 1 : 0)) - 1;

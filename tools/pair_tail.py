@@ -56,6 +56,8 @@ def main():
     env.close()
     a = np.concatenate(rows).astype(np.float64)          # [waves x launches, 32]
     phases = dict(PHASES)
+    phases[5] = "P4a column loads + register LTDL"
+    phases[4] = "P4b 1/D + factor publish"
     phases[11] = "P10 pgs: u update"
     phases[27] = "P10 set-up: wide Delassus rows / narrow row data"
     phases[28] = "P10 pgs: sweeps"
@@ -63,7 +65,7 @@ def main():
     phases[30] = "P10 wide: J rows + v"
     phases[24] = "P10 narrow: J row + v"
     phases[25] = "P10 narrow: Delassus rows"
-    ph = [k for k in phases if k != 5]
+    ph = list(phases)
     tot = a[:, ph].sum(axis=1)
     order = np.argsort(tot)
     k = max(1, len(tot) // 50)
