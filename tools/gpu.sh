@@ -35,6 +35,16 @@ TAG=${TAG:-cur}
 RP="rocprofv3 --output-format csv"
 B="python3 bench.py --steps 30 --warmup 5 --no-cpu-baseline --fuse-envs 0 --no-side --task $TASK ${BARGS:-}"
 
+# the diagnostic stamps library stays off the box (.gpurunignore): the two stamps recipes build
+# it there (a few minutes of hipcc on the box's CPU) when it is missing
+stamps_lib() {
+  [ -f omniisaacgymenvs_amd/libmi_sim_stamps.so ] && return 0
+  ( while sleep 30; do echo "   building the stamps library ..."; done ) &
+  local tick=$!
+  run build_stamps 900 python -c "import __graft_entry__ as g; g.build_hip_stamps()"
+  kill $tick
+}
+
 run() {  # run <name> <timeout> <cmd...>; exit codes 0/1 (test failures) continue, others stop
   local name=$1 t=$2; shift 2
   echo "== $name: $*"
@@ -95,8 +105,10 @@ recipe() {
   freerun)
     for T in Humanoid Ant Cartpole; do run free_run_${T}_$TAG 300 python -u tools/free_run.py $T 4096; done ;;
   stamps)
+    stamps_lib
     for T in ${TASKS:-Humanoid Ant}; do run stamps_${T}_$TAG 150 python -u tools/phase_stamps.py $T 4096; done ;;
-  tail)   # slowest-wave phase stamps of the paired kernel (needs libmi_sim_stamps.so on the box)
+  tail)   # slowest-wave phase stamps of the paired kernel
+    stamps_lib
     for T in ${TASKS:-Humanoid}; do run tail_${T}_$TAG 150 python -u tools/pair_tail.py $T 4096 3; done ;;
   patha)
     run path_a 200 python -u tools/path_a_timing.py ;;
