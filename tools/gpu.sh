@@ -39,10 +39,11 @@ B="python3 bench.py --steps 30 --warmup 5 --no-cpu-baseline --fuse-envs 0 --no-s
 # it there (a few minutes of hipcc on the box's CPU) when it is missing
 stamps_lib() {
   [ -f omniisaacgymenvs_amd/libmi_sim_stamps.so ] && return 0
-  ( while sleep 30; do echo "   building the stamps library ..."; done ) &
+  ( for _ in $(seq 1 20); do sleep 30; echo "   building the stamps library ..."; done ) &   # bounded: 10 min
   local tick=$!
-  run build_stamps 900 python -c "import __graft_entry__ as g; g.build_hip_stamps()"
-  kill $tick
+  trap "kill $tick 2>/dev/null" EXIT
+  run build_stamps 600 python -c "import __graft_entry__ as g; g.build_hip_stamps()"
+  kill $tick 2>/dev/null
 }
 
 run() {  # run <name> <timeout> <cmd...>; exit codes 0/1 (test failures) continue, others stop
