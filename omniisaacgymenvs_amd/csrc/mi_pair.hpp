@@ -108,14 +108,18 @@ MI_D void ct_ltdl_pair(int lane, float (&Mc)[T::nvc]) {
 // with R, the rhs entries R[c]: fn(c, S_c, R[c]) with the loads of DOF c + SP issued before DOF c's
 // arithmetic, into a ring of SP + 1 buffers indexed at compile time. Each DOF's arithmetic is a
 // handful of VALU ops, so with the loads in line every DOF exposed a full LDS round trip.
-template <class TP, int SP, bool WITH_R, class F>
+// S0: the first DOF whose S_c is read (the callers that know S_c of the free root's six DOFs
+// at compile time pass TP::nr; fn then gets an unread sv for c < S0).
+template <class TP, int SP, bool WITH_R, int S0 = 0, class F>
 MI_D void sdof_loop(const float* Ss, const float* R, F&& fn) {
     constexpr int NB = SP + 1;
     float sb[NB][6], rb[NB];
     auto load = [&](auto C) {
         constexpr int c = C;
+        if constexpr (c >= S0) {
 #pragma unroll
-        for (int q = 0; q < 6; ++q) sb[c % NB][q] = Ss[6 * c + q];
+            for (int q = 0; q < 6; ++q) sb[c % NB][q] = Ss[6 * c + q];
+        }
         if constexpr (WITH_R) rb[c % NB] = R[c];
     };
     sfor<0, (SP < TP::nv ? SP : TP::nv)>([&](auto C) { load(C); });
@@ -147,6 +151,16 @@ MI_D void sdof_loop(const float* Ss, const float* R, F&& fn) {
 #define MI_PAIR_SDOF_PD 6   // DOF-loop prefetch depth (sdof_loop): 2 -> 0.1609 ms, 4 -> 0.1592 (A/B, round 3); 6: 0.1356 -> 0.1349 (round 4)
 #endif
 
+// S_c . f for DOF c: the free root's six DOFs have unit subspaces (linear x, y, z then angular
+// x, y, z: the P1 set-up below), so their dot product is one component of f (what dot6 with a
+// unit vector returns, up to the sign of a zero); the joint DOFs' from S_c in LDS
+template <class TP, int c>
+MI_D float sdot(const float (&sv)[6], const float (&f)[6]) {
+    if constexpr (TP::nr == 6 && c < 6) return f[c < 3 ? 3 + c : c - 3];
+    else return dot6(sv, f);
+}
+constexpr int sdof_first_loaded(int nr) { return nr == 6 ? 6 : 0; }
+
 // J_r[c] of this lane's constraint row r (contact or limit), for every DOF c (lane = row)
 template <class TP>
 MI_D void pair_jrow(const MC& mc, const WaveTabs& t, const float* sm, int r, int nr,
@@ -166,9 +180,9 @@ MI_D void pair_jrow(const MC& mc, const WaveTabs& t, const float* sm, int r, int
         sg = sm[t.s_lsg + kdof - nr];
     }
     const float* Ss = sm + t.s_S;
-    sdof_loop<TP, MI_PAIR_SDOF_PD, false>(Ss, nullptr, [&](auto C, const float (&sv)[6], float) {
+    sdof_loop<TP, MI_PAIR_SDOF_PD, false, sdof_first_loaded(TP::nr)>(Ss, nullptr, [&](auto C, const float (&sv)[6], float) {
         constexpr int c = C;
-        const float v = dot6(sv, f);
+        const float v = sdot<TP, c>(sv, f);
         const bool ia = (msk >> c) & 1u, ib = (msk2 >> c) & 1u;
         float xc = (ia ? v : 0.0f) - (ib ? v : 0.0f);
         asm volatile("" : "+v"(xc));
@@ -329,9 +343,9 @@ MI_D void pair_artic_substep(const DevModel& m, const WaveTabs& t, const DevStat
             r += st.eff[sx(st, k - nr, i)] - damp * us[k];
         }
         rhs[k] = r;
-        sdof_loop<TP, MI_PAIR_SDOF_PD, false>(Ss, nullptr, [&](auto J, const float (&sj)[6], float) {
+        sdof_loop<TP, MI_PAIR_SDOF_PD, false, sdof_first_loaded(TP::nr)>(Ss, nullptr, [&](auto J, const float (&sj)[6], float) {
             constexpr int j = J;
-            Mx[k * nv + j] = dot6(sj, f);
+            Mx[k * nv + j] = sdot<TP, j>(sj, f);
         });
         Mx[k * nv + k] = diag;
     }
@@ -632,9 +646,9 @@ MI_D void pair_artic_substep(const DevModel& m, const WaveTabs& t, const DevStat
             msk2 = l2 >= 0.0f ? mc.mask((int)l2) : 0u;
             contact_row_f<TP::kSelf>(sm, t, r, f);
         }
-        sdof_loop<TP, MI_PAIR_SDOF_PD, true>(Ss, rhs, [&](auto C, const float (&sv)[6], float rcl) {
+        sdof_loop<TP, MI_PAIR_SDOF_PD, true, sdof_first_loaded(TP::nr)>(Ss, rhs, [&](auto C, const float (&sv)[6], float rcl) {
             constexpr int c = C;
-            const float v = dot6(sv, f);
+            const float v = sdot<TP, c>(sv, f);
             const bool ia = (msk >> c) & 1u, ib = (msk2 >> c) & 1u;
             float xc = (ia ? v : 0.0f) - (ib ? v : 0.0f);
             float rc = rcl;
