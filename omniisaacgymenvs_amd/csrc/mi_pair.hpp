@@ -130,7 +130,7 @@ MI_D void sdof_loop(const float* Ss, const float* R, F&& fn) {
     });
 }
 #ifndef MI_PAIR_WIDE_PD
-#define MI_PAIR_WIDE_PD 12   // W-row prefetch depth of the wide Delassus set-up (A/B round 4: 4 0.1360, 8 0.1335, 12 0.1331 ms)
+#define MI_PAIR_WIDE_PD 16   // W-row prefetch depth of the wide Delassus set-up (A/B round 4: 4 0.1360, 8 0.1335, 12 0.1331 ms; later 12 0.1240, 16 0.1226)
 #endif
 #ifndef MI_PAIR_WIDE_AREG
 #define MI_PAIR_WIDE_AREG 32   // wide-PGS Delassus rows in registers (0, 32 or 64); the rest streamed
