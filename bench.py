@@ -162,9 +162,9 @@ def cpu_baseline(task_name: str, env, seconds: float) -> dict:
       * the C oracle's fused step of the metric's task (oracle/oracle.c, the build's CPU
         restatement: the reference's PhysX-CPU path is closed and absent) at 1, 4 and all granted
         threads, with the env count scaled per thread count to the time budget;
-      * config 1 (Cartpole, 16 envs): the reference's Cartpole task as torch ops on CPU tensors
-        (oracle/torch_cartpole.py, CPU torch as the reference's pipeline=cpu runs it) and the C
-        oracle, 1 thread each."""
+      * config 1 (Cartpole, 16 envs): the product's CPU pipeline (make_env(device="cpu"): the
+        reference's Cartpole task as torch ops on CPU tensors, as its pipeline=cpu runs it) and
+        the C oracle, 1 thread each."""
     import numpy as np
     from oracle.oracle import OracleSim, lib as orc_lib, make_buffers
 
@@ -216,7 +216,6 @@ def cpu_baseline(task_name: str, env, seconds: float) -> dict:
     try:
         import torch
         from omniisaacgymenvs_amd.robots.articulations import GridCloner
-        from oracle.torch_cartpole import CpuTorchCartpole
         from tests.helpers import sim_params, task_params_from_cfg
         tp1, m1, _ = task_params_from_cfg("Cartpole")
         sp1 = sim_params(rest_offset=0.001)
@@ -232,16 +231,17 @@ def cpu_baseline(task_name: str, env, seconds: float) -> dict:
         threads0 = torch.get_num_threads()
         torch.set_num_threads(1)
         try:
-            torch.manual_seed(42)
-            ct = CpuTorchCartpole(m1, sp1, tp1, 16, seed=42, noise="torch")
-            ct.reset()
+            from omniisaacgymenvs_amd.utils.task_util import make_env
+            ce = make_env("Cartpole", num_envs=16, device="cpu", seed=42)
+            ce.reset()
             at = [torch.from_numpy(a1[k]) for k in range(8)]
-            c1t = {"value": round(protocol(lambda k: ct.step(at[k % 8]), 16), 1), "unit": "env-steps/s",
-                   "cores": 1, "kind": "port",
-                   "sample": "Cartpole 16 envs on CPU torch (oracle/torch_cartpole.py: the reference's "
-                             "cartpole.py:80-162 task ops + VecEnvRLGames.step sequence, analytic "
-                             "dynamics, torch.rand resets), 200 warm-up + median of 5 x 2000 env-steps, "
-                             "1 torch thread"}
+            c1t = {"value": round(protocol(lambda k: ce.step(at[k % 8]), 16), 1), "unit": "env-steps/s",
+                   "cores": 1, "kind": "product",
+                   "sample": "Cartpole 16 envs on the product's CPU pipeline (make_env(device='cpu'): "
+                             "CartpoleTask's cartpole.py:80-162 torch ops over robots/cpu_cartpole.py, "
+                             "VecEnvRLGames.step method by method, Philox resets), 200 warm-up + median "
+                             "of 5 x 2000 env-steps, 1 torch thread"}
+            ce.close()
         finally:
             torch.set_num_threads(threads0)
     except Exception as e:   # noqa: BLE001 - the side leg must not sink the bench line

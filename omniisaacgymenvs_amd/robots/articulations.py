@@ -91,7 +91,8 @@ class ArticulationView:
         dev = torch.device(device)
         if dev.type != "cuda":
             raise N.NativeUnavailable(
-                f"sim_device={device!r}: libmi_sim.so runs on the GPU only (no CPU fallback)")
+                f"sim_device={device!r}: libmi_sim.so runs on the GPU only (no CPU fallback; the "
+                f"CPU pipeline, robots/cpu_cartpole.py, serves the Cartpole task alone)")
         lib = N.lib()
         self.device = dev
         self.count = int(num_envs)

@@ -1,56 +1,29 @@
-"""BASELINE config 0: Cartpole, 16 envs, CPU — plumbing + obs/reward parity, with a dummy
-PPO rollout through the rl_games IVecEnv contract (rlgames_utils.py:94-118).
+"""BASELINE config 1: Cartpole, 16 envs, CPU torch — plumbing + obs/reward parity, with a
+dummy PPO rollout through the rl_games IVecEnv contract (rlgames_utils.py:94-118).
 
-The product refuses to run without a GPU (no CPU fallback), so on CPU the env under the
-VecEnv contract is a TEST twin backed by the CPU oracle (test infrastructure only). It keeps
-the reference's step semantics (actions clamped to ±1, obs clamped to ±5, reset consumes one
-step, terminal obs returned, re-init at the next step) and is driven through RLGPUEnv.
+The env is the PRODUCT's CPU pipeline (make_env(..., device="cpu"): CartpoleTask over
+robots/cpu_cartpole.py, VecEnvRLGames stepping it method by method, as the reference's
+pipeline=cpu does). It keeps the reference's step semantics (actions clamped to ±1, obs clamped
+to ±5, reset consumes one step, terminal obs returned, re-init at the next step) and is driven
+through RLGPUEnv. Parity against the C oracle: tests/test_cpu_pipeline_cartpole.py.
 """
 import numpy as np
 import torch
 
-from omniisaacgymenvs_amd.robots.articulations import GridCloner
 from omniisaacgymenvs_amd.utils.rlgames.rlgames_utils import RLGPUEnv, register_env
-from omniisaacgymenvs_amd.utils.spaces import Box
-from oracle.oracle import OracleSim, make_buffers
-from tests.helpers import sim_params, task_params_from_cfg
+from omniisaacgymenvs_amd.utils.task_util import make_env
 
 N_ENVS, HORIZON = 16, 16
 
 
-class OracleCartpoleVecEnv:
-    """VecEnvRLGames contract over the CPU oracle (tests only)."""
-
-    def __init__(self, num_envs=N_ENVS, seed=42):
-        tp, m, _ = task_params_from_cfg("Cartpole")
-        self.tp = tp
-        self.num_envs, self.num_states = num_envs, 0
-        self.action_space = Box(-np.ones(1), np.ones(1))
-        self.observation_space = Box(-np.inf * np.ones(4), np.inf * np.ones(4))
-        self.state_space = Box(np.zeros(0), np.zeros(0))
-        self.orc = OracleSim(m, sim_params(rest_offset=0.001), num_envs,
-                             GridCloner(4.0).get_clone_positions(num_envs), seed=seed)
-        self.orc.configure(tp)
-        self.b = make_buffers(num_envs, 4, 1)
-        self.b["reset"][:] = 1
-
-    def step(self, actions):
-        a = actions.detach().cpu().numpy().astype(np.float32).reshape(self.num_envs, 1)
-        self.orc.env_step(a, 2, self.b)
-        obs = torch.from_numpy(self.b["obs"].copy())
-        return ({"obs": obs, "states": torch.zeros((self.num_envs, 0))},
-                torch.from_numpy(self.b["rew"].copy()), torch.from_numpy(self.b["reset"].copy()), {})
-
-    def reset(self):
-        self.b["reset"][:] = 1
-        return self.step(torch.zeros((self.num_envs, 1)))[0]
-
-    def get_number_of_agents(self):
-        return 1
+def cartpole_cpu_env(seed=42, rank=0, world=1, num_envs=N_ENVS):
+    """The product's config-1 env: shard `rank` of a `world`-rank run (global env ids)."""
+    return make_env("Cartpole", num_envs=num_envs, device="cpu", seed=seed,
+                    env_id_offset=rank * num_envs, global_num_envs=world * num_envs)
 
 
 def test_config0_rollout_plumbing():
-    register_env("rlgpu_test", lambda **kw: OracleCartpoleVecEnv())
+    register_env("rlgpu_test", lambda **kw: cartpole_cpu_env())
     env = RLGPUEnv("rlgpu_test", N_ENVS)
     info = env.get_env_info()
     assert info["observation_space"].shape == (4,) and info["action_space"].shape == (1,)
@@ -100,16 +73,18 @@ def test_config0_rollout_plumbing():
 
 
 def test_config0_obs_reward_parity_with_task_math():
-    """The env's obs/reward equal the cartpole.py formulas applied to the returned state."""
-    env = OracleCartpoleVecEnv()
+    """The env's rewards / dones equal the cartpole.py formulas applied to the task's
+    (unclamped) observations of the same step."""
+    env = cartpole_cpu_env()
     env.reset()
     for k in range(30):
         obs, rew, done, _ = env.step(torch.rand((N_ENVS, 1)) * 2 - 1)
-        o = env.b["obs_task"]
+        o = env.task.obs_buf.numpy()
         x, xd, th, thd = o[:, 0], o[:, 1], o[:, 2], o[:, 3]
         r = 1.0 - th * th - 0.01 * np.abs(xd) - 0.005 * np.abs(thd)
         r = np.where(np.abs(x) > 3.0, -2.0, r)
         r = np.where(np.abs(th) > np.float32(np.pi / 2), -2.0, r).astype(np.float32)
         np.testing.assert_allclose(rew.numpy(), r, rtol=1e-6, atol=1e-6)
-        d = (np.abs(x) > 3.0) | (np.abs(th) > np.float32(np.pi / 2)) | (env.b["progress"] >= 500)
+        d = (np.abs(x) > 3.0) | (np.abs(th) > np.float32(np.pi / 2)) | (env.task.progress_buf.numpy() >= 500)
         np.testing.assert_array_equal(done.numpy(), d.astype(np.int64))
+        np.testing.assert_array_equal(obs["obs"].numpy(), np.clip(o, -5.0, 5.0))

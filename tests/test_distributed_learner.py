@@ -7,7 +7,7 @@ multi_gpu: True (cfg/train/*PPO.yaml `multi_gpu`):
     gradients and the KL are averaged by one all-reduce per minibatch, the normalisation
     statistics merge the ranks' moments — replicas stay identical, and the averaged gradient is
     the gradient of one learner on the union of the ranks' minibatches.
-The env is the oracle-backed Cartpole test twin (test infrastructure: the product refuses CPU)."""
+The env is the product's CPU-pipeline Cartpole, one shard per rank (global env ids)."""
 import os
 
 import numpy as np
@@ -25,10 +25,10 @@ def _worker(rank, world, port, q):
     dist.init_process_group("gloo", rank=rank, world_size=world)
     from omniisaacgymenvs_amd.rlg.a2c_continuous import A2CAgent
     from omniisaacgymenvs_amd.utils.rlgames.rlgames_utils import RLGPUEnv, register_env
-    from tests.test_cartpole_cpu_rollout import OracleCartpoleVecEnv
+    from tests.test_cartpole_cpu_rollout import cartpole_cpu_env
     from tests.test_rl_cpu import _cartpole_cpu_params
 
-    register_env(f"rlgpu_mg{rank}", lambda **kw: OracleCartpoleVecEnv(seed=100 + rank))
+    register_env(f"rlgpu_mg{rank}", lambda **kw: cartpole_cpu_env(seed=100, rank=rank, world=world))
     params = _cartpole_cpu_params()
     params["config"]["multi_gpu"] = True
     params["config"]["multi_gpu_mode"] = "central"
@@ -101,10 +101,10 @@ def _dp_worker(rank, world, port, q):
     dist.init_process_group("gloo", rank=rank, world_size=world)
     from omniisaacgymenvs_amd.rlg.a2c_continuous import A2CAgent
     from omniisaacgymenvs_amd.utils.rlgames.rlgames_utils import RLGPUEnv, register_env
-    from tests.test_cartpole_cpu_rollout import OracleCartpoleVecEnv
+    from tests.test_cartpole_cpu_rollout import cartpole_cpu_env
     from tests.test_rl_cpu import _cartpole_cpu_params
 
-    register_env(f"rlgpu_dp{rank}", lambda **kw: OracleCartpoleVecEnv(seed=200 + rank))
+    register_env(f"rlgpu_dp{rank}", lambda **kw: cartpole_cpu_env(seed=200, rank=rank, world=world))
     params = _cartpole_cpu_params()
     params["config"]["multi_gpu"] = True          # multi_gpu_mode defaults to data_parallel
     agent = A2CAgent(RLGPUEnv(f"rlgpu_dp{rank}", N_ENVS), params, run_dir=f"/tmp/dp_{port}_{rank}")

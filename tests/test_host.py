@@ -139,10 +139,13 @@ def test_product_fails_loudly_without_gpu():
         pytest.skip("GPU present")
     from omniisaacgymenvs_amd.utils.task_util import make_env
 
+    # sim_device=cpu is the reference's CPU pipeline: served for Cartpole only
+    # (robots/cpu_cartpole.py), refused for the articulated robots
     with pytest.raises(N.NativeUnavailable):
-        make_env("Cartpole", num_envs=8, device="cpu")
-    with pytest.raises(RuntimeError):
-        make_env("Humanoid", num_envs=8, device="cuda:0")
+        make_env("Humanoid", num_envs=8, device="cpu")
+    for task in ("Cartpole", "Humanoid"):
+        with pytest.raises(RuntimeError):
+            make_env(task, num_envs=8, device="cuda:0")
 
 
 def test_generated_topologies_up_to_date():

@@ -1,7 +1,7 @@
 """PPO learner on CPU: the torch statements of its ops against numpy
 restatements of rl-games 1.5.2, and BASELINE config 0 — Cartpole, 16 envs, CPU torch, the
-learner's full train loop over the IVecEnv contract (env = the oracle-backed test twin of
-tests/test_cartpole_cpu_rollout.py; the product refuses to run without a GPU)."""
+learner's full train loop over the IVecEnv contract (env = the product's CPU pipeline,
+make_env("Cartpole", device="cpu"), tests/test_cartpole_cpu_rollout.py)."""
 import math
 import os
 
@@ -15,7 +15,7 @@ from omniisaacgymenvs_amd.rlg.models import ModelA2CContinuousLogStd, RunningMea
 from omniisaacgymenvs_amd.utils.hydra_cfg.hydra_utils import compose
 from omniisaacgymenvs_amd.utils.rlgames.rlgames_utils import RLGPUEnv, register_env
 from tests.rl_ref import gae_np
-from tests.test_cartpole_cpu_rollout import N_ENVS, OracleCartpoleVecEnv
+from tests.test_cartpole_cpu_rollout import N_ENVS, cartpole_cpu_env
 
 
 def test_gae_torch_matches_numpy():
@@ -125,7 +125,7 @@ def _cartpole_cpu_params(minibatch=64):
 def test_config0_ppo_train_loop_cpu(tmp_path):
     """Config 0: the learner's full epoch (rollout, GAE, value/advantage normalisation, PPO
     minibatches with the adaptive LR, meters, checkpoints) on CPU torch over RLGPUEnv."""
-    register_env("rlgpu_cfg0", lambda **kw: OracleCartpoleVecEnv())
+    register_env("rlgpu_cfg0", lambda **kw: cartpole_cpu_env())
     env = RLGPUEnv("rlgpu_cfg0", N_ENVS)
     params = _cartpole_cpu_params()
     params["config"]["save_frequency"] = 2
@@ -150,7 +150,7 @@ def test_config0_ppo_train_loop_cpu(tmp_path):
 
 
 def test_minibatch_must_divide_batch():
-    register_env("rlgpu_cfg0b", lambda **kw: OracleCartpoleVecEnv())
+    register_env("rlgpu_cfg0b", lambda **kw: cartpole_cpu_env())
     params = _cartpole_cpu_params(minibatch=8192)        # CartpolePPO default: 256 % 8192 != 0
     try:
         A2CAgent(RLGPUEnv("rlgpu_cfg0b", N_ENVS), params)
