@@ -12,7 +12,9 @@
  *                        eval mode: action ~ Normal(mu, exp(logstd)) and its neg-log-prob
  *   mi_rl_ppo_loss     — rl_games algos_torch/a2c_continuous.py calc_gradients: the PPO loss
  *                        terms, the policy KL and the loss gradient w.r.t. the network heads
- * The MLP GEMMs stay in hipBLASLt (torch.nn.Linear).
+ *   mi_rl_policy_step  — the rollout's whole policy evaluation (normalisation, MLP, heads,
+ *                        sampling) as one f32-MFMA launch
+ * The training minibatch GEMMs stay in hipBLASLt (torch.nn.Linear, autograd).
  *
  * Conventions: as mi_sim.h — 0 on success or a negative MI_E_* code (mi_rl_last_error());
  * device pointers; `stream` is a hipStream_t passed as void*; stream-ordered, non-blocking.
@@ -79,6 +81,38 @@ int32_t mi_rl_ppo_loss(const void* mu, int32_t mu_half, const float* logstd, con
                        float entropy_coef, float bounds_coef, const float* grad_scale,
                        void* grad_mu, void* grad_value, float* grad_logstd_part,
                        float* sums_part, float* mu_out, float* sigma_out, void* stream);
+
+/* The rollout policy of rl_games a2c_continuous (play_steps: ModelA2CContinuousLogStd in eval mode
+ * -> get_action_values), fused: RunningMeanStd input normalisation, the MLP trunk (ELU), the mu
+ * and value heads, value un-normalisation and the Gaussian sample of mi_rl_sample_gauss, for
+ * every row, in ONE launch (f32 MFMA GEMMs, activations in LDS). Network: HumanoidPPO.yaml:24-25
+ * (units [400, 200, 100], elu, fixed sigma); torch nn.Linear weights [out][in]. */
+#define MI_RL_MAX_HIDDEN 4
+typedef struct {
+    int32_t num_obs;                          /* O */
+    int32_t num_actions;                      /* A (<= 64) */
+    int32_t num_hidden;                       /* hidden layers, 1 .. MI_RL_MAX_HIDDEN */
+    int32_t units[MI_RL_MAX_HIDDEN];          /* hidden widths (<= 512) */
+    const float* w[MI_RL_MAX_HIDDEN + 2];     /* device: hidden layers, then mu [A][u], value [1][u] */
+    const float* b[MI_RL_MAX_HIDDEN + 2];
+} mi_rl_mlp;
+/* floats of the packed weight buffer (zero-padded [N16][K16] per layer + bias; the heads as one
+ * [A + 1] layer), or -1 on a bad description */
+int64_t mi_rl_mlp_packed_size(const mi_rl_mlp* mlp);
+/* Repack the network's current weights (stream-ordered; call after every weight update). */
+int32_t mi_rl_mlp_pack(const mi_rl_mlp* mlp, float* packed, void* stream);
+/* For rows n < num_rows of obs [R][O]: obs_out[n] = obs[n] (the rollout slot; may be NULL);
+ * x = clamp((obs - mean) / sqrt(var + eps), +-5) when obs_mean / obs_var (f64 running
+ * statistics) are given; mu, v = heads(MLP(x)); values[n] = sqrt(var_v + eps) clamp(v, +-5) +
+ * mean_v when value_mean / value_var are given, else v; sigma = exp(logstd) ([A], fixed sigma);
+ * actions / neglogp exactly as mi_rl_sample_gauss(mu, logstd, 0, ..., seed, counter_base,
+ * counter_offset); mu_out / sigma_out [R][A]. Any output may be NULL (neglogp needs actions). */
+int32_t mi_rl_policy_step(const mi_rl_mlp* mlp, const float* packed, const float* obs,
+                          int32_t num_rows, const double* obs_mean, const double* obs_var,
+                          const double* value_mean, const double* value_var, float eps,
+                          const float* logstd, uint64_t seed, const int64_t* counter_base,
+                          uint64_t counter_offset, float* obs_out, float* actions, float* neglogp,
+                          float* values, float* mu_out, float* sigma_out, void* stream);
 
 #ifdef __cplusplus
 }

@@ -135,6 +135,9 @@ MI_D void sdof_loop(const float* Ss, const float* R, F&& fn) {
 #ifndef MI_PAIR_WIDE_AREG
 #define MI_PAIR_WIDE_AREG 32   // wide-PGS Delassus rows in registers (0, 32 or 64); the rest streamed
 #endif
+// wide-PGS Delassus rows that live in the wave's global scratch (rows AREG..63): the scratch
+// holds exactly these, (64 - AREG) rows x 64 lanes of f32 per resident-or-not wave (N / 2 waves)
+constexpr int kWideScratchRows = 64 - MI_PAIR_WIDE_AREG;
 #ifndef MI_PAIR_WIDE_AP
 #define MI_PAIR_WIDE_AP 8   // Delassus rows streamed ahead of the wide sweeps' chain
 #endif
@@ -804,11 +807,13 @@ MI_D void pair_artic_substep(const DevModel& m, const WaveTabs& t, const DevStat
         constexpr int AR = MI_PAIR_WIDE_AREG;   // Delassus rows kept in registers; the rest streamed
         const int l64 = pair_l64(), me = l64 >> 5;
         const int kc = l64 < NV ? l64 : 0;
-        // this wave's scratch (i >> 1: the same for both halves), addressed through a buffer
-        // resource: one lane offset register for every row (row s at soffset 256 s)
+        // this wave's scratch (i >> 1: the same for both halves) holds rows AR..63, addressed
+        // through a buffer resource: one lane offset register for every row (row s at soffset
+        // 256 (s - AR)); loads past the record range (prefetch beyond row 63) return 0
         const int wv = __builtin_amdgcn_readfirstlane(i >> 1);
+        constexpr int WR = kWideScratchRows > 0 ? kWideScratchRows : 1;
         const __amdgpu_buffer_rsrc_t ars = __builtin_amdgcn_make_buffer_rsrc(
-            (void*)(t.g_wa + (size_t)wv * (64 * 64)), (short)0, 64 * 64 * (int)sizeof(float), 0x00020000);
+            (void*)(t.g_wa + (size_t)wv * (WR * 64)), (short)0, WR * 64 * (int)sizeof(float), 0x00020000);
         const int avo = l64 * (int)sizeof(float);
         STAMP(29);
         for (int h = 0; h < 2; ++h) {
@@ -834,7 +839,7 @@ MI_D void pair_artic_substep(const DevModel& m, const WaveTabs& t, const DevStat
 #pragma unroll
                         for (int q = 0; q < 4; ++q)
                             __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(unsigned, a[q]), ars, avo,
-                                                                  (g0 + q) * 256, 0);
+                                                                  (g0 + q - AR) * 256, 0);
                     }
                 }
                 if constexpr (g0 < AR) { Ar[g0] = a[0]; Ar[g0 + 1] = a[1]; Ar[g0 + 2] = a[2]; Ar[g0 + 3] = a[3]; }
@@ -854,7 +859,7 @@ MI_D void pair_artic_substep(const DevModel& m, const WaveTabs& t, const DevStat
                 asm volatile("" : "+s"(nrow_it));
                 float lamn = 0.0f;
                 // rows rr .. rr + PA - 1 of A in flight (rows past the env's count are loaded but
-                // never used: the scratch is allocated for 64 rows and zeroed at creation)
+                // never used: the scratch is allocated for rows AR..63 and zeroed at creation)
                 // a fresh pointer each sweep: the loads must not be hoisted out of the sweep loop
                 // (they would all stay live: the register peak this scratch is here to remove)
                 int vo = avo, lw = l64;
@@ -862,7 +867,7 @@ MI_D void pair_artic_substep(const DevModel& m, const WaveTabs& t, const DevStat
                 // out of the sweep loop (64 SGPR-pair masks would spill and reload per row)
                 asm volatile("" : "+v"(vo), "+v"(lw));
                 auto ald = [&](int r) {
-                    return __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(ars, vo, r * 256, 0));
+                    return __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(ars, vo, (r - AR) * 256, 0));
                 };
                 // rows AR.. streamed: their first PA loads are issued before the sweep, so the
                 // register rows' steps hide their latency

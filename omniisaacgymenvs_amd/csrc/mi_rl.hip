@@ -213,6 +213,241 @@ __global__ __launch_bounds__(256) void k_ppo_loss(
     }
 }
 
+// ---------------------------------------------------------------------------------------
+// Rollout policy step: rl_games ModelA2CContinuousLogStd in eval mode (running-mean-std input
+// normalisation, the MLP trunk with ELU, the mu / value heads, value un-normalisation) plus the
+// Gaussian sample, for a tile of 16 rows per workgroup, in ONE launch. The GEMMs run on the f32
+// MFMA (v_mfma_f32_16x16x4_f32: exact f32 products, f32 accumulation — torch's fp32 matmul up to
+// summation order); activations stay in LDS between layers, weights stream from L2 (the packed
+// copy is ~0.55 MB for the Humanoid network, shared by every workgroup).
+//
+// MFMA operand maps (16x16x4 f32): lane l holds A[l & 15][k = l >> 4] and B[k = l >> 4][l & 15];
+// D register i of lane l is row 4 (l >> 4) + i, column l & 15. A K-chunk of 16 is consumed as 4
+// MFMAs whose k index is permuted (step s, lane group j = l >> 4 -> k = 4 j + s), so each lane
+// fetches ONE float4 of the activation row (LDS) and ONE float4 of the weight row (global) per
+// chunk and feeds component s to step s; the sum over the chunk is unchanged.
+// ---------------------------------------------------------------------------------------
+namespace {
+constexpr int kPolRows = 16;      // rows per workgroup (one MFMA row tile)
+constexpr int kPolWaves = 4;
+constexpr int kPolTiles = 8;      // max 16-column tiles per wave per layer (N_pad <= 512)
+constexpr int kPolMaxLayers = MI_RL_MAX_HIDDEN + 1;
+
+struct PolLayer {
+    int K, N, Kp, Np;             // true and padded (multiple of 16) input / output widths
+    long long w, b;               // float offsets of the packed [Np][Kp] weights and [Np] bias
+};
+struct PolDesc {
+    int O, A, L;                  // obs, actions, layers incl. the head (hidden + 1)
+    int xs;                       // LDS activation row stride (floats)
+    PolLayer ly[kPolMaxLayers];
+    long long total;              // floats in the packed buffer
+};
+
+int pad16(int x) { return (x + 15) & ~15; }
+
+int pol_desc(const mi_rl_mlp* m, PolDesc* d) {
+    if (!m) return fail(kNull, "mi_rl: null mlp");
+    if (m->num_obs <= 0 || m->num_actions <= 0 || m->num_actions > 64 || m->num_hidden < 1 ||
+        m->num_hidden > MI_RL_MAX_HIDDEN)
+        return fail(kShape, "mi_rl: mlp O=%d A=%d hidden=%d", m->num_obs, m->num_actions, m->num_hidden);
+    d->O = m->num_obs;
+    d->A = m->num_actions;
+    d->L = m->num_hidden + 1;
+    long long off = 0;
+    int in = m->num_obs, mx = pad16(m->num_obs);
+    for (int l = 0; l < d->L; ++l) {
+        const int out = l < m->num_hidden ? m->units[l] : m->num_actions + 1;   // head: mu | value
+        if (out <= 0 || pad16(out) > 16 * kPolWaves * kPolTiles)
+            return fail(kShape, "mi_rl: layer %d width %d (max %d)", l, out, 16 * kPolWaves * kPolTiles);
+        PolLayer& y = d->ly[l];
+        y.K = in; y.N = out; y.Kp = pad16(in); y.Np = pad16(out);
+        y.w = off; off += (long long)y.Np * y.Kp;
+        y.b = off; off += y.Np;
+        if (y.Np > mx) mx = y.Np;
+        in = out;
+    }
+    d->xs = mx + 4;               // +4 floats: rows start on different LDS banks
+    d->total = off;
+    return kOk;
+}
+
+__global__ void k_pol_pack(PolDesc d, mi_rl_mlp m, float* __restrict__ packed) {
+    // one thread per packed element (zeros in the padding)
+    const long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= d.total) return;
+    for (int l = 0; l < d.L; ++l) {
+        const PolLayer& y = d.ly[l];
+        const bool head = l == d.L - 1;
+        if (i >= y.w && i < y.w + (long long)y.Np * y.Kp) {
+            const int n = (int)((i - y.w) / y.Kp), k = (int)((i - y.w) % y.Kp);
+            float v = 0.0f;
+            if (k < y.K && n < y.N) {
+                if (!head) v = m.w[l][(size_t)n * y.K + k];
+                else v = n < d.A ? m.w[l][(size_t)n * y.K + k] : m.w[l + 1][k];   // mu rows, value row
+            }
+            packed[i] = v;
+            return;
+        }
+        if (i >= y.b && i < y.b + y.Np) {
+            const int n = (int)(i - y.b);
+            float v = 0.0f;
+            if (n < y.N) v = !head ? m.b[l][n] : (n < d.A ? m.b[l][n] : m.b[l + 1][0]);
+            packed[i] = v;
+            return;
+        }
+    }
+}
+
+typedef float pf4 __attribute__((ext_vector_type(4)));
+
+// one layer for the workgroup's 16 rows: Y[16][Np] = act(X[16][Kp] W^T + b), X / Y in LDS
+__device__ __forceinline__ void pol_layer(const PolLayer& y, const float* __restrict__ packed,
+                                          const float* X, float* Y, int xs, bool elu, int wave,
+                                          int lane) {
+    const int r = lane & 15, j = lane >> 4;
+    const int nt = y.Np >> 4;                     // column tiles
+    const int mine = (nt - wave + kPolWaves - 1) / kPolWaves;   // this wave's tiles: wave, +4, ..
+    const float* W = packed + y.w;
+    pf4 acc[kPolTiles];
+    pf4 wb[kPolTiles], wn[kPolTiles];
+#pragma unroll
+    for (int t = 0; t < kPolTiles; ++t) acc[t] = pf4{0.0f, 0.0f, 0.0f, 0.0f};
+    const int nc = y.Kp >> 4;
+    // this lane's weight row of tile t: n = 16 (wave + 4 t) + r, chunk c at k = 16 c + 4 j
+    auto wld = [&](int t, int c) {
+        return *(const pf4*)(W + (size_t)(16 * (wave + kPolWaves * t) + r) * y.Kp + 16 * c + 4 * j);
+    };
+#pragma unroll
+    for (int t = 0; t < kPolTiles; ++t)
+        if (t < mine) wb[t] = wld(t, 0);
+    for (int c = 0; c < nc; ++c) {
+        const pf4 a = *(const pf4*)(X + r * xs + 16 * c + 4 * j);
+        const bool more = c + 1 < nc;
+#pragma unroll
+        for (int t = 0; t < kPolTiles; ++t)
+            if (t < mine && more) wn[t] = wld(t, c + 1);
+#pragma unroll
+        for (int s = 0; s < 4; ++s) {
+#pragma unroll
+            for (int t = 0; t < kPolTiles; ++t)
+                if (t < mine) acc[t] = __builtin_amdgcn_mfma_f32_16x16x4f32(a[s], wb[t][s], acc[t], 0, 0, 0);
+        }
+#pragma unroll
+        for (int t = 0; t < kPolTiles; ++t)
+            if (t < mine && more) wb[t] = wn[t];
+    }
+    const float* B = packed + y.b;
+#pragma unroll
+    for (int t = 0; t < kPolTiles; ++t) {
+        if (t < mine) {
+            const int col = 16 * (wave + kPolWaves * t) + r;
+            const float bias = B[col];
+#pragma unroll
+            for (int i = 0; i < 4; ++i) {
+                float v = acc[t][i] + bias;
+                if (elu) v = v > 0.0f ? v : expm1f(v);
+                Y[(4 * j + i) * xs + col] = v;
+            }
+        }
+    }
+}
+
+__global__ __launch_bounds__(kPolRows * 16) void k_policy_step(
+    PolDesc d, const float* __restrict__ packed, const float* __restrict__ obs, int R,
+    const double* __restrict__ om, const double* __restrict__ ov, const double* __restrict__ vm,
+    const double* __restrict__ vv, float eps, const float* __restrict__ logstd, uint64_t seed,
+    const int64_t* __restrict__ cbase, uint64_t coff, float* __restrict__ obs_out,
+    float* __restrict__ act, float* __restrict__ nlp, float* __restrict__ val,
+    float* __restrict__ mu_out, float* __restrict__ sg_out) {
+#pragma clang fp contract(off)
+    extern __shared__ float pl[];                 // two [16][xs] activation tiles + noise [16][64]
+    float* X0 = pl;
+    float* X1 = pl + kPolRows * d.xs;
+    float* Z = pl + 2 * kPolRows * d.xs;
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int row0 = blockIdx.x * kPolRows;
+    const int O = d.O, A = d.A;
+    // input tile: raw obs -> obs_out (the rollout slot), normalised (running mean / std,
+    // clamped to +-5, rl_games RunningMeanStd.forward in eval mode) -> X0, zero padding
+    const int Kp0 = d.ly[0].Kp;
+    for (int e = tid; e < kPolRows * Kp0; e += blockDim.x) {
+        const int rr = e / Kp0, k = e - rr * Kp0, n = row0 + rr;
+        float x = 0.0f;
+        if (k < O && n < R) {
+            const float raw = obs[(size_t)n * O + k];
+            if (obs_out) obs_out[(size_t)n * O + k] = raw;
+            x = raw;
+            if (om) {
+                const float mean = (float)om[k], var = (float)ov[k];
+                x = (raw - mean) / sqrtf(var + eps);
+                x = fminf(fmaxf(x, -5.0f), 5.0f);
+            }
+        }
+        X0[rr * d.xs + k] = x;
+    }
+    __syncthreads();
+    float* X = X0;
+    float* Y = X1;
+    for (int l = 0; l < d.L; ++l) {
+        const bool head = l == d.L - 1;
+        pol_layer(d.ly[l], packed, X, Y, d.xs, !head, wave, lane);
+        __syncthreads();
+        float* tmp = X; X = Y; Y = tmp;
+    }
+    // X: head outputs [16][Np]: mu in columns 0..A-1, the normalised value in column A
+    const int nb = (A + 3) >> 2;
+    if (act) {   // Gaussian noise of k_sample_gauss: Philox block q of row n -> normals 4q .. 4q+3
+        const uint64_t counter = (cbase ? (uint64_t)cbase[0] : 0ull) + coff;
+        for (int e = tid; e < kPolRows * nb; e += blockDim.x) {
+            const int rr = e / nb, q = e - rr * nb, n = row0 + rr;
+            if (n >= R) continue;
+            float z[4];
+            normal4(seed, counter, (uint32_t)n, (uint32_t)q, z);
+#pragma unroll
+            for (int k = 0; k < 4; ++k) Z[rr * 64 + 4 * q + k] = z[k];
+        }
+    }
+    __syncthreads();
+    // element-wise outputs: mu, sigma = exp(logstd), action = mu + sigma z
+    for (int e = tid; e < kPolRows * A; e += blockDim.x) {
+        const int rr = e / A, jj = e - rr * A, n = row0 + rr;
+        if (n >= R) continue;
+        const float m = X[rr * d.xs + jj];
+        const float sg = expf(logstd[jj]);
+        if (mu_out) mu_out[(size_t)n * A + jj] = m;
+        if (sg_out) sg_out[(size_t)n * A + jj] = sg;
+        if (act) act[(size_t)n * A + jj] = m + sg * Z[rr * 64 + jj];
+    }
+    // per row: value (un-normalised: sqrt(var + eps) * clamp(v, +-5) + mean) and neglogp in
+    // k_sample_gauss's order
+    if (tid < kPolRows) {
+        const int n = row0 + tid;
+        if (n < R) {
+            float v = X[tid * d.xs + A];
+            if (vm) {
+                const float mean = (float)vm[0], var = (float)vv[0];
+                v = sqrtf(var + eps) * fminf(fmaxf(v, -5.0f), 5.0f) + mean;
+            }
+            if (val) val[n] = v;
+            if (act && nlp) {
+                float sq = 0.0f, lsum = 0.0f;
+                for (int jj = 0; jj < A; ++jj) {
+                    const float m = X[tid * d.xs + jj];
+                    const float ls = logstd[jj];
+                    const float sg = expf(ls);
+                    const float a = m + sg * Z[tid * 64 + jj];
+                    const float dd = (a - m) / sg;
+                    sq += dd * dd;
+                    lsum += ls;
+                }
+                nlp[n] = 0.5f * sq + 0.918938533204672742f * (float)A + lsum;
+            }
+        }
+    }
+}
+}  // namespace
+
 extern "C" {
 
 int32_t mi_rl_abi_version(void) { return MI_RL_ABI_VERSION; }
@@ -282,6 +517,44 @@ int32_t mi_rl_sample_gauss(const float* mu, const float* logstd, int32_t logstd_
                        (hipStream_t)stream, mu, logstd, logstd_stride, num_rows, num_actions, seed,
                        counter_base, counter_offset, actions, neglogp);
     return launch_check("mi_rl_sample_gauss");
+}
+
+int64_t mi_rl_mlp_packed_size(const mi_rl_mlp* mlp) {
+    PolDesc d;
+    if (pol_desc(mlp, &d)) return -1;
+    return d.total;
+}
+
+int32_t mi_rl_mlp_pack(const mi_rl_mlp* mlp, float* packed, void* stream) {
+    PolDesc d;
+    if (int rc = pol_desc(mlp, &d)) return rc;
+    if (!packed) return fail(kNull, "mi_rl_mlp_pack: null packed buffer");
+    for (int l = 0; l < mlp->num_hidden + 2; ++l)
+        if (!mlp->w[l] || !mlp->b[l]) return fail(kNull, "mi_rl_mlp_pack: null weight / bias of layer %d", l);
+    hipLaunchKernelGGL(k_pol_pack, dim3((unsigned)((d.total + kBlock - 1) / kBlock)), dim3(kBlock), 0,
+                       (hipStream_t)stream, d, *mlp, packed);
+    return launch_check("mi_rl_mlp_pack");
+}
+
+int32_t mi_rl_policy_step(const mi_rl_mlp* mlp, const float* packed, const float* obs,
+                          int32_t num_rows, const double* obs_mean, const double* obs_var,
+                          const double* value_mean, const double* value_var, float eps,
+                          const float* logstd, uint64_t seed, const int64_t* counter_base,
+                          uint64_t counter_offset, float* obs_out, float* actions, float* neglogp,
+                          float* values, float* mu_out, float* sigma_out, void* stream) {
+    PolDesc d;
+    if (int rc = pol_desc(mlp, &d)) return rc;
+    if (!packed || !obs || !logstd) return fail(kNull, "mi_rl_policy_step: null packed / obs / logstd");
+    if ((obs_mean == nullptr) != (obs_var == nullptr) || (value_mean == nullptr) != (value_var == nullptr))
+        return fail(kNull, "mi_rl_policy_step: mean and var come in pairs");
+    if (num_rows <= 0) return fail(kShape, "mi_rl_policy_step: R=%d", num_rows);
+    if (neglogp && !actions) return fail(kNull, "mi_rl_policy_step: neglogp needs actions");
+    const size_t lds = sizeof(float) * ((size_t)2 * kPolRows * d.xs + (size_t)kPolRows * 64);
+    hipLaunchKernelGGL(k_policy_step, dim3((num_rows + kPolRows - 1) / kPolRows), dim3(kPolRows * 16),
+                       lds, (hipStream_t)stream, d, packed, obs, num_rows, obs_mean, obs_var,
+                       value_mean, value_var, eps, logstd, seed, counter_base, counter_offset,
+                       obs_out, actions, neglogp, values, mu_out, sigma_out);
+    return launch_check("mi_rl_policy_step");
 }
 
 }  // extern "C"

@@ -86,6 +86,8 @@ struct mi_sim {
     bool mir_valid = false;
     hipStream_t mir_stream = nullptr;   // stream of the last refresh; a reader on another stream
     hipEvent_t mir_ev = nullptr;        // waits on mir_ev (recorded after that refresh)
+    hipStream_t mir_reader = nullptr;   // a stream other than the writer's that was handed the
+    hipEvent_t rd_ev = nullptr;         // mirrors: the next mirror write waits for its queued reads
     std::vector<float> lower, upper;  // host copy for mi_sim_info
     std::vector<void*> allocs;
     // launch timing (mi_sim_time_launches): every tev_every-th mi_env_step launch carries a
@@ -1478,10 +1480,14 @@ int mi_sim_create(const mi_model_desc* md, const mi_sim_params* prm, int32_t N, 
         if ((rc = dev_alloc(s, &p, sizeof(float) * (size_t)N * s->wt.g_row_stride))) return cleanup(rc);
         s->rows = (float*)p;
         s->wt.g_wa = nullptr;
-        if (s->pair) {   // wide-PGS Delassus scratch, one 64 x 64 block per wave (mi_pair.hpp)
-            const size_t nb = sizeof(float) * (size_t)(N / 2) * 64 * 64;
+        if (s->pair) {   // wide-PGS Delassus scratch: rows AREG..63 x 64 lanes per wave (mi_pair.hpp)
+            const size_t nb = sizeof(float) * (size_t)(N / 2) * 64 * (size_t)(kWideScratchRows > 0 ? kWideScratchRows : 1);
+            size_t fr = 0, tot = 0;
+            if (hipMemGetInfo(&fr, &tot) == hipSuccess && nb > fr)
+                return cleanup(fail(MI_E_ARG, "%d envs: the wide-PGS scratch needs %.1f MB (%d B per env), "
+                                              "%.1f MB of device memory free", N, nb / 1e6,
+                                    (int)(nb / (size_t)N), fr / 1e6));
             if ((rc = dev_alloc(s, &p, nb))) return cleanup(rc);
-            if (hipMemset(p, 0, nb) != hipSuccess) return cleanup(fail(MI_E_HIP, "hipMemset (Delassus scratch)"));
             s->wt.g_wa = (float*)p;
         }
         AL(ws, float, 64);
@@ -1533,6 +1539,7 @@ int mi_sim_destroy(mi_sim* s) {
     for (hipEvent_t e : s->tev) (void)hipEventDestroy(e);
     if (s->pending_ev) (void)hipEventDestroy(s->pending_ev);
     if (s->mir_ev) (void)hipEventDestroy(s->mir_ev);
+    if (s->rd_ev) (void)hipEventDestroy(s->rd_ev);
     for (void* p : s->allocs) (void)hipFree(p);
     delete s;
     return MI_OK;
@@ -1556,20 +1563,56 @@ int mi_sim_info(const mi_sim* s, int32_t* num_envs, int32_t* num_dof, int32_t* n
 #define STREAM(x) ((hipStream_t)(x))
 #define NEED(p) if (!(p)) return fail(MI_E_NULL, "%s: null %s", __func__, #p)
 
+static bool capturing(hipStream_t st) {
+    hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
+    return hipStreamIsCapturing(st, &cs) == hipSuccess && cs != hipStreamCaptureStatusNone;
+}
+
+// Before a launch on `w` overwrites the state mirrors: reads of them queued on another stream
+// (a getter called there, then torch's copies of the handed-out tensor) must finish first. The
+// host enqueued those reads before this call, so an event recorded on the reader's stream now
+// covers them.
+static int order_mirror_write(mi_sim* s, hipStream_t w) {
+    hipStream_t r = s->mir_reader;
+    s->mir_reader = nullptr;
+    if (!r || r == w || capturing(r) || capturing(w)) return MI_OK;
+    if (!s->rd_ev) HIP_TRY(hipEventCreateWithFlags(&s->rd_ev, hipEventDisableTiming));
+    HIP_TRY(hipEventRecord(s->rd_ev, r));
+    HIP_TRY(hipStreamWaitEvent(w, s->rd_ev, 0));
+    return MI_OK;
+}
+
+// After a launch on `w` wrote the mirrors: valid in stream order, with an event for readers on
+// other streams. Under stream capture nothing has run yet (and an event recorded at capture
+// time is not re-recorded by a replay), so the mirrors are left invalid: the next getter
+// refreshes them on its own stream.
+static int publish_mirrors(mi_sim* s, hipStream_t w) {
+    if (capturing(w)) {
+        s->mir_valid = false;
+        s->mir_stream = nullptr;
+        return MI_OK;
+    }
+    if (!s->mir_ev) HIP_TRY(hipEventCreateWithFlags(&s->mir_ev, hipEventDisableTiming));
+    HIP_TRY(hipEventRecord(s->mir_ev, w));
+    s->mir_stream = w;
+    s->mir_valid = true;
+    return MI_OK;
+}
+
 static int launch_sim(mi_sim* s, int substeps, hipStream_t stream) {
     s->mir_valid = false;
-    bool mirrored = false;
+    // the paired kernel refreshes the mirrors itself (free-root models: the state it writes is
+    // the mirrors' whole content)
+    const bool mirrored = s->wave && s->pair && s->mir[0] && s->dm.nr == 6 && (s->dm.S == 0 || s->mir[5]);
+    if (mirrored)
+        if (int rc = order_mirror_write(s, stream)) return rc;
     if (s->wave)
         with_topo(s->topo, [&](auto T) {
             if constexpr (has_pair<decltype(T)>()) {
                 if (s->pair) {
-                    // the paired kernel refreshes the mirrors itself (free-root models: the
-                    // state it writes is the mirrors' whole content)
                     Mirrors mir{};
-                    if (s->mir[0] && s->dm.nr == 6 && (s->dm.S == 0 || s->mir[5])) {
+                    if (mirrored)
                         for (int k = 0; k < 6; ++k) mir.p[k] = s->mir[k];
-                        mirrored = true;
-                    }
                     hipLaunchKernelGGL(k_sim_step_pair<decltype(T)>, wave_grid(s), wave_block(s), s->lds_bytes,
                                        stream, (const KParams*)s->kp_dev, substeps, mir);
                     return;
@@ -1582,19 +1625,10 @@ static int launch_sim(mi_sim* s, int substeps, hipStream_t stream) {
         hipLaunchKernelGGL(k_sim_step, grid_for(s, s->N), dim3(s->block), 0, stream, s->dm, s->ds,
                            s->sp, substeps);
     LAUNCH_CHECK();
-    if (mirrored) {   // valid after this launch, in stream order (mi_get_state_mirror)
-        if (!s->mir_ev) HIP_TRY(hipEventCreateWithFlags(&s->mir_ev, hipEventDisableTiming));
-        HIP_TRY(hipEventRecord(s->mir_ev, stream));
-        s->mir_stream = stream;
-        s->mir_valid = true;
-    }
+    if (mirrored) return publish_mirrors(s, stream);   // valid after this launch (mi_get_state_mirror)
     return MI_OK;
 }
 
-static bool capturing(hipStream_t st) {
-    hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
-    return hipStreamIsCapturing(st, &cs) == hipSuccess && cs != hipStreamCaptureStatusNone;
-}
 
 // Issue the substeps mi_sim_step deferred, on the stream they were requested on; a caller on
 // another stream waits for them. Substeps requested before a stream capture began cannot be
@@ -1733,10 +1767,13 @@ int mi_get_state_mirror(mi_sim* s, void* stream) {
     HIP_TRY(hipSetDevice(s->device));
     FLUSH(s, stream);
     if (s->mir_valid) {
-        if (STREAM(stream) != s->mir_stream)    // the refresh ran on another stream: order after it
+        if (STREAM(stream) != s->mir_stream) {  // the refresh ran on another stream: order after it
             HIP_TRY(hipStreamWaitEvent(STREAM(stream), s->mir_ev, 0));
+            s->mir_reader = STREAM(stream);     // and the next mirror write after this reader
+        }
         return MI_OK;
     }
+    if (int rc = order_mirror_write(s, STREAM(stream))) return rc;
     GFields f{};
     int nf = 0;
     const int fs = s->ds.fs, es = s->ds.es;
@@ -1748,11 +1785,7 @@ int mi_get_state_mirror(mi_sim* s, void* stream) {
     if (s->dm.S > 0) f.f[nf++] = {s->ds.sens, s->mir[5], 6 * s->dm.S, s->ds.sfs, s->ds.ses};
     const int rc = gather_fields(s, f, nf, stream);
     if (rc) return rc;
-    if (!s->mir_ev) HIP_TRY(hipEventCreateWithFlags(&s->mir_ev, hipEventDisableTiming));
-    HIP_TRY(hipEventRecord(s->mir_ev, STREAM(stream)));
-    s->mir_stream = STREAM(stream);
-    s->mir_valid = true;
-    return MI_OK;
+    return publish_mirrors(s, STREAM(stream));
 }
 
 int mi_sim_step(mi_sim* s, int32_t substeps, void* stream) {

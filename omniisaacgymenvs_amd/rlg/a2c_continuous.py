@@ -176,6 +176,9 @@ class A2CAgent:
             raise ValueError(f"minibatch_size {self.minibatch_size} must divide horizon x actors = "
                              f"{self.batch_size} (docs/troubleshoot.md:44)")
         self.num_minibatches = self.batch_size // self.minibatch_size
+        # frames one epoch adds over the whole job (rl_games multi_gpu: curr_frames * world):
+        # data-parallel ranks each step their own shard; central's batch is already global
+        self.frames_per_epoch = self.batch_size * (self.world if self.dp else 1)
         self.mini_epochs = int(cfg["mini_epochs"])
         self.gamma, self.tau = _f(cfg["gamma"]), _f(cfg["tau"])
         self.e_clip = _f(cfg["e_clip"])
@@ -620,11 +623,11 @@ class A2CAgent:
         t0 = time.perf_counter()
         if not self.is_learner:        # a policy replica: wait for the learner's weights
             self._broadcast_weights()
-            self.frame += self.batch_size
+            self.frame += self.frames_per_epoch
             st = {"epoch": self.epoch_num, "frames": self.frame, "play_time": play_time,
                   "update_time": time.perf_counter() - t0,
-                  "fps_step_inference": self.batch_size / play_time,
-                  "fps_total": self.batch_size / (play_time + time.perf_counter() - t0),
+                  "fps_step_inference": self.frames_per_epoch / play_time,
+                  "fps_total": self.frames_per_epoch / (play_time + time.perf_counter() - t0),
                   "mean_rewards": self.game_rewards.get_mean(),
                   "mean_lengths": self.game_lengths.get_mean(), "games": self.game_rewards.current_size}
             self.stats = st
@@ -684,12 +687,12 @@ class A2CAgent:
         if self.central:
             self._broadcast_weights()
         update_time = time.perf_counter() - t0
-        self.frame += self.batch_size
+        self.frame += self.frames_per_epoch
         st = {
             "epoch": self.epoch_num, "frames": self.frame, "play_time": play_time,
             "update_time": update_time,
-            "fps_step_inference": self.batch_size / play_time,
-            "fps_total": self.batch_size / (play_time + update_time),
+            "fps_step_inference": self.frames_per_epoch / play_time,
+            "fps_total": self.frames_per_epoch / (play_time + update_time),
             "a_loss": a_loss_m, "c_loss": c_loss_m, "b_loss": b_loss_m, "entropy": ent_m,
             "kl": kl_m, "lr": self.last_lr,
             "mean_rewards": self.game_rewards.get_mean(), "mean_lengths": self.game_lengths.get_mean(),

@@ -29,6 +29,16 @@ class RLKernelsUnavailable(RuntimeError):
     pass
 
 
+MI_RL_MAX_HIDDEN = 4
+
+
+class MiRlMlp(C.Structure):
+    """include/mi_rl.h mi_rl_mlp."""
+    _fields_ = [("num_obs", C.c_int32), ("num_actions", C.c_int32), ("num_hidden", C.c_int32),
+                ("units", C.c_int32 * MI_RL_MAX_HIDDEN),
+                ("w", C.c_void_p * (MI_RL_MAX_HIDDEN + 2)), ("b", C.c_void_p * (MI_RL_MAX_HIDDEN + 2))]
+
+
 def load_library() -> C.CDLL:
     """Load libmi_rl.so and declare every prototype of include/mi_rl.h (no GPU needed)."""
     global _LIB
@@ -49,6 +59,13 @@ def load_library() -> C.CDLL:
         lib.mi_rl_sample_gauss.argtypes = [vp, vp, i32, i32, i32, u64, vp, u64, vp, vp, vp]
         lib.mi_rl_ppo_loss.restype = i32
         lib.mi_rl_ppo_loss.argtypes = [vp, i32, vp, vp, i32] + [vp] * 7 + [i32, i32, f, i32, f, f, f] + [vp] * 8
+        lib.mi_rl_mlp_packed_size.restype = C.c_int64
+        lib.mi_rl_mlp_packed_size.argtypes = [C.POINTER(MiRlMlp)]
+        lib.mi_rl_mlp_pack.restype = i32
+        lib.mi_rl_mlp_pack.argtypes = [C.POINTER(MiRlMlp), vp, vp]
+        lib.mi_rl_policy_step.restype = i32
+        lib.mi_rl_policy_step.argtypes = ([C.POINTER(MiRlMlp), vp, vp, i32, vp, vp, vp, vp, f, vp, u64, vp, u64]
+                                          + [vp] * 7)
         _LIB = lib
     return _LIB
 
@@ -188,3 +205,70 @@ def ppo_loss(mu: torch.Tensor, logstd: torch.Tensor, value: torch.Tensor, mb: di
         g_mu.data_ptr(), g_val.data_ptr(), part_ls.data_ptr(), part_sums.data_ptr(),
         mb["mu"].data_ptr(), mb["sigma"].data_ptr(), _stream(mu)), "mi_rl_ppo_loss")
     return g_mu, g_val, part_ls.sum(0), part_sums.sum(0) * (1.0 / B)
+
+
+# ------------------------------------------------------------------------------ rollout policy
+class FusedPolicy:
+    """The rollout's policy evaluation as ONE launch (mi_rl_policy_step): running-mean-std obs
+    normalisation, the ELU MLP trunk, mu / value heads on the f32 MFMA, value un-normalisation
+    and the Gaussian sample (mi_rl_sample_gauss's draws). ``model`` is a
+    ModelA2CContinuousLogStd with fixed sigma and ELU; its weights are repacked into a padded
+    copy by :meth:`pack` (call after every weight update; capturable)."""
+
+    def __init__(self, model):
+        net = model.a2c_network
+        lin = [m for m in net.actor_mlp if isinstance(m, torch.nn.Linear)]
+        acts = [m for m in net.actor_mlp if not isinstance(m, torch.nn.Linear)]
+        if not net.fixed_sigma or not all(isinstance(a, torch.nn.ELU) for a in acts):
+            raise ValueError("FusedPolicy: fixed-sigma ELU networks only")
+        if not 1 <= len(lin) <= MI_RL_MAX_HIDDEN:
+            raise ValueError(f"FusedPolicy: {len(lin)} hidden layers (1..{MI_RL_MAX_HIDDEN})")
+        self.model = model
+        d = MiRlMlp()
+        d.num_obs, d.num_actions, d.num_hidden = lin[0].in_features, net.mu.out_features, len(lin)
+        layers = lin + [net.mu, net.value]
+        for i, m in enumerate(lin):
+            d.units[i] = m.out_features
+        for i, m in enumerate(layers):
+            if m.weight.dtype != torch.float32 or not m.weight.is_contiguous() or not m.bias.is_contiguous():
+                raise ValueError("FusedPolicy: contiguous f32 weights expected")
+            d.w[i], d.b[i] = m.weight.data_ptr(), m.bias.data_ptr()
+        self.desc = d
+        self._params = layers                  # keep the weights the descriptor points at alive
+        n = kernels().mi_rl_mlp_packed_size(C.byref(d))
+        if n < 0:
+            raise ValueError(f"FusedPolicy: {load_library().mi_rl_last_error().decode()}")
+        dev = lin[0].weight.device
+        self.packed = torch.zeros((int(n),), device=dev, dtype=torch.float32)
+
+    def pack(self) -> None:
+        _check(kernels().mi_rl_mlp_pack(C.byref(self.desc), self.packed.data_ptr(), _stream(self.packed)),
+               "mi_rl_mlp_pack")
+
+    def step(self, obs: torch.Tensor, seed: int = 0, counter_base: Optional[torch.Tensor] = None,
+             counter_offset: int = 0, obs_out=None, actions=None, neglogp=None, values=None,
+             mu=None, sigma=None) -> None:
+        """Writes the given outputs ([R, O] / [R, A] / [R] f32, contiguous)."""
+        m = self.model
+        R = obs.shape[0]
+        if obs.dtype != torch.float32 or not obs.is_contiguous() or obs.shape[1] != self.desc.num_obs:
+            raise ValueError(f"FusedPolicy.step: obs {tuple(obs.shape)} {obs.dtype}")
+        for t, w in ((obs_out, self.desc.num_obs), (actions, self.desc.num_actions), (neglogp, 1),
+                     (values, 1), (mu, self.desc.num_actions), (sigma, self.desc.num_actions)):
+            if t is not None and (t.dtype != torch.float32 or not t.is_contiguous() or t.numel() != R * w
+                                  or t.device != obs.device):
+                raise ValueError("FusedPolicy.step: outputs must be contiguous f32 of the obs rows")
+        om = ov = vm = vv = None
+        if m.normalize_input:
+            om, ov = m.running_mean_std.running_mean, m.running_mean_std.running_var
+        if m.normalize_value:
+            vm, vv = m.value_mean_std.running_mean, m.value_mean_std.running_var
+        eps = m.running_mean_std.epsilon if m.normalize_input else 1e-5
+        if counter_base is not None and (counter_base.dtype != torch.int64 or counter_base.device != obs.device):
+            raise ValueError("FusedPolicy.step: counter_base must be an int64 tensor on the obs device")
+        ls = m.a2c_network.sigma
+        _check(kernels().mi_rl_policy_step(
+            C.byref(self.desc), self.packed.data_ptr(), obs.data_ptr(), R, _ptr(om), _ptr(ov), _ptr(vm),
+            _ptr(vv), float(eps), ls.data_ptr(), int(seed) & ((1 << 64) - 1), _ptr(counter_base),
+            int(counter_offset), _ptr(obs_out), _ptr(actions), _ptr(neglogp), _ptr(values), _ptr(mu),
+            _ptr(sigma), _stream(obs)), "mi_rl_policy_step")

@@ -164,7 +164,7 @@ def test_two_rank_data_parallel_learner():
         assert res["batch"] == 16 * N_ENVS                 # per-rank batch (rl_games multi_gpu)
         assert res["minibatches"] == 4                     # as a single rank
         assert all(res["equal_after_epoch"])                # identical replicas after every update
-        assert res["frames"] == EPOCHS * res["batch"]
+        assert res["frames"] == EPOCHS * res["batch"] * 2       # whole-job frames (both shards)
         assert res["grad_err"] <= 1e-5 * max(1.0, res["grad_mag"]), (res["grad_err"], res["grad_mag"])
     assert out[0]["lrs"] == out[1]["lrs"]                  # one adaptive LR (averaged KL)
     assert out[0]["games"] == out[1]["games"]              # episode statistics all-reduced

@@ -272,4 +272,50 @@ def test_state_mirrors_track_every_state_write(gpu, name, n, pair, path, monkeyp
         copy = q2.clone()
     side.synchronize()
     assert q2 is q and np.array_equal(copy.cpu().numpy(), _direct(view)["q"])
+    # read on a side stream, then a step on the default stream that rewrites the mirrors: the
+    # write waits for the side stream's queued copy (delayed here so an unordered write would
+    # land first), so the copy holds the pre-step state
+    before = _direct(view)["q"]
+    with torch.cuda.stream(side):
+        q3 = view.get_joint_positions(clone=False)
+        torch.cuda._sleep(20_000_000)
+        late = q3.clone()
+    env._world.step()
+    env._world.step()
+    view.get_joint_positions(clone=False)                # issues the physics (+ mirror) launch
+    torch.cuda.synchronize()
+    assert np.array_equal(late.cpu().numpy(), before)
+    same()
+    env.close()
+
+
+@pytest.mark.parametrize("name", ["Humanoid", "Ant"])
+def test_state_mirrors_after_captured_steps(gpu, name):
+    """Steps captured in a HIP graph (the physics launch and a getter's refresh inside the
+    capture): after each replay the getters' mirrors equal the per-call gathers — events are not
+    recorded during capture, so a getter outside it refreshes on its own stream."""
+    env = make_env(name, num_envs=256, device="cuda:0", seed=21)
+    env.reset()
+    view = env.task.get_robot()
+    env.use_fused(False)
+    acts = (torch.rand((256, env.num_actions), generator=torch.Generator().manual_seed(3)) * 2 - 1).cuda()
+    env.step(acts)                                      # warm the method-by-method path
+    torch.cuda.synchronize()
+    g = torch.cuda.CUDAGraph()
+    s = torch.cuda.Stream()
+    s.wait_stream(torch.cuda.current_stream())
+    with torch.cuda.stream(s):
+        with torch.cuda.graph(g, stream=s):
+            view.set_joint_efforts(acts * 2.0)
+            env._world.step()
+            env._world.step()
+            inside = view.get_joint_positions(clone=True)
+    torch.cuda.current_stream().wait_stream(s)
+    for _ in range(3):
+        g.replay()
+        torch.cuda.synchronize()
+        a, b = _mirrored(view), _direct(view)
+        for k in a:
+            assert np.array_equal(a[k], b[k]), k
+        assert np.array_equal(inside.cpu().numpy(), b["q"])
     env.close()

@@ -114,6 +114,28 @@ def test_library_exports_every_header_symbol():
     assert lib.mi_abi_version() == 3
 
 
+def test_rl_library_exports_every_header_symbol():
+    """libmi_rl.so exports every entry point include/mi_rl.h declares, and its MLP descriptor
+    checks run on the host (no GPU)."""
+    from omniisaacgymenvs_amd.rlg import ops
+    txt = open(os.path.join(ROOT, "include", "mi_rl.h")).read()
+    syms = sorted(set(re.findall(r"^\s*(?:int32_t|int64_t|const char\*)\s+(mi_rl_\w+)\s*\(", txt, flags=re.M)))
+    assert len(syms) >= 8
+    lib = ops.load_library()
+    for s in syms:
+        assert hasattr(lib, s), s
+    d = ops.MiRlMlp()
+    d.num_obs, d.num_actions, d.num_hidden = 87, 21, 3
+    d.units[0], d.units[1], d.units[2] = 400, 200, 100
+    # padded [N16][K16] + bias per layer: 400x96, 208x400, 112x208, head 32x112
+    want = 400 * 96 + 400 + 208 * 400 + 208 + 112 * 208 + 112 + 32 * 112 + 32
+    assert lib.mi_rl_mlp_packed_size(C.byref(d)) == want
+    d.num_hidden = 0
+    assert lib.mi_rl_mlp_packed_size(C.byref(d)) == -1
+    d.num_hidden, d.units[0] = 3, 600                       # wider than the kernel's 512
+    assert lib.mi_rl_mlp_packed_size(C.byref(d)) == -1
+
+
 def test_abi_rejects_bad_input_without_touching_a_gpu():
     lib = N.load_library()
     out = C.c_void_p()
