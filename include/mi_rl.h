@@ -13,7 +13,8 @@
  *   mi_rl_ppo_loss     — rl_games algos_torch/a2c_continuous.py calc_gradients: the PPO loss
  *                        terms, the policy KL and the loss gradient w.r.t. the network heads
  *   mi_rl_policy_step  — the rollout's whole policy evaluation (normalisation, MLP, heads,
- *                        sampling) as one f32-MFMA launch
+ *                        sampling, action rescale) as one f32-MFMA launch
+ *   mi_rl_record_step  — the rollout's per-step bookkeeping after env.step
  * The training minibatch GEMMs stay in hipBLASLt (torch.nn.Linear, autograd).
  *
  * Conventions: as mi_sim.h — 0 on success or a negative MI_E_* code (mi_rl_last_error());
@@ -106,13 +107,31 @@ int32_t mi_rl_mlp_pack(const mi_rl_mlp* mlp, float* packed, void* stream);
  * statistics) are given; mu, v = heads(MLP(x)); values[n] = sqrt(var_v + eps) clamp(v, +-5) +
  * mean_v when value_mean / value_var are given, else v; sigma = exp(logstd) ([A], fixed sigma);
  * actions / neglogp exactly as mi_rl_sample_gauss(mu, logstd, 0, ..., seed, counter_base,
- * counter_offset); mu_out / sigma_out [R][A]. Any output may be NULL (neglogp needs actions). */
+ * counter_offset); mu_out / sigma_out [R][A]; env_actions [R][A] = rl_games preprocess_actions
+ * (clamp to +-1, rescale to [action_low, action_high], [A] each). Any output may be NULL
+ * (neglogp and env_actions need actions). */
 int32_t mi_rl_policy_step(const mi_rl_mlp* mlp, const float* packed, const float* obs,
                           int32_t num_rows, const double* obs_mean, const double* obs_var,
                           const double* value_mean, const double* value_var, float eps,
                           const float* logstd, uint64_t seed, const int64_t* counter_base,
                           uint64_t counter_offset, float* obs_out, float* actions, float* neglogp,
-                          float* values, float* mu_out, float* sigma_out, void* stream);
+                          float* values, float* mu_out, float* sigma_out, const float* action_low,
+                          const float* action_high, float* env_actions, void* stream);
+
+/* The rollout's bookkeeping after env.step (rl_games a2c_common play_steps), one launch:
+ *   rewards_out[n] = rewards[n] * reward_scale      (the experience buffer row; reward_shaper)
+ *   obs_state[n]   = obs_in[n]  ([N][O]),  dones_state[n] = (float) dones[n]
+ *   cur_rewards[n] += rewards[n]; cur_lengths[n] += 1
+ *   episode_sums[0..2] = sum_n d, sum_n d * cur_rewards, sum_n d * cur_lengths  (f64; the
+ *                        finished episodes' count, reward and length sums of this step)
+ *   cur_rewards[n] *= 1 - d; cur_lengths[n] *= 1 - d
+ * scratch: f64 [ceil(N / 256)][3]; ticket: a device uint32 that is 0 before the first call
+ * (the launch leaves it 0 again, so the call can be captured in a graph and replayed). */
+int32_t mi_rl_record_step(const float* obs_in, int32_t num_obs, const float* rewards,
+                          const int64_t* dones, int32_t num_envs, float reward_scale,
+                          float* obs_state, float* rewards_out, float* dones_state,
+                          float* cur_rewards, float* cur_lengths, double* episode_sums,
+                          double* scratch, uint32_t* ticket, void* stream);
 
 #ifdef __cplusplus
 }

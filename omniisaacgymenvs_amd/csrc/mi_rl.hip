@@ -229,9 +229,13 @@ __global__ __launch_bounds__(256) void k_ppo_loss(
 // ---------------------------------------------------------------------------------------
 namespace {
 constexpr int kPolRows = 16;      // rows per workgroup (one MFMA row tile)
-constexpr int kPolWaves = 4;
+#ifndef MI_POL_WAVES
+#define MI_POL_WAVES 8
+#endif
+constexpr int kPolWaves = MI_POL_WAVES;   // waves per workgroup (column tiles dealt round-robin)
 constexpr int kPolTiles = 8;      // max 16-column tiles per wave per layer (N_pad <= 512)
 constexpr int kPolMaxLayers = MI_RL_MAX_HIDDEN + 1;
+constexpr int kPolMaxWidth = 16 * kPolWaves * kPolTiles < 512 ? 16 * kPolWaves * kPolTiles : 512;
 
 struct PolLayer {
     int K, N, Kp, Np;             // true and padded (multiple of 16) input / output widths
@@ -258,8 +262,8 @@ int pol_desc(const mi_rl_mlp* m, PolDesc* d) {
     int in = m->num_obs, mx = pad16(m->num_obs);
     for (int l = 0; l < d->L; ++l) {
         const int out = l < m->num_hidden ? m->units[l] : m->num_actions + 1;   // head: mu | value
-        if (out <= 0 || pad16(out) > 16 * kPolWaves * kPolTiles)
-            return fail(kShape, "mi_rl: layer %d width %d (max %d)", l, out, 16 * kPolWaves * kPolTiles);
+        if (out <= 0 || pad16(out) > kPolMaxWidth)
+            return fail(kShape, "mi_rl: layer %d width %d (max %d)", l, out, kPolMaxWidth);
         PolLayer& y = d->ly[l];
         y.K = in; y.N = out; y.Kp = pad16(in); y.Np = pad16(out);
         y.w = off; off += (long long)y.Np * y.Kp;
@@ -301,65 +305,106 @@ __global__ void k_pol_pack(PolDesc d, mi_rl_mlp m, float* __restrict__ packed) {
 
 typedef float pf4 __attribute__((ext_vector_type(4)));
 
-// one layer for the workgroup's 16 rows: Y[16][Np] = act(X[16][Kp] W^T + b), X / Y in LDS
-__device__ __forceinline__ void pol_layer(const PolLayer& y, const float* __restrict__ packed,
+constexpr int kPolDepth = 3;      // weight chunks in flight per tile (L2 latency vs MFMA time)
+
+// T column tiles of one layer for this wave (tiles wave, wave + 4, ...), K-chunk loop with the
+// weight float4s of the next kPolDepth chunks in flight; T is a template constant so every
+// accumulator and ring slot is a fixed register (a runtime tile count with per-tile predicates
+// made the compiler shuffle the whole accumulator array around each MFMA)
+template <int T>
+__device__ __forceinline__ void pol_tiles(const PolLayer& y, const float* __restrict__ packed,
                                           const float* X, float* Y, int xs, bool elu, int wave,
                                           int lane) {
     const int r = lane & 15, j = lane >> 4;
-    const int nt = y.Np >> 4;                     // column tiles
-    const int mine = (nt - wave + kPolWaves - 1) / kPolWaves;   // this wave's tiles: wave, +4, ..
-    const float* W = packed + y.w;
-    pf4 acc[kPolTiles];
-    pf4 wb[kPolTiles], wn[kPolTiles];
+    const int Kp = y.Kp, nc = Kp >> 4;
+    const float* W = packed + y.w + (size_t)(16 * wave + r) * Kp + 4 * j;
+    const size_t tstride = (size_t)16 * kPolWaves * Kp;          // next tile of this wave
+    const float* xp = X + r * xs + 4 * j;
+    pf4 acc[T];
+    pf4 ring[kPolDepth][T];
 #pragma unroll
-    for (int t = 0; t < kPolTiles; ++t) acc[t] = pf4{0.0f, 0.0f, 0.0f, 0.0f};
-    const int nc = y.Kp >> 4;
-    // this lane's weight row of tile t: n = 16 (wave + 4 t) + r, chunk c at k = 16 c + 4 j
-    auto wld = [&](int t, int c) {
-        return *(const pf4*)(W + (size_t)(16 * (wave + kPolWaves * t) + r) * y.Kp + 16 * c + 4 * j);
-    };
+    for (int t = 0; t < T; ++t) acc[t] = pf4{0.0f, 0.0f, 0.0f, 0.0f};
 #pragma unroll
-    for (int t = 0; t < kPolTiles; ++t)
-        if (t < mine) wb[t] = wld(t, 0);
-    for (int c = 0; c < nc; ++c) {
-        const pf4 a = *(const pf4*)(X + r * xs + 16 * c + 4 * j);
-        const bool more = c + 1 < nc;
+    for (int p = 0; p < kPolDepth; ++p) {
+        const int c = p < nc ? p : nc - 1;
 #pragma unroll
-        for (int t = 0; t < kPolTiles; ++t)
-            if (t < mine && more) wn[t] = wld(t, c + 1);
+        for (int t = 0; t < T; ++t) ring[p][t] = *(const pf4*)(W + t * tstride + 16 * c);
+    }
+    // whole groups of kPolDepth chunks: no branch inside, so the waits before each chunk's
+    // MFMAs count only that chunk's loads (the later chunks' stay in flight)
+    pf4 a = *(const pf4*)xp;
+    int c0 = 0;
+    for (; c0 + kPolDepth <= nc; c0 += kPolDepth) {
 #pragma unroll
-        for (int s = 0; s < 4; ++s) {
+        for (int p = 0; p < kPolDepth; ++p) {
+            const int c = c0 + p;
+            const pf4 an = *(const pf4*)(xp + 16 * (c + 1 < nc ? c + 1 : c));   // next chunk's A
 #pragma unroll
-            for (int t = 0; t < kPolTiles; ++t)
-                if (t < mine) acc[t] = __builtin_amdgcn_mfma_f32_16x16x4f32(a[s], wb[t][s], acc[t], 0, 0, 0);
+            for (int s = 0; s < 4; ++s) {
+#pragma unroll
+                for (int t = 0; t < T; ++t)
+                    acc[t] = __builtin_amdgcn_mfma_f32_16x16x4f32(a[s], ring[p][t][s], acc[t], 0, 0, 0);
+            }
+            const int cn = c + kPolDepth < nc ? c + kPolDepth : nc - 1;
+#pragma unroll
+            for (int t = 0; t < T; ++t) ring[p][t] = *(const pf4*)(W + t * tstride + 16 * cn);
+            a = an;
         }
+    }
+    // the last nc % kPolDepth chunks: ring slot p holds chunk c0 + p
 #pragma unroll
-        for (int t = 0; t < kPolTiles; ++t)
-            if (t < mine && more) wb[t] = wn[t];
+    for (int p = 0; p < kPolDepth - 1; ++p) {
+        if (c0 + p < nc) {
+            const pf4 ap = *(const pf4*)(xp + 16 * (c0 + p));
+#pragma unroll
+            for (int s = 0; s < 4; ++s) {
+#pragma unroll
+                for (int t = 0; t < T; ++t)
+                    acc[t] = __builtin_amdgcn_mfma_f32_16x16x4f32(ap[s], ring[p][t][s], acc[t], 0, 0, 0);
+            }
+        }
     }
     const float* B = packed + y.b;
 #pragma unroll
-    for (int t = 0; t < kPolTiles; ++t) {
-        if (t < mine) {
-            const int col = 16 * (wave + kPolWaves * t) + r;
-            const float bias = B[col];
+    for (int t = 0; t < T; ++t) {
+        const int col = 16 * (wave + kPolWaves * t) + r;
+        const float bias = B[col];
 #pragma unroll
-            for (int i = 0; i < 4; ++i) {
-                float v = acc[t][i] + bias;
-                if (elu) v = v > 0.0f ? v : expm1f(v);
-                Y[(4 * j + i) * xs + col] = v;
-            }
+        for (int i = 0; i < 4; ++i) {
+            float v = acc[t][i] + bias;
+            if (elu) v = v > 0.0f ? v : expm1f(v);
+            Y[(4 * j + i) * xs + col] = v;
         }
     }
 }
 
-__global__ __launch_bounds__(kPolRows * 16) void k_policy_step(
+// one layer for the workgroup's 16 rows: Y[16][Np] = act(X[16][Kp] W^T + b), X / Y in LDS
+__device__ __forceinline__ void pol_layer(const PolLayer& y, const float* __restrict__ packed,
+                                          const float* X, float* Y, int xs, bool elu, int wave,
+                                          int lane) {
+    const int nt = y.Np >> 4;
+    const int mine = __builtin_amdgcn_readfirstlane((nt - wave + kPolWaves - 1) / kPolWaves);
+    switch (mine) {
+        case 1: pol_tiles<1>(y, packed, X, Y, xs, elu, wave, lane); break;
+        case 2: pol_tiles<2>(y, packed, X, Y, xs, elu, wave, lane); break;
+        case 3: pol_tiles<3>(y, packed, X, Y, xs, elu, wave, lane); break;
+        case 4: pol_tiles<4>(y, packed, X, Y, xs, elu, wave, lane); break;
+        case 5: pol_tiles<5>(y, packed, X, Y, xs, elu, wave, lane); break;
+        case 6: pol_tiles<6>(y, packed, X, Y, xs, elu, wave, lane); break;
+        case 7: pol_tiles<7>(y, packed, X, Y, xs, elu, wave, lane); break;
+        case 8: pol_tiles<8>(y, packed, X, Y, xs, elu, wave, lane); break;
+        default: break;                           // 0: this wave has no tile in this layer
+    }
+}
+
+__global__ __launch_bounds__(64 * kPolWaves) void k_policy_step(
     PolDesc d, const float* __restrict__ packed, const float* __restrict__ obs, int R,
     const double* __restrict__ om, const double* __restrict__ ov, const double* __restrict__ vm,
     const double* __restrict__ vv, float eps, const float* __restrict__ logstd, uint64_t seed,
     const int64_t* __restrict__ cbase, uint64_t coff, float* __restrict__ obs_out,
     float* __restrict__ act, float* __restrict__ nlp, float* __restrict__ val,
-    float* __restrict__ mu_out, float* __restrict__ sg_out) {
+    float* __restrict__ mu_out, float* __restrict__ sg_out, const float* __restrict__ alo,
+    const float* __restrict__ ahi, float* __restrict__ env_act) {
 #pragma clang fp contract(off)
     extern __shared__ float pl[];                 // two [16][xs] activation tiles + noise [16][64]
     float* X0 = pl;
@@ -417,7 +462,14 @@ __global__ __launch_bounds__(kPolRows * 16) void k_policy_step(
         const float sg = expf(logstd[jj]);
         if (mu_out) mu_out[(size_t)n * A + jj] = m;
         if (sg_out) sg_out[(size_t)n * A + jj] = sg;
-        if (act) act[(size_t)n * A + jj] = m + sg * Z[rr * 64 + jj];
+        if (act) {
+            const float a = m + sg * Z[rr * 64 + jj];
+            act[(size_t)n * A + jj] = a;
+            if (env_act) {   // rl_games preprocess_actions: clamp to +-1, rescale to [low, high]
+                const float ac = fminf(fmaxf(a, -1.0f), 1.0f);
+                env_act[(size_t)n * A + jj] = alo[jj] + (ac + 1.0f) * 0.5f * (ahi[jj] - alo[jj]);
+            }
+        }
     }
     // per row: value (un-normalised: sqrt(var + eps) * clamp(v, +-5) + mean) and neglogp in
     // k_sample_gauss's order
@@ -444,6 +496,67 @@ __global__ __launch_bounds__(kPolRows * 16) void k_policy_step(
                 nlp[n] = 0.5f * sq + 0.918938533204672742f * (float)A + lsum;
             }
         }
+    }
+}
+}  // namespace
+
+// ---------------------------------------------------------------------------------------
+// Rollout bookkeeping after env.step (rl_games a2c_common play_steps): shaped rewards into the
+// experience buffer, the next obs / dones, the running episode reward / length meters and the
+// per-step sums of finished episodes — ~20 small torch kernels per step, here one launch.
+// The episode sums reduce deterministically: per-block partials in fixed order, the last block
+// to finish (ticket counter, reset by that block for the next launch / graph replay) adds them
+// in block order.
+// ---------------------------------------------------------------------------------------
+namespace {
+constexpr int kRecBlock = 256;
+
+__global__ __launch_bounds__(kRecBlock) void k_record_step(
+    const float* __restrict__ obs_in, int O, const float* __restrict__ rew_in,
+    const int64_t* __restrict__ done_in, int N, float scale, float* __restrict__ obs_state,
+    float* __restrict__ rew_out, float* __restrict__ done_state, float* __restrict__ cur_rew,
+    float* __restrict__ cur_len, double* __restrict__ sums, double* __restrict__ partial,
+    unsigned* __restrict__ ticket) {
+#pragma clang fp contract(off)
+    __shared__ double red[3][kRecBlock];
+    __shared__ bool last;
+    const int tid = threadIdx.x, n = blockIdx.x * kRecBlock + tid;
+    // obs rows of this block's envs (coalesced float copy over the block's [kRecBlock][O] span)
+    const size_t o0 = (size_t)blockIdx.x * kRecBlock * O;
+    const size_t o1 = (size_t)(n - tid + kRecBlock < N ? n - tid + kRecBlock : N) * O;
+    for (size_t e = o0 + tid; e < o1; e += kRecBlock) obs_state[e] = obs_in[e];
+    double c = 0.0, rs = 0.0, ls = 0.0;
+    if (n < N) {
+        const float r = rew_in[n];
+        rew_out[n] = r * scale;
+        const float d = (float)done_in[n];
+        done_state[n] = d;
+        const float cr = cur_rew[n] + r, cl = cur_len[n] + 1.0f;
+        c = (double)d;
+        rs = (double)cr * (double)d;
+        ls = (double)cl * (double)d;
+        cur_rew[n] = cr * (1.0f - d);
+        cur_len[n] = cl * (1.0f - d);
+    }
+    red[0][tid] = c; red[1][tid] = rs; red[2][tid] = ls;
+    __syncthreads();
+    for (int w = kRecBlock / 2; w > 0; w >>= 1) {
+        if (tid < w)
+            for (int k = 0; k < 3; ++k) red[k][tid] += red[k][tid + w];
+        __syncthreads();
+    }
+    if (tid == 0) {
+        for (int k = 0; k < 3; ++k) partial[(size_t)blockIdx.x * 3 + k] = red[k][0];
+        __threadfence();
+        last = atomicAdd(ticket, 1u) == gridDim.x - 1;
+    }
+    __syncthreads();
+    if (last && tid < 3) {
+        __threadfence();
+        double t = 0.0;
+        for (unsigned b = 0; b < gridDim.x; ++b) t += ((volatile double*)partial)[(size_t)b * 3 + tid];
+        sums[tid] = t;
+        if (tid == 0) *ticket = 0u;
     }
 }
 }  // namespace
@@ -541,20 +654,39 @@ int32_t mi_rl_policy_step(const mi_rl_mlp* mlp, const float* packed, const float
                           const double* value_mean, const double* value_var, float eps,
                           const float* logstd, uint64_t seed, const int64_t* counter_base,
                           uint64_t counter_offset, float* obs_out, float* actions, float* neglogp,
-                          float* values, float* mu_out, float* sigma_out, void* stream) {
+                          float* values, float* mu_out, float* sigma_out, const float* action_low,
+                          const float* action_high, float* env_actions, void* stream) {
     PolDesc d;
     if (int rc = pol_desc(mlp, &d)) return rc;
     if (!packed || !obs || !logstd) return fail(kNull, "mi_rl_policy_step: null packed / obs / logstd");
     if ((obs_mean == nullptr) != (obs_var == nullptr) || (value_mean == nullptr) != (value_var == nullptr))
         return fail(kNull, "mi_rl_policy_step: mean and var come in pairs");
     if (num_rows <= 0) return fail(kShape, "mi_rl_policy_step: R=%d", num_rows);
-    if (neglogp && !actions) return fail(kNull, "mi_rl_policy_step: neglogp needs actions");
+    if ((neglogp || env_actions) && !actions) return fail(kNull, "mi_rl_policy_step: neglogp / env_actions need actions");
+    if (env_actions && (!action_low || !action_high)) return fail(kNull, "mi_rl_policy_step: env_actions need the action bounds");
     const size_t lds = sizeof(float) * ((size_t)2 * kPolRows * d.xs + (size_t)kPolRows * 64);
-    hipLaunchKernelGGL(k_policy_step, dim3((num_rows + kPolRows - 1) / kPolRows), dim3(kPolRows * 16),
+    hipLaunchKernelGGL(k_policy_step, dim3((num_rows + kPolRows - 1) / kPolRows), dim3(64 * kPolWaves),
                        lds, (hipStream_t)stream, d, packed, obs, num_rows, obs_mean, obs_var,
                        value_mean, value_var, eps, logstd, seed, counter_base, counter_offset,
-                       obs_out, actions, neglogp, values, mu_out, sigma_out);
+                       obs_out, actions, neglogp, values, mu_out, sigma_out, action_low, action_high,
+                       env_actions);
     return launch_check("mi_rl_policy_step");
+}
+
+int32_t mi_rl_record_step(const float* obs_in, int32_t num_obs, const float* rewards,
+                          const int64_t* dones, int32_t num_envs, float reward_scale,
+                          float* obs_state, float* rewards_out, float* dones_state,
+                          float* cur_rewards, float* cur_lengths, double* episode_sums,
+                          double* scratch, uint32_t* ticket, void* stream) {
+    if (!obs_in || !rewards || !dones || !obs_state || !rewards_out || !dones_state || !cur_rewards ||
+        !cur_lengths || !episode_sums || !scratch || !ticket)
+        return fail(kNull, "mi_rl_record_step: null buffer");
+    if (num_envs <= 0 || num_obs <= 0) return fail(kShape, "mi_rl_record_step: N=%d O=%d", num_envs, num_obs);
+    hipLaunchKernelGGL(k_record_step, dim3((num_envs + kRecBlock - 1) / kRecBlock), dim3(kRecBlock), 0,
+                       (hipStream_t)stream, obs_in, num_obs, rewards, dones, num_envs, reward_scale,
+                       obs_state, rewards_out, dones_state, cur_rewards, cur_lengths, episode_sums,
+                       scratch, ticket);
+    return launch_check("mi_rl_record_step");
 }
 
 }  // extern "C"

@@ -232,6 +232,18 @@ class A2CAgent:
         # loss + head gradients as one HIP launch (mi_rl_ppo_loss); needs the fixed log-std head
         self.fused_loss = (self.device.type == "cuda" and bool(cfg.get("fused_loss", True))
                            and self.model.a2c_network.fixed_sigma)
+        # the rollout's policy evaluation (normalisation, MLP, heads, sampling) as ONE launch
+        # (mi_rl_policy_step, f32 MFMA) instead of the torch modules + sampling kernel
+        self.fused_policy = None
+        self._env_act = None
+        if self.device.type == "cuda" and bool(cfg.get("fused_policy", True)):
+            try:
+                self.fused_policy = ops.FusedPolicy(self.model)
+            except ValueError as e:        # a network the kernel does not cover: torch modules
+                print(f"[rlg] fused rollout policy off ({e})")
+        # the rollout's per-step bookkeeping after env.step as one launch (mi_rl_record_step)
+        self.recorder = (ops.RolloutRecorder(self.num_actors, self.device)
+                         if self.fused_policy is not None else None)
         # split-K weight gradients of the minibatch GEMMs (models.linear_train); 1 = one GEMM
         self.wgrad_splits = int(cfg.get("wgrad_splits", 32))
         # action-noise streams: one per rank (replicas must not share exploration noise)
@@ -354,19 +366,50 @@ class A2CAgent:
         values = self.model.unnorm_value(value.float()).squeeze(-1)
         return act, nlp, values, mu, torch.exp(logstd)
 
+    def _record_fused(self, obs, rewards, dones, infos) -> bool:
+        """The fused bookkeeping applies when the env hands back device f32 obs / rewards and
+        i64 dones and no time-out bootstrap is requested (the reference's tasks set none)."""
+        if self.recorder is None:
+            return False
+        if self.value_bootstrap and isinstance(infos, dict) and "time_outs" in infos:
+            return False
+        o = obs["obs"] if isinstance(obs, dict) else obs
+        return (o.device == self.device and o.dtype == torch.float32 and o.is_contiguous()
+                and rewards.device == self.device and rewards.dtype == torch.float32
+                and rewards.is_contiguous() and dones.device == self.device
+                and dones.dtype == torch.int64 and dones.is_contiguous())
+
     def _rollout_body(self) -> None:
         """horizon env steps; everything stays on the device (graph-capturable)."""
         b = self.buf
+        fp = self.fused_policy
+        if fp is not None:
+            fp.pack()                  # this epoch's weights (the graph replays the repack)
         for n in range(self.horizon):
-            act, nlp, values, mu, sigma = self._policy_step(self.obs, n)
-            b["obses"][n].copy_(self.obs)
             b["dones"][n].copy_(self.dones)
-            b["actions"][n].copy_(act)
-            b["neglogpacs"][n].copy_(nlp)
-            b["values"][n].copy_(values)
-            b["mus"][n].copy_(mu)
-            b["sigmas"][n].copy_(sigma)
-            obs, rewards, dones, infos = self.env.step(self.preprocess_actions(act))
+            if fp is not None:         # the policy writes its outputs straight into slot n
+                if self._env_act is None:
+                    self._env_act = torch.empty_like(b["actions"][n])
+                fp.step(self.obs, self.sample_seed, self.rng_counter, n, obs_out=b["obses"][n],
+                        actions=b["actions"][n], neglogp=b["neglogpacs"][n], values=b["values"][n],
+                        mu=b["mus"][n], sigma=b["sigmas"][n], env_actions=self._env_act,
+                        action_low=self.actions_low, action_high=self.actions_high)
+                values = b["values"][n]
+                obs, rewards, dones, infos = self.env.step(self._env_act)
+            else:
+                act, nlp, values, mu, sigma = self._policy_step(self.obs, n)
+                b["obses"][n].copy_(self.obs)
+                b["actions"][n].copy_(act)
+                b["neglogpacs"][n].copy_(nlp)
+                b["values"][n].copy_(values)
+                b["mus"][n].copy_(mu)
+                b["sigmas"][n].copy_(sigma)
+                obs, rewards, dones, infos = self.env.step(self.preprocess_actions(act))
+            if self._record_fused(obs, rewards, dones, infos):
+                self.recorder.step(self._obs_tensor(obs), rewards, dones, self.reward_scale, self.obs,
+                                   b["rewards"][n], self.dones, self.current_rewards,
+                                   self.current_lengths, self.episode_sums[n])
+                continue
             rewards = rewards.to(self.device, dtype=torch.float32).view(-1)
             shaped = rewards * self.reward_scale
             if self.value_bootstrap and isinstance(infos, dict) and "time_outs" in infos:
@@ -383,8 +426,11 @@ class A2CAgent:
             self.current_rewards.mul_(1.0 - d)
             self.current_lengths.mul_(1.0 - d)
         # bootstrap value of the state after the last step
-        _, _, value = self.model.policy(self.obs)
-        self.last_values.copy_(self.model.unnorm_value(value.float()).squeeze(-1))
+        if fp is not None:
+            fp.step(self.obs, values=self.last_values)
+        else:
+            _, _, value = self.model.policy(self.obs)
+            self.last_values.copy_(self.model.unnorm_value(value.float()).squeeze(-1))
         self.rng_counter.add_(self.horizon)
 
     def play_steps(self) -> float:

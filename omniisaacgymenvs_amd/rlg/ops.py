@@ -65,7 +65,9 @@ def load_library() -> C.CDLL:
         lib.mi_rl_mlp_pack.argtypes = [C.POINTER(MiRlMlp), vp, vp]
         lib.mi_rl_policy_step.restype = i32
         lib.mi_rl_policy_step.argtypes = ([C.POINTER(MiRlMlp), vp, vp, i32, vp, vp, vp, vp, f, vp, u64, vp, u64]
-                                          + [vp] * 7)
+                                          + [vp] * 10)
+        lib.mi_rl_record_step.restype = i32
+        lib.mi_rl_record_step.argtypes = [vp, i32, vp, vp, i32, f] + [vp] * 9
         _LIB = lib
     return _LIB
 
@@ -247,14 +249,21 @@ class FusedPolicy:
 
     def step(self, obs: torch.Tensor, seed: int = 0, counter_base: Optional[torch.Tensor] = None,
              counter_offset: int = 0, obs_out=None, actions=None, neglogp=None, values=None,
-             mu=None, sigma=None) -> None:
-        """Writes the given outputs ([R, O] / [R, A] / [R] f32, contiguous)."""
+             mu=None, sigma=None, env_actions=None, action_low=None, action_high=None) -> None:
+        """Writes the given outputs ([R, O] / [R, A] / [R] f32, contiguous). env_actions: the
+        actions clamped to +-1 and rescaled to [action_low, action_high] (rl_games
+        preprocess_actions)."""
         m = self.model
         R = obs.shape[0]
         if obs.dtype != torch.float32 or not obs.is_contiguous() or obs.shape[1] != self.desc.num_obs:
             raise ValueError(f"FusedPolicy.step: obs {tuple(obs.shape)} {obs.dtype}")
-        for t, w in ((obs_out, self.desc.num_obs), (actions, self.desc.num_actions), (neglogp, 1),
-                     (values, 1), (mu, self.desc.num_actions), (sigma, self.desc.num_actions)):
+        A = self.desc.num_actions
+        if env_actions is not None:
+            for t in (action_low, action_high):
+                if t is None or t.dtype != torch.float32 or not t.is_contiguous() or t.numel() != A:
+                    raise ValueError("FusedPolicy.step: env_actions need [A] f32 action bounds")
+        for t, w in ((obs_out, self.desc.num_obs), (actions, A), (neglogp, 1), (values, 1), (mu, A),
+                     (sigma, A), (env_actions, A)):
             if t is not None and (t.dtype != torch.float32 or not t.is_contiguous() or t.numel() != R * w
                                   or t.device != obs.device):
                 raise ValueError("FusedPolicy.step: outputs must be contiguous f32 of the obs rows")
@@ -271,4 +280,33 @@ class FusedPolicy:
             C.byref(self.desc), self.packed.data_ptr(), obs.data_ptr(), R, _ptr(om), _ptr(ov), _ptr(vm),
             _ptr(vv), float(eps), ls.data_ptr(), int(seed) & ((1 << 64) - 1), _ptr(counter_base),
             int(counter_offset), _ptr(obs_out), _ptr(actions), _ptr(neglogp), _ptr(values), _ptr(mu),
-            _ptr(sigma), _stream(obs)), "mi_rl_policy_step")
+            _ptr(sigma), _ptr(action_low), _ptr(action_high), _ptr(env_actions), _stream(obs)),
+            "mi_rl_policy_step")
+
+
+class RolloutRecorder:
+    """The rollout's bookkeeping after env.step in one launch (mi_rl_record_step): shaped rewards
+    into the experience buffer, next obs / dones, episode meters, the step's finished-episode
+    sums. Owns the reduction scratch and the ticket counter."""
+
+    def __init__(self, num_envs: int, device):
+        self.n = int(num_envs)
+        self.scratch = torch.zeros(((self.n + 255) // 256, 3), device=device, dtype=torch.float64)
+        self.ticket = torch.zeros((1,), device=device, dtype=torch.int32)
+
+    def step(self, obs_in, rewards, dones, reward_scale: float, obs_state, rewards_out, dones_state,
+             cur_rewards, cur_lengths, episode_sums) -> None:
+        N, O = obs_in.shape
+        if N != self.n or obs_state.shape != obs_in.shape:
+            raise ValueError("RolloutRecorder.step: obs shape")
+        for t, dt, k in ((obs_in, torch.float32, N * O), (rewards, torch.float32, N), (dones, torch.int64, N),
+                         (obs_state, torch.float32, N * O), (rewards_out, torch.float32, N),
+                         (dones_state, torch.float32, N), (cur_rewards, torch.float32, N),
+                         (cur_lengths, torch.float32, N), (episode_sums, torch.float64, 3)):
+            if t.dtype != dt or not t.is_contiguous() or t.numel() != k or t.device != obs_in.device:
+                raise ValueError(f"RolloutRecorder.step: {tuple(t.shape)} {t.dtype}, want {k} x {dt}")
+        _check(kernels().mi_rl_record_step(
+            obs_in.data_ptr(), O, rewards.data_ptr(), dones.data_ptr(), N, float(reward_scale),
+            obs_state.data_ptr(), rewards_out.data_ptr(), dones_state.data_ptr(), cur_rewards.data_ptr(),
+            cur_lengths.data_ptr(), episode_sums.data_ptr(), self.scratch.data_ptr(), self.ticket.data_ptr(),
+            _stream(obs_in)), "mi_rl_record_step")

@@ -220,3 +220,35 @@ def test_ppo_learns_ant_on_reference_schedule(gpu):
     assert ag.graph is not None and ag.upd_graphs
     assert st["mean_rewards"] >= 1000.0 and st["mean_rewards"] > 50.0 * max(first, 1.0), (first, st["mean_rewards"])
     env.close()
+
+
+def test_ppo_learns_humanoid_on_reference_schedule(gpu):
+    """HumanoidPPO.yaml as shipped (cfg/train/HumanoidPPO.yaml:59 max_epochs; 4096 envs, horizon
+    32, minibatch 32768, 5 mini-epochs, adaptive LR, fp16 update) through the learner — fused
+    rollout policy included — and the fused Humanoid step: after 150 epochs the mean episode
+    reward must be >= 600 and >= 8x the first finished episodes' (~55-62). The committed curve
+    (profiles/r04/train_curve_humanoid.jsonl, same seed) reads 62 at epoch 1, 401 at epoch 100,
+    818 at 125 and 2097 at 150; the bound leaves room for ~25 epochs of GEMM / box drift."""
+    from omniisaacgymenvs_amd.rlg.a2c_continuous import A2CAgent
+    from omniisaacgymenvs_amd.utils.rlgames.rlgames_utils import RLGPUEnv, register_env
+    from omniisaacgymenvs_amd.utils.task_util import make_env
+
+    env = make_env("Humanoid", device="cuda:0", seed=42)
+    register_env("rlgpu_humanoid_learn", lambda **kw: env)
+    params = env.task_cfg["train"]["params"]
+    params["config"]["save_frequency"] = 0
+    params["config"]["save_best_after"] = 10 ** 9
+    ag = A2CAgent(RLGPUEnv("rlgpu_humanoid_learn", env.num_envs), params, run_dir="/tmp/humanoid_learn")
+    assert ag.num_actors == 4096 and ag.minibatch_size == 32768 and ag.horizon == 32
+    assert ag.fused_policy is not None and ag.recorder is not None
+    ag.env_reset()
+    first = None
+    for ep in range(150):
+        st = ag.train_epoch()
+        assert math.isfinite(st["a_loss"]) and math.isfinite(st["c_loss"])
+        if first is None and st["games"] > 0:
+            first = st["mean_rewards"]
+    assert ag.graph is not None and ag.upd_graphs
+    print(f"humanoid: first {first:.1f}, epoch 150 {st['mean_rewards']:.1f}")
+    assert st["mean_rewards"] >= 600.0 and st["mean_rewards"] > 8.0 * max(first, 1.0), (first, st["mean_rewards"])
+    env.close()

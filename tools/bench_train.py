@@ -25,6 +25,8 @@ def main():
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--no-graph", action="store_true", help="eager rollout and eager updates")
     ap.add_argument("--no-graph-update", action="store_true", help="eager (sync-free) updates only")
+    ap.add_argument("--no-fused-policy", action="store_true",
+                    help="rollout policy as torch modules + sampling kernel (A/B of mi_rl_policy_step)")
     args = ap.parse_args()
     import torch
 
@@ -37,6 +39,7 @@ def main():
     params = env.task_cfg["train"]["params"]
     params["config"]["graph_rollout"] = not args.no_graph
     params["config"]["graph_update"] = not (args.no_graph or args.no_graph_update)
+    params["config"]["fused_policy"] = not args.no_fused_policy
     n = env.num_envs
     agent = A2CAgent(RLGPUEnv("rlgpu", n), params, run_dir=os.path.join("/tmp", "bench_train"))
     agent.env_reset()
@@ -58,7 +61,7 @@ def main():
         "task": args.task, "num_envs": n, "horizon": agent.horizon,
         "minibatch": agent.minibatch_size, "mini_epochs": agent.mini_epochs,
         "mixed_precision": agent.mixed_precision, "graph_rollout": agent.graph is not None,
-        "graph_update": len(agent.upd_graphs) > 0,
+        "graph_update": len(agent.upd_graphs) > 0, "fused_policy": agent.fused_policy is not None,
         "units": params["network"]["mlp"]["units"], "epochs": args.epochs,
         "fps_total": round(frames / wall, 1), "fps_step_inference": round(frames / play, 1),
         "ms_per_epoch": round(1e3 * wall / args.epochs, 3),
