@@ -53,6 +53,9 @@ def parse(argv=None):
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-side", action="store_true", help="skip the Cartpole / Ant side runs")
     ap.add_argument("--modular", action="store_true", help="method-by-method path, not fused")
+    ap.add_argument("--solver", choices=["config", "tgs", "pgs"], default="config",
+                    help="contact / limit solver: the task config's (cfg/config.yaml solver_type: 1 = "
+                         "TGS, the reference's default) or an override (A/B)")
     ap.add_argument("--events-apart", action="store_true",
                     help="diagnostic: time the window without kernel events, events in a second window")
     ap.add_argument("--fuse-envs", type=int, default=1048576,
@@ -312,13 +315,23 @@ def action_pool(view, n, A, seed, device, pool=16):
     return actions
 
 
-def side_run(task_name: str, n: int, steps: int = 200, warmup: int = 30) -> dict:
+def solver_overrides(solver: str) -> list:
+    return {"config": [], "tgs": ["solver_type=1"], "pgs": ["solver_type=0"]}[solver]
+
+
+def solver_label(view) -> str:
+    p = view.sim_params
+    return (f"TGS ({p.solver_iterations} position / {p.velocity_iterations} velocity iterations)"
+            if p.solver_type == 1 else f"PGS ({p.solver_iterations} sweeps)")
+
+
+def side_run(task_name: str, n: int, steps: int = 200, warmup: int = 30, solver: str = "config") -> dict:
     """BASELINE configs 2 and 3 (Cartpole / Ant at 4096 envs on 1 GPU): the same fused step,
     kernel time from HIP events on the launch stream, algorithmic HBM fraction."""
     import torch
     from omniisaacgymenvs_amd.utils.task_util import make_env
 
-    env = make_env(task_name, num_envs=n, device="cuda:0", seed=42)
+    env = make_env(task_name, num_envs=n, device="cuda:0", seed=42, overrides=solver_overrides(solver))
     task = env.task
     view = task.get_robot()
     actions = action_pool(view, n, task.num_actions, 42, "cuda:0")
@@ -353,6 +366,7 @@ def side_run(task_name: str, n: int, steps: int = 200, warmup: int = 30) -> dict
     torch.cuda.synchronize()
     el_g = time.perf_counter() - t0
     out = {"workload": f"{task_name} {n} envs, fused env step", "kernel": kernel_name(view, task),
+           "solver": solver_label(view),
            "value": round(n * steps / el, 1), "unit": "env-steps/s", "ms_per_step": round(el / steps * 1e3, 4),
            "kernel_ms": round(kms, 4), "achieved": round(ach, 3), "unit_bw": "GB/s",
            "frac": round(ach / HBM_PEAK_GBS, 6), "algo_bytes_per_env": ALGO_BYTES[task_name],
@@ -390,7 +404,8 @@ def main():
 
     n_local = args.num_envs
     env = make_env(args.task, num_envs=n_local, device=device, seed=args.seed,
-                   env_id_offset=rank * n_local, global_num_envs=world * n_local)
+                   env_id_offset=rank * n_local, global_num_envs=world * n_local,
+                   overrides=solver_overrides(args.solver))
     if args.modular:
         env.use_fused(False)
     task = env.task
@@ -503,6 +518,7 @@ def main():
                                    f"(controlFrequencyInv=2 substeps @ dt=0.0083)",
                        "task": args.task, "num_envs_per_gpu": n_local, "global_envs": world * n_local,
                        "substeps": task.control_frequency_inv, "path": "fused" if env.fused else "modular",
+                       "solver": solver_label(view),
                        "lds_bytes_per_env": view.sim_kernel_path()[2],
                        "parallelism": f"env-shard x{world}" + (
                            f" + async RCCL gather of the rollout slab to the learner rank every "
@@ -537,7 +553,8 @@ def main():
         dist.destroy_process_group()
     if rank == 0:
         if world == 1 and not args.no_side and args.task == "Humanoid":
-            out["side_configs"] = [side_run("Cartpole", 4096), side_run("Ant", 4096)]
+            out["side_configs"] = [side_run("Cartpole", 4096, solver=args.solver),
+                                   side_run("Ant", 4096, solver=args.solver)]
         if world == 1 and args.fuse_envs > 0 and args.task != "Cartpole":
             # north_star: achieved HBM GB/s of the obs/reward fuse (RLTask.post_physics_step as ONE
             # streaming kernel, the method-by-method path) where its working set streams from HBM

@@ -32,7 +32,7 @@
 extern "C" {
 #endif
 
-#define MI_ABI_VERSION 3
+#define MI_ABI_VERSION 4
 
 enum {
     MI_OK = 0,
@@ -104,7 +104,8 @@ typedef struct mi_model_desc {
 typedef struct mi_sim_params {
     float dt;                       /* sim.dt                                         */
     float gravity[3];               /* sim.gravity                                    */
-    int32_t solver_iterations;      /* physx.solver_position_iteration_count (+vel)   */
+    int32_t solver_iterations;      /* PGS: position + velocity iteration counts;     */
+                                    /* TGS: solver_position_iteration_count          */
     float contact_offset;           /* physx.contact_offset                           */
     float rest_offset;              /* physx.rest_offset                              */
     float friction;                 /* default_physics_material.dynamic_friction      */
@@ -114,7 +115,24 @@ typedef struct mi_sim_params {
     float max_angular_velocity;     /* rad/s, PhysX default 5729.58 deg/s             */
     float angular_damping;          /* 1/s, per-link angular velocity damping, PhysX  */
                                     /* default 0.05 (docs/transfering_policies_...:74) */
+    int32_t solver_type;            /* physx.solver_type (cfg/config.yaml:31): 0 PGS, */
+                                    /* 1 TGS (MI_SOLVER_*); anything else is refused  */
+    int32_t velocity_iterations;    /* TGS: solver_velocity_iteration_count (PGS: 0)  */
 } mi_sim_params;
+
+/* Contact / limit solvers. Both build the same constraint rows from the same
+ * state, with the rows' separation d (contact gap - rest_offset, or the joint's distance inside
+ * its limit).
+ *   MI_SOLVER_PGS: solver_iterations velocity-level Gauss-Seidel sweeps over the whole substep,
+ *     bias b = d >= 0 ? -d / dt : -erp d / dt (capped at max_depenetration_velocity); positions
+ *     integrated with the final velocity.
+ *   MI_SOLVER_TGS (PhysX's default, solver_type 1): solver_iterations position iterations, each a
+ *     sub-step h = dt / solver_iterations: one sweep with the bias of the row's CURRENT separation
+ *     d + J (sum of h u over the earlier sub-steps) over h; then velocity_iterations sweeps with
+ *     the speculative bias only (no position correction). Positions advance by the sub-steps'
+ *     velocities (dt x their mean), the velocity state is the last sweep's. */
+#define MI_SOLVER_PGS 0
+#define MI_SOLVER_TGS 1
 
 /* Task-layer parameters (cfg/task/{Humanoid,Ant,Cartpole}.yaml `env:` + task
  * constants from tasks/shared/locomotion.py:147-171, tasks/humanoid.py:81-112,

@@ -25,10 +25,21 @@ namespace mi {
 
 struct SimP {
     float dt, g[3];
-    int iters;
+    int iters;        // PGS: sweeps; TGS: position iterations (sub-steps)
     float contact_offset, rest_offset, friction, max_depen, erp, max_angvel;
     float ang_damp;   // per-link angular damping (1/s): torque -ang_damp * I_com * omega
+    int tgs;          // solver_type 1 (include/mi_sim.h MI_SOLVER_TGS)
+    int viters;       // TGS velocity iterations
+    float h;          // TGS sub-step dt / iters (PGS: dt)
 };
+
+// Constraint-row bias of a normal / limit row with separation e. PGS: over the substep (the
+// row stores its bias). TGS: over the sub-step h from the row's current separation; position
+// iterations correct a penetration (erp), velocity iterations only keep the speculative part.
+MI_D float row_bias(const SimP& p, float e, float step, bool correct) {
+    float b = e >= 0.0f ? -e / step : (correct ? -p.erp * e / step : 0.0f);
+    return b > p.max_depen ? p.max_depen : b;
+}
 
 MI_D void cartpole_substep(const DevModel& m, const SimP& p, float& x, float& th, float& xd,
                            float& thd, float F0, float F1) {
@@ -290,8 +301,7 @@ MI_D void artic_substep(const DevModel& m, const DevState& st, const SimP& p, in
         if (!(gap < p.contact_offset)) continue;
         const float pc[3] = {x[0], x[1], x[2] - r};
         const float d = gap - p.rest_offset;
-        float bn = d >= 0.0f ? -d / dt : -p.erp * d / dt;
-        if (bn > p.max_depen) bn = p.max_depen;
+        const float bn = p.tgs ? d : row_bias(p, d, dt, true);   // TGS: the row keeps its separation
 #pragma unroll
         for (int q = 0; q < 3; ++q) w[m.o_cp + 3 * ncon + q] = pc[q];
         w[m.o_cl + ncon] = (float)l;
@@ -321,9 +331,7 @@ MI_D void artic_substep(const DevModel& m, const DevState& st, const SimP& p, in
         const int ro = m.o_Jr + nrows * nv;
         for (int q = 0; q < nv; ++q) w[ro + q] = 0.0f;
         w[ro + k] = sg;
-        float bl = d >= 0.0f ? -d / dt : -p.erp * d / dt;
-        if (bl > p.max_depen) bl = p.max_depen;
-        w[m.o_b + nrows] = bl;
+        w[m.o_b + nrows] = p.tgs ? d : row_bias(p, d, dt, true);
         w[m.o_rk + nrows] = 3.0f;
         ++nrows;
     }
@@ -338,13 +346,21 @@ MI_D void artic_substep(const DevModel& m, const DevState& st, const SimP& p, in
     }
     // ---------------- projected Gauss-Seidel ----------------
     const float mu = p.friction;
-    for (int it = 0; it < p.iters; ++it) {
+    // TGS (include/mi_sim.h): o_b holds the row's separation, o_ds its change over the sub-steps
+    // so far, o_r (the solved rhs, dead here) the running sum of the sub-steps' velocities
+    for (int r = 0; r < nrows; ++r) w[m.o_ds + r] = 0.0f;
+    for (int q = 0; q < nv; ++q) w[m.o_r + q] = 0.0f;
+    for (int it = 0; it < p.iters + p.viters; ++it) {
         for (int r = 0; r < nrows; ++r) {
             const int ro = m.o_Jr + r * nv, wo = m.o_W + r * nv;
             float jv = 0.0f;
             for (int q = 0; q < nv; ++q) jv += w[ro + q] * w[m.o_u + q];
             const float l0 = w[m.o_lam + r];
-            float ln = l0 + (w[m.o_b + r] - jv) / w[m.o_Ad + r];
+            const int kd = (int)w[m.o_rk + r];
+            const float br = !p.tgs ? w[m.o_b + r]
+                             : (kd == 1 || kd == 2) ? 0.0f
+                             : row_bias(p, w[m.o_b + r] + w[m.o_ds + r], p.h, it < p.iters);
+            float ln = l0 + (br - jv) / w[m.o_Ad + r];
             const int kind = (int)w[m.o_rk + r];
             if (kind == 1 || kind == 2) {
                 const float lim = mu * w[m.o_lam + r - kind];
@@ -356,7 +372,19 @@ MI_D void artic_substep(const DevModel& m, const DevState& st, const SimP& p, in
             for (int q = 0; q < nv; ++q) w[m.o_u + q] += w[wo + q] * dl;
             w[m.o_lam + r] = ln;
         }
+        if (p.tgs && it < p.iters) {   // the sub-step moves the rows by h J u, the positions by h u
+            for (int r = 0; r < nrows; ++r) {
+                const int ro = m.o_Jr + r * nv;
+                float jv = 0.0f;
+                for (int q = 0; q < nv; ++q) jv += w[ro + q] * w[m.o_u + q];
+                w[m.o_ds + r] += p.h * jv;
+            }
+            for (int q = 0; q < nv; ++q) w[m.o_r + q] += w[m.o_u + q];
+        }
     }
+    if (p.tgs)   // the positions' velocity: the sub-steps' mean
+        for (int q = 0; q < nv; ++q) w[m.o_r + q] = w[m.o_r + q] / (float)p.iters;
+    const int o_up = p.tgs ? m.o_r : m.o_u;
     // ---------------- force sensors ----------------
     for (int si = 0; si < m.S; ++si) {
         const int l = m.sensor_link[si];
@@ -390,18 +418,28 @@ MI_D void artic_substep(const DevModel& m, const DevState& st, const SimP& p, in
     // ---------------- integrate ----------------
     bool finite = true;
     if (nr) {
-        float u[6];
+        float u[6], up[6];
 #pragma unroll
-        for (int k = 0; k < 6; ++k) u[k] = w[m.o_u + k];
-        float* om = u + 3;
+        for (int k = 0; k < 6; ++k) { u[k] = w[m.o_u + k]; up[k] = w[o_up + k]; }
+        if (p.tgs) {   // the velocity state's angular velocity cap
+            const float wv = sqrtf(dot3(u + 3, u + 3));
+            if (wv > p.max_angvel) {
+                const float sc = p.max_angvel / wv;
+                u[3] *= sc; u[4] *= sc; u[5] *= sc;
+            }
+        }
+        float* om = up + 3;
         float wn = sqrtf(dot3(om, om));
         if (wn > p.max_angvel) {
             const float sc = p.max_angvel / wn;
             om[0] *= sc; om[1] *= sc; om[2] *= sc;
             wn = p.max_angvel;
         }
+        if (!p.tgs)
 #pragma unroll
-        for (int k = 0; k < 3; ++k) rp[k] += dt * u[k];
+            for (int k = 0; k < 6; ++k) u[k] = up[k];
+#pragma unroll
+        for (int k = 0; k < 3; ++k) rp[k] += dt * up[k];
         const float th = wn * dt;
         if (th > 0.0f) {
             float sh, ch;
@@ -426,7 +464,7 @@ MI_D void artic_substep(const DevModel& m, const DevState& st, const SimP& p, in
     }
     for (int j = 0; j < D; ++j) {
         const float v = w[m.o_u + nr + j];
-        const float qn = st.q[sx(st, j, i)] + dt * v;
+        const float qn = st.q[sx(st, j, i)] + dt * w[o_up + nr + j];
         st.qd[sx(st, j, i)] = v;
         st.q[sx(st, j, i)] = qn;
         finite &= isfinite(v) && isfinite(qn);

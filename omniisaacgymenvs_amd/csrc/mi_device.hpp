@@ -52,7 +52,7 @@ struct DevModel {
     float cart_mass, pole_mass, pole_com, pole_inertia, cart_damping, pole_damping;
     // workspace slot offsets
     int o_R, o_o, o_aw, o_Ic, o_S, o_V, o_A, o_F, o_M, o_u, o_r, o_Jr, o_W, o_b, o_lam, o_Ad,
-        o_rk, o_cp, o_cl;
+        o_rk, o_cp, o_cl, o_ds;
 };
 
 // Physics state element (field k, env i) lives at k * fs + i * es floats from the field's

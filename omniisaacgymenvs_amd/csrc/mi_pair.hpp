@@ -135,9 +135,13 @@ MI_D void sdof_loop(const float* Ss, const float* R, F&& fn) {
 #ifndef MI_PAIR_WIDE_AREG
 #define MI_PAIR_WIDE_AREG 32   // wide-PGS Delassus rows in registers (0, 32 or 64); the rest streamed
 #endif
-// wide-PGS Delassus rows that live in the wave's global scratch (rows AREG..63): the scratch
-// holds exactly these, (64 - AREG) rows x 64 lanes of f32 per resident-or-not wave (N / 2 waves)
-constexpr int kWideScratchRows = 64 - MI_PAIR_WIDE_AREG;
+#ifndef MI_PAIR_WIDE_MFMA
+#define MI_PAIR_WIDE_MFMA 0   // wide Delassus set-up as f32 MFMA tiles through the wave's scratch (0: per-lane FMA rows)
+#endif
+// the wave's global scratch of the wide sweeps, rows of 64 lanes of f32 per wave (N / 2 waves):
+// with the MFMA set-up the whole 64 x 64 Delassus block plus J^T (up to 32 DOF columns); else
+// the rows AREG..63 the sweeps stream (the rest stay in registers)
+constexpr int kWideScratchRows = MI_PAIR_WIDE_MFMA ? 64 + 32 : 64 - MI_PAIR_WIDE_AREG;
 #ifndef MI_PAIR_WIDE_AP
 #define MI_PAIR_WIDE_AP 8   // Delassus rows streamed ahead of the wide sweeps' chain
 #endif
@@ -389,8 +393,7 @@ MI_D void pair_artic_substep(const DevModel& m, const WaveTabs& t, const DevStat
                 act = gap < p.contact_offset;
                 pc[0] = x[0]; pc[1] = x[1]; pc[2] = x[2] - rr;
                 const float d = gap - p.rest_offset;
-                bn = d >= 0.0f ? -d / dt : -p.erp * d / dt;
-                if (bn > p.max_depen) bn = p.max_depen;
+                bn = p.tgs ? d : row_bias(p, d, dt, true);   // TGS: the row keeps its separation
             }
             const unsigned mask = hballot(act);
             if (act) {
@@ -484,8 +487,7 @@ MI_D void pair_artic_substep(const DevModel& m, const WaveTabs& t, const DevStat
                     const float gap = mi_pair_contact(A, A + 3, A[6], B, B + 3, B[6], pc, n);
                     act = gap < p.contact_offset;
                     const float d = gap - p.rest_offset;
-                    bn = d >= 0.0f ? -d / dt : -p.erp * d / dt;
-                    if (bn > p.max_depen) bn = p.max_depen;
+                    bn = p.tgs ? d : row_bias(p, d, dt, true);   // TGS: the row keeps its separation
                 }
                 const unsigned mask = hballot(act);
                 const int rank = __popc(mask & lanemask_lt(lane));
@@ -574,8 +576,7 @@ MI_D void pair_artic_substep(const DevModel& m, const WaveTabs& t, const DevStat
                 float d = 0.0f;
                 if (qj < lo || qp < lo) { d = qj - lo; sg = 1.0f; act = true; }
                 else if (qj > hi || qp > hi) { d = hi - qj; sg = -1.0f; act = true; }
-                bl = d >= 0.0f ? -d / dt : -p.erp * d / dt;
-                if (bl > p.max_depen) bl = p.max_depen;
+                bl = p.tgs ? d : row_bias(p, d, dt, true);
             }
         }
         const unsigned lb = hballot(act);
@@ -743,7 +744,14 @@ MI_D void pair_artic_substep(const DevModel& m, const WaveTabs& t, const DevStat
         float lamv[RMAX];
 #pragma unroll
         for (int rr = 0; rr < RMAX; ++rr) lamv[rr] = 0.0f;
-        for (int it = 0; it < p.iters; ++it) {
+        // TGS: b holds the row's separation; each sub-step's bias comes from the separation plus
+        // h x the row velocities J_r u of the earlier sub-steps (ds), and the owner lane sums its
+        // row's lambda over the sub-steps (lsum: u-bar = u* + W lsum / iters)
+        [[maybe_unused]] const float sep = b;
+        [[maybe_unused]] float ds = 0.0f, lsum = 0.0f;
+        for (int it = 0; it < p.iters + p.viters; ++it) {
+            if constexpr (TP::kTgs)
+                b = (kd == 1 || kd == 2) ? 0.0f : row_bias(p, sep + ds, p.h, it < p.iters);
             asm volatile("" : "+v"(b), "+v"(ia), "+v"(kd));
             int nrow_it = nrows_max;
             asm volatile("" : "+s"(nrow_it));
@@ -770,9 +778,20 @@ MI_D void pair_artic_substep(const DevModel& m, const WaveTabs& t, const DevStat
                     lamv[rr] = ln;
                 }
             });
+            if constexpr (TP::kTgs) {
+                if (it < p.iters) {   // the sub-step moves row r by h v_r; its lambda joins the sum
+                    ds += p.h * v;
+                    float lo = 0.0f;
+#pragma unroll
+                    for (int rr = 0; rr < RMAX; ++rr) lo = lane_here(lane) == rr ? lamv[rr] : lo;
+                    lsum += lo;
+                }
+            }
         }
         STAMP(28);
         float u = lane < NV ? us[lane] : 0.0f;
+        [[maybe_unused]] float ub = u;
+        [[maybe_unused]] const float lbar = lsum / (float)p.iters;
         const int kc = lane < NV ? lane : 0;
         sfor<0, RMAX / 4>([&](auto G) {
             constexpr int g0 = 4 * G;
@@ -781,9 +800,18 @@ MI_D void pair_artic_substep(const DevModel& m, const WaveTabs& t, const DevStat
                 pair_wcol(t, sm, gW, g0, kc, NV, wq);
 #pragma unroll
                 for (int q = 0; q < 4; ++q) u = g0 + q < nrows ? u + wq[q] * lamv[g0 + q] : u;
+                if constexpr (TP::kTgs) {
+                    sfor<0, 4>([&](auto Q) {
+                        constexpr int q = Q;
+                        const float lq = pbcc<g0 + q>(lbar);
+                        ub = g0 + q < nrows ? ub + wq[q] * lq : ub;
+                    });
+                }
             }
         });
         if (lane < NV) us[lane] = u;
+        if constexpr (TP::kTgs)   // the positions' velocity (sub-steps' mean), in the dead rhs
+            if (lane < NV) sm[t.s_r + lane] = ub;
         wave_sync();
         {   // reuse: lambda of row rr, written by lane rr (one select chain, one store)
             float lo = 0.0f;
@@ -807,11 +835,13 @@ MI_D void pair_artic_substep(const DevModel& m, const WaveTabs& t, const DevStat
         constexpr int AR = MI_PAIR_WIDE_AREG;   // Delassus rows kept in registers; the rest streamed
         const int l64 = pair_l64(), me = l64 >> 5;
         const int kc = l64 < NV ? l64 : 0;
-        // this wave's scratch (i >> 1: the same for both halves) holds rows AR..63, addressed
-        // through a buffer resource: one lane offset register for every row (row s at soffset
-        // 256 (s - AR)); loads past the record range (prefetch beyond row 63) return 0
+        // this wave's scratch (i >> 1: the same for both halves), addressed through a buffer
+        // resource: one lane offset register for every row (Delassus row s at soffset 256 (s -
+        // A0), A0 = 0 with the MFMA set-up (all 64 rows there), else AR); loads past the record
+        // range (prefetch beyond the last row) return 0
         const int wv = __builtin_amdgcn_readfirstlane(i >> 1);
         constexpr int WR = kWideScratchRows > 0 ? kWideScratchRows : 1;
+        constexpr int A0 = MI_PAIR_WIDE_MFMA ? 0 : AR;
         const __amdgpu_buffer_rsrc_t ars = __builtin_amdgcn_make_buffer_rsrc(
             (void*)(t.g_wa + (size_t)wv * (WR * 64)), (short)0, WR * 64 * (int)sizeof(float), 0x00020000);
         const int avo = l64 * (int)sizeof(float);
@@ -819,8 +849,15 @@ MI_D void pair_artic_substep(const DevModel& m, const WaveTabs& t, const DevStat
         for (int h = 0; h < 2; ++h) {
             const int nrh = __builtin_amdgcn_readlane(nrows, 32 * h);
             const int nnh = 3 * __builtin_amdgcn_readlane(ncon, 32 * h);
-            if (nrh == 0) continue;
             float* smh = sm + (h - me) * t.env_stride;                 // env of half h
+            if (nrh == 0) {
+                // no rows: u = u*; TGS integrates positions with u-bar = u* as well
+                if constexpr (TP::kTgs) {
+                    if (l64 < NV) smh[t.s_r + l64] = smh[t.s_us + l64];
+                    wave_sync();
+                }
+                continue;
+            }
             const float* gWh = gW + (ptrdiff_t)(h - me) * (ptrdiff_t)t.g_row_stride;
             const int rl = l64 < nrh ? l64 : 0;
             float Jr[TP::nvc];
@@ -830,6 +867,126 @@ MI_D void pair_artic_substep(const DevModel& m, const WaveTabs& t, const DevStat
             sfor<0, NV>([&](auto C) { v += Jr[C] * ush[C]; });
             STAMP(30);
             float Ar[AR > 0 ? AR : 1];
+#if MI_PAIR_WIDE_MFMA
+            {
+                // A = J W^T as v_mfma_f32_16x16x4f32 tiles (A[m][k] at lane m + 16 k, B[k][n] at
+                // lane n + 16 k, D[4 (l >> 4) + i][l & 15] in register i): J^T goes to the scratch
+                // (column c at row 64 + c, lane = constraint row; rows past the env's count and the
+                // padding columns 0), each 16-row block of J comes back in the A-operand layout, W
+                // in the B-operand layout straight from LDS / the slab. A tile's D is stored as
+                // scratch rows 16 R + 4 (l >> 4) + i, lanes 16 S + (l & 15): row s then holds
+                // A[s][r] at lane r (A symmetric), the layout the sweeps read. Every 16-lane
+                // column block is written (rows past the count come out 0), row blocks up to the
+                // count only (the sweeps read no further). Sums in the MFMA's order, not DOF order.
+                constexpr int KP = (NV + 3) & ~3, KC = KP / 4;
+                static_assert(KP <= 32, "wide scratch holds 32 J^T columns");
+                sfor<0, KP>([&](auto C) {
+                    constexpr int c = C;
+                    float jv = 0.0f;
+                    if constexpr (c < NV) jv = l64 < nrh ? Jr[c] : 0.0f;
+                    __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(unsigned, jv), ars, avo, (64 + c) * 256, 0);
+                });
+                wave_sync();   // J^T stored before the A-operand loads read it back
+                const int lr = l64 & 15, lk = l64 >> 4;
+                const int jvo = ((64 + lk) * 64 + lr) * (int)sizeof(float);
+                const int dvo = (4 * lk * 64 + lr) * (int)sizeof(float);
+                sfor<0, 4>([&](auto S) {   // column block: lanes 16 S .. 16 S + 15
+                    const int s = 16 * S + lr;
+                    float wb[KC];
+                    sfor<0, KC>([&](auto K) {
+                        const int c = 4 * K + lk;
+                        float w = 0.0f;
+                        if (16 * S < nrh && s < nrh && c < NV) {
+                            if (s < t.w_rows_lds) w = lds_ptr(smh)[t.s_W + pw_idx(s, c, NV)];
+                            else w = gWh[pair_sidx(s, c)];
+                        }
+                        wb[K] = w;
+                    });
+                    sfor<0, 4>([&](auto R) {   // row block: scratch rows 16 R .. 16 R + 15
+                        if (16 * R < nrh) {
+                            pv4 d = {0.0f, 0.0f, 0.0f, 0.0f};
+                            sfor<0, KC>([&](auto K) {
+                                const float ja = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(
+                                                                               ars, jvo, (K * 256 + 16 * R) * 4, 0));
+                                d = __builtin_amdgcn_mfma_f32_16x16x4f32(ja, wb[K], d, 0, 0, 0);
+                            });
+                            // D moved to VGPRs first: stored straight from the accumulator tuple, this
+                            // compiler (ROCm 7.2) emits four stores of its first register
+                            // (tools/mfma_wide_check.hip)
+                            float o4[4] = {d.x, d.y, d.z, d.w};
+                            asm volatile("" : "+v"(o4[0]), "+v"(o4[1]), "+v"(o4[2]), "+v"(o4[3]));
+#pragma unroll
+                            for (int q = 0; q < 4; ++q)
+                                __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(unsigned, o4[q]), ars, dvo,
+                                                                      ((16 * R + q) * 64 + 16 * S) * 4, 0);
+                        }
+                    });
+                });
+                wave_sync();   // the tiles stored before the rows are read back lane = row
+                if constexpr (AR > 0) {
+                    sfor<0, AR / 4>([&](auto G) {
+                        constexpr int g0 = 4 * G;
+                        if (g0 < nrh) {
+#pragma unroll
+                            for (int q = 0; q < 4; ++q)
+                                Ar[g0 + q] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(
+                                                                           ars, avo, (g0 + q) * 256, 0));
+                        } else {
+#pragma unroll
+                            for (int q = 0; q < 4; ++q) Ar[g0 + q] = 0.0f;
+                        }
+                    });
+                }
+#ifdef MI_WIDE_DBG
+                {
+                    int bad_row = -1;
+                    float bm = 0.0f, ba = 0.0f;
+                    for (int g0 = 0; g0 < nrh; g0 += 4) {
+                        float a[4];
+                        pair_dgroup<TP, 4>(t, smh, gWh, g0, nrh, Jr, a);
+                        for (int q = 0; q < 4; ++q) {
+                            const float m = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(
+                                                                         ars, avo, (g0 + q) * 256, 0));
+                            if (l64 < nrh && g0 + q < nrh && bad_row < 0 && !(fabsf(m - a[q]) <= 1e-4f * (1.0f + fabsf(a[q])))) {
+                                bad_row = g0 + q; bm = m; ba = a[q];
+                            }
+                        }
+                    }
+                    const unsigned long long bl = __ballot(bad_row >= 0);
+                    if (bl && l64 == __builtin_ctzll(bl))
+                        printf("WIDE_DBG wave %d half %d nrh %d lane %d row %d mfma %g fma %g w_rows_lds %d\n", wv, h, nrh,
+                               l64, bad_row, bm, ba, t.w_rows_lds);
+                    if (l64 == 0 && !bl) printf("WIDE_OK wave %d half %d nrh %d\n", wv, h, nrh);
+                    // FMA values in the old layout (row s, lane r: J_r . W_s), read back transposed
+                    for (int g0 = 0; g0 < nrh; g0 += 4) {
+                        float a[4];
+                        pair_dgroup<TP, 4>(t, smh, gWh, g0, nrh, Jr, a);
+                        for (int q = 0; q < 4; ++q)
+                            __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(unsigned, a[q]), ars, avo, (g0 + q) * 256, 0);
+                    }
+                    wave_sync();
+                    int bad_m = -1, bad_s = -1;
+                    float m1 = 0.0f, m2 = 0.0f, s1 = 0.0f, s2 = 0.0f;
+                    sfor<0, AR>([&](auto Sx) {
+                        constexpr int s = Sx;
+                        if (s < nrh && l64 < nrh) {
+                            // row l64, lane s: J_s . W_l64 (FMA, lane s)
+                            const float tr = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(ars, l64 * 256, s * 4, 0));
+                            const float own = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(ars, avo, s * 256, 0));
+                            if (bad_m < 0 && !(fabsf(Ar[s] - tr) <= 1e-4f * (1.0f + fabsf(tr)))) { bad_m = s; m1 = Ar[s]; m2 = tr; }
+                            if (bad_s < 0 && !(fabsf(own - tr) <= 1e-4f * (1.0f + fabsf(tr)))) { bad_s = s; s1 = own; s2 = tr; }
+                        }
+                    });
+                    const unsigned long long b1 = __ballot(bad_m >= 0), b2 = __ballot(bad_s >= 0);
+                    if (b1 && l64 == __builtin_ctzll(b1))
+                        printf("WIDE_MFMA_BAD wave %d lane %d s %d mfma %g fma_T %g\n", wv, l64, bad_m, m1, m2);
+                    if (b2 && l64 == __builtin_ctzll(b2))
+                        printf("WIDE_ASYM wave %d lane %d s %d J_l.W_s %g J_s.W_l %g\n", wv, l64, bad_s, s1, s2);
+                    if (l64 == 0 && !b1) printf("WIDE_MFMA_OK wave %d\n", wv);
+                }
+#endif
+            }
+#else
             sfor<0, 16>([&](auto G) {
                 constexpr int g0 = 4 * G;
                 float a[4] = {0.0f, 0.0f, 0.0f, 0.0f};
@@ -845,6 +1002,7 @@ MI_D void pair_artic_substep(const DevModel& m, const WaveTabs& t, const DevStat
                 if constexpr (g0 < AR) { Ar[g0] = a[0]; Ar[g0 + 1] = a[1]; Ar[g0 + 2] = a[2]; Ar[g0 + 3] = a[3]; }
             });
             if constexpr (AR < 64) wave_sync();
+#endif
             STAMP(27);
             float b = 0.0f, ia = 0.0f, lam = 0.0f;    // ia 0: a dead row keeps its lambda 0
             int kd = 0;
@@ -853,7 +1011,13 @@ MI_D void pair_artic_substep(const DevModel& m, const WaveTabs& t, const DevStat
                 ia = 1.0f / smh[t.s_ad + l64];
                 kd = l64 < nnh ? l64 % 3 : 3;
             }
-            for (int it = 0; it < p.iters; ++it) {
+            // TGS as in the narrow sweeps: b holds the separation, ds the sub-steps' motion of
+            // the row, lsum the row's lambda summed over the sub-steps (lane = row here)
+            [[maybe_unused]] const float sep = b;
+            [[maybe_unused]] float ds = 0.0f, lsum = 0.0f;
+            for (int it = 0; it < p.iters + p.viters; ++it) {
+                if constexpr (TP::kTgs)
+                    b = (kd == 1 || kd == 2) ? 0.0f : row_bias(p, sep + ds, p.h, it < p.iters);
                 asm volatile("" : "+v"(b), "+v"(ia), "+v"(kd));
                 int nrow_it = nrh;
                 asm volatile("" : "+s"(nrow_it));
@@ -867,7 +1031,7 @@ MI_D void pair_artic_substep(const DevModel& m, const WaveTabs& t, const DevStat
                 // out of the sweep loop (64 SGPR-pair masks would spill and reload per row)
                 asm volatile("" : "+v"(vo), "+v"(lw));
                 auto ald = [&](int r) {
-                    return __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(ars, vo, (r - AR) * 256, 0));
+                    return __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(ars, vo, (r - A0) * 256, 0));
                 };
                 // rows AR.. streamed: their first PA loads are issued before the sweep, so the
                 // register rows' steps hide their latency
@@ -898,10 +1062,15 @@ MI_D void pair_artic_substep(const DevModel& m, const WaveTabs& t, const DevStat
                         lam = lw == rr ? mine : lam;
                     }
                 });
+                if constexpr (TP::kTgs) {
+                    if (it < p.iters) { ds += p.h * v; lsum += lam; }
+                }
             }
             STAMP(28);
-            // u = u* + sum_r W_r lambda_r, lane = DOF
+            // u = u* + sum_r W_r lambda_r, lane = DOF (TGS: and u-bar = u* + W lsum / iters)
             float u = ush[kc];
+            [[maybe_unused]] float ub = u;
+            [[maybe_unused]] const float lbar = lsum / (float)p.iters;
             sfor<0, 16>([&](auto G) {
                 constexpr int g0 = 4 * G;
                 if (g0 < nrh) {
@@ -911,11 +1080,17 @@ MI_D void pair_artic_substep(const DevModel& m, const WaveTabs& t, const DevStat
                     for (int q = 0; q < 4; ++q) {
                         const float lq = readlane(lam, g0 + q);
                         u = g0 + q < nrh ? u + wq[q] * lq : u;
+                        if constexpr (TP::kTgs) {
+                            const float lb = readlane(lbar, g0 + q);
+                            ub = g0 + q < nrh ? ub + wq[q] * lb : ub;
+                        }
                     }
                 }
             });
             wave_sync();
             if (l64 < NV) smh[t.s_us + l64] = u;
+            if constexpr (TP::kTgs)
+                if (l64 < NV) smh[t.s_r + l64] = ub;
             if (l64 < nrh) smh[t.s_ad + l64] = lam;            // reuse: lambda of row l64
             wave_sync();
             STAMP(11);
@@ -969,7 +1144,10 @@ MI_D void pair_artic_substep(const DevModel& m, const WaveTabs& t, const DevStat
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
         STAMP(27);
-        for (int it = 0; it < p.iters; ++it) {
+        // TGS in u space: b0 / b1 / s_rb hold the rows' separations; usum sums the sub-steps'
+        // velocities (lane = DOF), so row r has moved by h J_r usum before the current sub-step
+        [[maybe_unused]] float usum = 0.0f;
+        for (int it = 0; it < p.iters + p.viters; ++it) {
             asm volatile("" : "+v"(b0), "+v"(b1), "+v"(ia0), "+v"(ia1),
                          "+v"(ma), "+v"(mb), "+v"(ma2), "+v"(mb2));
             int lfb = lane, nrl = nrows;
@@ -995,7 +1173,10 @@ MI_D void pair_artic_substep(const DevModel& m, const WaveTabs& t, const DevStat
                 const float j0 = kind == 3 ? fr[0] : d6;
                 const float jc = ((((msk >> lane) & 1u) ? j0 : 0.0f) - (((msk2 >> lane) & 1u) ? j0 : 0.0f)) * kin;
                 const float jv = psum(jc * u);
-                const float br = pbc(bank ? b1 : b0, w), iar = pbc(bank ? ia1 : ia0, w);
+                float br = pbc(bank ? b1 : b0, w);
+                const float iar = pbc(bank ? ia1 : ia0, w);
+                if constexpr (TP::kTgs)
+                    br = (kind == 1 || kind == 2) ? 0.0f : row_bias(p, br + p.h * psum(jc * usum), p.h, it < p.iters);
                 const float l0 = pbc(bank ? lam1 : lam0, w);
                 float ln = l0 + (br - jv) * iar;
                 const bool fric = kind == 1 || kind == 2;
@@ -1032,7 +1213,10 @@ MI_D void pair_artic_substep(const DevModel& m, const WaveTabs& t, const DevStat
                 const float jv = psum(jc * u);
                 float* lp = gW + pair_sidx(rs, WNV - 1);
                 const float l0 = live_row ? *lp : 0.0f;
-                float ln = l0 + (br - jv) * (1.0f / ar);
+                float brt = br;
+                if constexpr (TP::kTgs)
+                    brt = (kind == 1 || kind == 2) ? 0.0f : row_bias(p, br + p.h * psum(jc * usum), p.h, it < p.iters);
+                float ln = l0 + (brt - jv) * (1.0f / ar);
                 const bool fric = kind == 1 || kind == 2;
                 const float lim = mu * lamn;
                 ln = fmaxf(ln, fric ? -lim : 0.0f);
@@ -1045,9 +1229,13 @@ MI_D void pair_artic_substep(const DevModel& m, const WaveTabs& t, const DevStat
                 if (live_row && lane == 0) *lp = ln;
                 __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
             }
+            if constexpr (TP::kTgs)
+                if (it < p.iters) usum += u;
         }
         STAMP(28);
         if (lane < nv) us[lane] = u;
+        if constexpr (TP::kTgs)   // the positions' velocity: the sub-steps' mean
+            if (lane < nv) sm[t.s_r + lane] = usum / (float)p.iters;
         if (lane < nrows) sm[t.s_ad + lane] = lam0;          // reuse: lambda of row lane
         if (lane + 32 < nrows) sm[t.s_ad + lane + 32] = lam1;
         for (int r = 64 + lane; r < nrows; r += 32) sm[t.s_ad + r] = gW[pair_sidx(r, WNV - 1)];
@@ -1161,9 +1349,12 @@ MI_D void pair_artic_substep(const DevModel& m, const WaveTabs& t, const DevStat
     }
     // ---- P11b: integrate; non-finite -> nan flag
     bool finite = true;
+    // TGS: positions advance with the sub-steps' mean velocity (in the dead rhs), the velocity
+    // state is the last sweep's
+    const float* up = TP::kTgs ? sm + t.s_r : us;
     if (lane < D) {
         const float v = us[nr + lane];
-        const float qn = sm[t.s_q + lane] + dt * v;
+        const float qn = sm[t.s_q + lane] + dt * up[nr + lane];
         if (store_state) {
             st.qd[sx(st, lane, i)] = v;
             st.q[sx(st, lane, i)] = qn;
@@ -1173,22 +1364,32 @@ MI_D void pair_artic_substep(const DevModel& m, const WaveTabs& t, const DevStat
     }
     if (store_state && lane < 6 * m.S) st.sens[ssx(st, lane, i)] = sm[t.s_rb + lane];
     if (nr && lane == 0) {
-        float u6[6], rp[3], rq[4];
+        float u6[6], p6[6], rp[3], rq[4];
 #pragma unroll
-        for (int k = 0; k < 6; ++k) u6[k] = us[k];
+        for (int k = 0; k < 6; ++k) { u6[k] = us[k]; p6[k] = up[k]; }
 #pragma unroll
         for (int k = 0; k < 3; ++k) rp[k] = sm[t.s_rp + k];
 #pragma unroll
         for (int k = 0; k < 4; ++k) rq[k] = sm[t.s_rp + 4 + k];
-        float* om = u6 + 3;
+        if constexpr (TP::kTgs) {   // the velocity state's angular velocity cap
+            const float wv = sqrtf(dot3(u6 + 3, u6 + 3));
+            if (wv > p.max_angvel) {
+                const float sc = p.max_angvel / wv;
+                u6[3] *= sc; u6[4] *= sc; u6[5] *= sc;
+            }
+        }
+        float* om = p6 + 3;
         float wn = sqrtf(dot3(om, om));
         if (wn > p.max_angvel) {
             const float sc = p.max_angvel / wn;
             om[0] *= sc; om[1] *= sc; om[2] *= sc;
             wn = p.max_angvel;
         }
+        if constexpr (!TP::kTgs)
 #pragma unroll
-        for (int k = 0; k < 3; ++k) rp[k] += dt * u6[k];
+            for (int k = 0; k < 6; ++k) u6[k] = p6[k];
+#pragma unroll
+        for (int k = 0; k < 3; ++k) rp[k] += dt * p6[k];
         const float th = wn * dt;
         if (th > 0.0f) {
             float sh, ch;

@@ -422,13 +422,18 @@ struct KParams {
 };
 
 // launch with the model's compile-time topology (mi_topo_gen.hpp) or the runtime tables
+// (per solver: TGS instantiations are Tgs<topology>)
 template <class F>
-static void with_topo(int id, F&& f) {
+static void with_topo(int id, bool tgs, F&& f) {
+    auto go = [&](auto T) {
+        if (tgs) f(Tgs<decltype(T)>{});
+        else f(T);
+    };
     switch (id) {
-        case RobotHumanoid::id: f(TopoCT<RobotHumanoid>{}); break;
+        case RobotHumanoid::id: go(TopoCT<RobotHumanoid>{}); break;
 #ifndef MI_DEV_ONLY_HUMANOID   // register / spill inspection builds (tools/regs.sh): one topology
-        case RobotAnt::id: f(TopoCT<RobotAnt>{}); break;
-        default: f(TopoRuntime{}); break;
+        case RobotAnt::id: go(TopoCT<RobotAnt>{}); break;
+        default: go(TopoRuntime{}); break;
 #else
         default: break;
 #endif
@@ -1103,6 +1108,7 @@ int mi_sim_create(const mi_model_desc* md, const mi_sim_params* prm, int32_t N, 
         m.o_lam = o; o += R;
         m.o_Ad = o; o += R;
         m.o_rk = o; o += R;
+        m.o_ds = o; o += R;     // TGS: a row's separation change over the sub-steps so far
         m.o_cp = o; o += 3 * m.npts;
         m.o_cl = o; o += m.npts;
     }
@@ -1276,7 +1282,7 @@ int mi_sim_create(const mi_model_desc* md, const mi_sim_params* prm, int32_t N, 
         // [s_R, s_total) gets the floats that leave envs_cu envs inside the CU's 160 KB.
         int waves = 2, lam_rows = 0;
         bool pair_ok = false;
-        with_topo(s->topo, [&](auto T) {
+        with_topo(s->topo, s->sp.tgs != 0, [&](auto T) {
             waves = decltype(T)::kWaves; lam_rows = decltype(T)::kLamRows;
             pair_ok = has_pair<decltype(T)>();
         });
@@ -1437,7 +1443,17 @@ int mi_sim_create(const mi_model_desc* md, const mi_sim_params* prm, int32_t N, 
     // params
     s->sp.dt = prm->dt;
     for (int k = 0; k < 3; ++k) s->sp.g[k] = prm->gravity[k];
+    if (prm->solver_type != MI_SOLVER_PGS && prm->solver_type != MI_SOLVER_TGS)
+        return cleanup(fail(MI_E_ARG, "solver_type %d: this build implements 0 (PGS) and 1 (TGS)",
+                            prm->solver_type));
+    if (prm->solver_iterations < 1 || prm->solver_iterations > 64 || prm->velocity_iterations < 0 ||
+        prm->velocity_iterations > 64)
+        return cleanup(fail(MI_E_ARG, "solver iterations %d / velocity iterations %d out of range",
+                            prm->solver_iterations, prm->velocity_iterations));
     s->sp.iters = prm->solver_iterations;
+    s->sp.tgs = prm->solver_type == MI_SOLVER_TGS ? 1 : 0;
+    s->sp.viters = s->sp.tgs ? prm->velocity_iterations : 0;
+    s->sp.h = s->sp.tgs ? prm->dt / (float)prm->solver_iterations : prm->dt;
     s->sp.contact_offset = prm->contact_offset;
     s->sp.rest_offset = prm->rest_offset;
     s->sp.friction = prm->friction;
@@ -1480,7 +1496,7 @@ int mi_sim_create(const mi_model_desc* md, const mi_sim_params* prm, int32_t N, 
         if ((rc = dev_alloc(s, &p, sizeof(float) * (size_t)N * s->wt.g_row_stride))) return cleanup(rc);
         s->rows = (float*)p;
         s->wt.g_wa = nullptr;
-        if (s->pair) {   // wide-PGS Delassus scratch: rows AREG..63 x 64 lanes per wave (mi_pair.hpp)
+        if (s->pair) {   // wide-PGS scratch: kWideScratchRows x 64 lanes per wave (mi_pair.hpp)
             const size_t nb = sizeof(float) * (size_t)(N / 2) * 64 * (size_t)(kWideScratchRows > 0 ? kWideScratchRows : 1);
             size_t fr = 0, tot = 0;
             if (hipMemGetInfo(&fr, &tot) == hipSuccess && nb > fr)
@@ -1507,7 +1523,7 @@ int mi_sim_create(const mi_model_desc* md, const mi_sim_params* prm, int32_t N, 
     if ((rc = sync_kparams(s))) return cleanup(rc);
     if (s->wave && s->lds_bytes > 64 * 1024) {   // above the default dynamic-LDS limit
         hipError_t e1 = hipSuccess, e2 = hipSuccess;
-        with_topo(s->topo, [&](auto T) {
+        with_topo(s->topo, s->sp.tgs != 0, [&](auto T) {
             if constexpr (has_pair<decltype(T)>()) {
                 if (s->pair) {
                     e1 = hipFuncSetAttribute((const void*)k_env_step_pair<decltype(T)>,
@@ -1607,7 +1623,7 @@ static int launch_sim(mi_sim* s, int substeps, hipStream_t stream) {
     if (mirrored)
         if (int rc = order_mirror_write(s, stream)) return rc;
     if (s->wave)
-        with_topo(s->topo, [&](auto T) {
+        with_topo(s->topo, s->sp.tgs != 0, [&](auto T) {
             if constexpr (has_pair<decltype(T)>()) {
                 if (s->pair) {
                     Mirrors mir{};
@@ -2049,7 +2065,7 @@ int mi_env_step(mi_sim* s, const float* actions, int32_t substeps, float* obs_ou
     hipEvent_t ev0 = nullptr, ev1 = nullptr;
     HIP_TRY(timed_launch(s, stream, &ev0, &ev1));
     if (s->wave && s->tp.kind != MI_TASK_CARTPOLE)
-        with_topo(s->topo, [&](auto T) {
+        with_topo(s->topo, s->sp.tgs != 0, [&](auto T) {
             if constexpr (has_pair<decltype(T)>()) {
                 if (s->pair) {
                     if (ev0)

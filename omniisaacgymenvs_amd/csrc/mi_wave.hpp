@@ -777,8 +777,7 @@ MI_D void wave_artic_substep(const DevModel& m, const WaveTabs& t, const DevStat
             act = gap < p.contact_offset;
             pc[0] = x[0]; pc[1] = x[1]; pc[2] = x[2] - r;
             const float d = gap - p.rest_offset;
-            bn = d >= 0.0f ? -d / dt : -p.erp * d / dt;
-            if (bn > p.max_depen) bn = p.max_depen;
+            bn = p.tgs ? d : row_bias(p, d, dt, true);   // TGS: the row keeps its separation
         }
         const unsigned long long mask = __ballot(act);
         ncon = __popcll(mask);
@@ -877,8 +876,7 @@ MI_D void wave_artic_substep(const DevModel& m, const WaveTabs& t, const DevStat
                 const float gap = mi_pair_contact(A, A + 3, A[6], B, B + 3, B[6], pc, n);
                 act = gap < p.contact_offset;
                 const float d = gap - p.rest_offset;
-                bn = d >= 0.0f ? -d / dt : -p.erp * d / dt;
-                if (bn > p.max_depen) bn = p.max_depen;
+                bn = p.tgs ? d : row_bias(p, d, dt, true);   // TGS: the row keeps its separation
             }
             const unsigned long long mask = __ballot(act);
             const int rank = __popcll(mask & ((1ull << lane) - 1ull));
@@ -926,8 +924,7 @@ MI_D void wave_artic_substep(const DevModel& m, const WaveTabs& t, const DevStat
                 const float gap = mi_pair_contact(a0, a1, A[7], b0, b1, B[7], pc, n);
                 act = gap < p.contact_offset;
                 const float d = gap - p.rest_offset;
-                bn = d >= 0.0f ? -d / dt : -p.erp * d / dt;
-                if (bn > p.max_depen) bn = p.max_depen;
+                bn = p.tgs ? d : row_bias(p, d, dt, true);   // TGS: the row keeps its separation
             }
             const unsigned long long mask = __ballot(act);
             const int rank = __popcll(mask & ((1ull << lane) - 1ull));
@@ -988,8 +985,7 @@ MI_D void wave_artic_substep(const DevModel& m, const WaveTabs& t, const DevStat
                 float d = 0.0f;
                 if (qj < lo || qp < lo) { d = qj - lo; sg = 1.0f; act = true; }
                 else if (qj > hi || qp > hi) { d = hi - qj; sg = -1.0f; act = true; }
-                bl = d >= 0.0f ? -d / dt : -p.erp * d / dt;
-                if (bl > p.max_depen) bl = p.max_depen;
+                bl = p.tgs ? d : row_bias(p, d, dt, true);
             }
         }
         limact = __ballot(act);
@@ -1205,7 +1201,14 @@ MI_D void wave_artic_substep(const DevModel& m, const WaveTabs& t, const DevStat
                 Ar[g0] = a0; Ar[g0 + 1] = a1; Ar[g0 + 2] = a2; Ar[g0 + 3] = a3;
             }
             const float mu = p.friction;
-            for (int it = 0; it < p.iters; ++it) {
+            // TGS: b holds the row's separation, ds the row's motion over the earlier sub-steps,
+            // lsum its lambda summed over the sub-steps (u-bar = u* + W lsum / iters)
+            [[maybe_unused]] const float sep = b;
+            [[maybe_unused]] float ds = 0.0f, lsum = 0.0f;
+            [[maybe_unused]] const int kdl = lane < nc ? lane % 3 : 3;
+            for (int it = 0; it < p.iters + p.viters; ++it) {
+                if constexpr (TP::kTgs)
+                    b = (kdl == 1 || kdl == 2) ? 0.0f : row_bias(p, sep + ds, p.h, it < p.iters);
                 // opaque per sweep: keeps the loop-invariant readlanes inside the sweep
                 asm volatile("" : "+v"(b), "+v"(ia));
                 int nrow_it = nrows;
@@ -1234,8 +1237,13 @@ MI_D void wave_artic_substep(const DevModel& m, const WaveTabs& t, const DevStat
                         lam = lane_here(lane) == rr ? ln : lam;
                     }
                 });
+                if constexpr (TP::kTgs) {
+                    if (it < p.iters) { ds += p.h * v; lsum += lam; }
+                }
             }
             float u = lane < NV ? us[lane] : 0.0f;
+            [[maybe_unused]] float ub = u;
+            [[maybe_unused]] const float lbar = lsum / (float)p.iters;
             const int kc = lane < NV ? lane : 0;
             // u = u* + sum_r W_r lambda_r in row order; four rows' W loads per uniform branch
             // (one LDS round trip per group instead of per row); rows past nrows add W 0
@@ -1250,8 +1258,14 @@ MI_D void wave_artic_substep(const DevModel& m, const WaveTabs& t, const DevStat
                 }
 #pragma unroll
                 for (int q = 0; q < 4; ++q) u += wq[q] * lq[q];
+                if constexpr (TP::kTgs) {
+#pragma unroll
+                    for (int q = 0; q < 4; ++q) ub += wq[q] * (g0 + q < nrows ? readlane(lbar, g0 + q) : 0.0f);
+                }
             }
             if (lane < NV) us[lane] = u;
+            if constexpr (TP::kTgs)   // the positions' velocity, in the dead rhs
+                if (lane < NV) sm[t.s_r + lane] = ub;
             if (lane < nrows) sm[t.s_ad + lane] = lam;           // reuse: lambda of row lane
             lam_done = true;
         }
@@ -1327,10 +1341,13 @@ MI_D void wave_artic_substep(const DevModel& m, const WaveTabs& t, const DevStat
         // sweep, so the normal's current lambda is carried in a wave-uniform value.
         const float* sJl = sm + t.s_J + (kl < nv ? kl : 0);
         const float kin = kl < nv ? 1.0f : 0.0f;
+        // TGS in u space: b0 / b1 hold the rows' separations; usum sums the sub-steps'
+        // velocities (lane = DOF; each half keeps its copy), so row r has moved by h J_r usum
+        [[maybe_unused]] float usum = 0.0f;
         auto sweeps = [&](auto ONE_, auto JL_) {
             constexpr bool ONE = decltype(ONE_)::value;
             constexpr bool JL = decltype(JL_)::value;   // J rows from LDS (one bank only)
-            for (int it = 0; it < p.iters; ++it) {
+            for (int it = 0; it < p.iters + p.viters; ++it) {
                 // opaque per sweep: stops the compiler hoisting the loop-invariant readlanes of
                 // every row out of the iteration loop (they would pin hundreds of SGPRs)
                 asm volatile("" : "+v"(b0), "+v"(b1), "+v"(ia0), "+v"(ia1), "+v"(k0), "+v"(k1),
@@ -1373,7 +1390,12 @@ MI_D void wave_artic_substep(const DevModel& m, const WaveTabs& t, const DevStat
                         if (rr + 1 < 64) jc_n = jrow(rr + 1, kind_n);
                         const float s = half_sums(jc_c * u);
                         const float jv = readlane(s, h ? 63 : 31);
-                        const float br = readlane(bb, rr), iar = readlane(ii, rr);
+                        float br = readlane(bb, rr);
+                        const float iar = readlane(ii, rr);
+                        if constexpr (TP::kTgs) {
+                            const float su = readlane(half_sums(jc_c * usum), h ? 63 : 31);
+                            br = (kind_c == 1 || kind_c == 2) ? 0.0f : row_bias(p, br + p.h * su, p.h, it < p.iters);
+                        }
                         const float l0 = readlane(h ? lam1 : lam0, rr);
                         float ln = l0 + (br - jv) * iar;
                         const bool fric = kind_c == 1 || kind_c == 2;
@@ -1395,12 +1417,16 @@ MI_D void wave_artic_substep(const DevModel& m, const WaveTabs& t, const DevStat
                     // hand u to the other half for its sub-sweep
                     if constexpr (!ONE) u = __shfl(u, kl + 32 * h, 64);
                 }
+                if constexpr (TP::kTgs)
+                    if (it < p.iters) usum += u;
             }
         };
         if (one_bank && nrows <= t.j_rows_lds) sweeps(std::true_type{}, std::true_type{});
         else if (one_bank) sweeps(std::true_type{}, std::false_type{});
         else sweeps(std::false_type{}, std::false_type{});
         if (lane < nv) us[lane] = u;
+        if constexpr (TP::kTgs)   // the positions' velocity: the sub-steps' mean
+            if (lane < nv) sm[t.s_r + lane] = usum / (float)p.iters;
         if (lane < nrows) sm[t.s_ad + lane] = lam0;          // reuse: lambda of row lane
         if (lane + 64 < nrows) sm[t.s_ad + lane + 64] = lam1;
     }
@@ -1449,9 +1475,12 @@ MI_D void wave_artic_substep(const DevModel& m, const WaveTabs& t, const DevStat
     }
     // ---- P11b: integrate; non-finite -> nan flag
     bool finite = true;
+    // TGS: positions advance with the sub-steps' mean velocity (in the dead rhs), the velocity
+    // state is the last sweep's
+    const float* up = TP::kTgs ? sm + t.s_r : us;
     if (lane < D) {
         const float v = us[nr + lane];
-        const float qn = sm[t.s_q + lane] + dt * v;
+        const float qn = sm[t.s_q + lane] + dt * up[nr + lane];
         if (store_state) {
             st.qd[sx(st, lane, i)] = v;
             st.q[sx(st, lane, i)] = qn;
@@ -1461,22 +1490,32 @@ MI_D void wave_artic_substep(const DevModel& m, const WaveTabs& t, const DevStat
     }
     if (store_state && lane < 6 * m.S) st.sens[ssx(st, lane, i)] = sm[t.s_rb + lane];
     if (nr && lane == 0) {
-        float u6[6], rp[3], rq[4];
+        float u6[6], p6[6], rp[3], rq[4];
 #pragma unroll
-        for (int k = 0; k < 6; ++k) u6[k] = us[k];
+        for (int k = 0; k < 6; ++k) { u6[k] = us[k]; p6[k] = up[k]; }
 #pragma unroll
         for (int k = 0; k < 3; ++k) rp[k] = sm[t.s_rp + k];
 #pragma unroll
         for (int k = 0; k < 4; ++k) rq[k] = sm[t.s_rp + 4 + k];
-        float* om = u6 + 3;
+        if constexpr (TP::kTgs) {   // the velocity state's angular velocity cap
+            const float wv = sqrtf(dot3(u6 + 3, u6 + 3));
+            if (wv > p.max_angvel) {
+                const float sc = p.max_angvel / wv;
+                u6[3] *= sc; u6[4] *= sc; u6[5] *= sc;
+            }
+        }
+        float* om = p6 + 3;
         float wn = sqrtf(dot3(om, om));
         if (wn > p.max_angvel) {
             const float sc = p.max_angvel / wn;
             om[0] *= sc; om[1] *= sc; om[2] *= sc;
             wn = p.max_angvel;
         }
+        if constexpr (!TP::kTgs)
 #pragma unroll
-        for (int k = 0; k < 3; ++k) rp[k] += dt * u6[k];
+            for (int k = 0; k < 6; ++k) u6[k] = p6[k];
+#pragma unroll
+        for (int k = 0; k < 3; ++k) rp[k] += dt * p6[k];
         const float th = wn * dt;
         if (th > 0.0f) {
             float sh, ch;

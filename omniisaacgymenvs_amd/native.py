@@ -18,6 +18,7 @@ LIB_PATH = os.environ.get("MI_SIM_LIB", os.path.join(_HERE, "libmi_sim.so"))
 MI_OK = 0
 MI_TASK_CARTPOLE, MI_TASK_ANT, MI_TASK_HUMANOID = 0, 1, 2
 MI_DYN_ARTICULATION, MI_DYN_CARTPOLE = 0, 1
+MI_SOLVER_PGS, MI_SOLVER_TGS = 0, 1
 MI_JOINT_HINGE, MI_JOINT_SLIDE = 0, 1
 MI_GEOM_SPHERE, MI_GEOM_CAPSULE = 0, 1
 
@@ -46,7 +47,7 @@ class MiSimParams(C.Structure):
         ("contact_offset", C.c_float), ("rest_offset", C.c_float), ("friction", C.c_float),
         ("max_depenetration_velocity", C.c_float), ("erp", C.c_float),
         ("enable_self_collisions", C.c_int32), ("max_angular_velocity", C.c_float),
-        ("angular_damping", C.c_float),
+        ("angular_damping", C.c_float), ("solver_type", C.c_int32), ("velocity_iterations", C.c_int32),
     ]
 
 

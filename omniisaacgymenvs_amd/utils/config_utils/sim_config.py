@@ -117,8 +117,18 @@ class SimConfig:
         p = N.MiSimParams()
         p.dt = float(sp["dt"])
         p.gravity[:] = [float(g) for g in sp["gravity"]]
-        p.solver_iterations = int(a["solver_position_iteration_count"]) + int(
-            a["solver_velocity_iteration_count"])
+        # physx.solver_type (cfg/config.yaml:31, default 1 = TGS): TGS takes the position and
+        # velocity iteration counts separately (position iterations are its sub-steps); PGS runs
+        # their sum as sweeps (include/mi_sim.h MI_SOLVER_*)
+        st = int(px.get("solver_type", 1))
+        if st not in (N.MI_SOLVER_PGS, N.MI_SOLVER_TGS):
+            raise ValueError(f"physx.solver_type {st}: this build implements 0 (PGS) and 1 (TGS)")
+        npos, nvel = int(a["solver_position_iteration_count"]), int(a["solver_velocity_iteration_count"])
+        p.solver_type = st
+        if st == N.MI_SOLVER_TGS:
+            p.solver_iterations, p.velocity_iterations = npos, nvel
+        else:
+            p.solver_iterations, p.velocity_iterations = npos + nvel, 0
         p.contact_offset = float(a["contact_offset"])
         p.rest_offset = float(a["rest_offset"])
         p.friction = float(sp["default_physics_material"]["dynamic_friction"])

@@ -372,7 +372,7 @@ static void cartpole_substep(const model_t* m, const mi_sim_params* p, float* q,
 /* ------------------------------------------------------------------------------------ */
 typedef struct {
     float *R, *o, *aw, *I6, *Iw, *S, *V, *A, *J, *M, *Gc, *C, *u, *rhs, *ud;
-    float *Jr, *W, *b, *lam, *Ad, *cpt, *cdir, *tmp;
+    float *Jr, *W, *b, *lam, *Ad, *cpt, *cdir, *tmp, *sep, *dsum, *ubar;
     int *rkind, *rcon, *clink, *clink2;
     int nrows, ncon;
     float margin; /* min distance of any activation decision from its threshold (test aid) */
@@ -391,6 +391,7 @@ static ws_t* ws_new(const model_t* m) {
     w->rhs = (float*)calloc(nv + 1, 4); w->ud = (float*)calloc(nv + 1, 4);
     w->Jr = (float*)calloc((size_t)R * nv + 1, 4); w->W = (float*)calloc((size_t)R * nv + 1, 4);
     w->b = (float*)calloc(R, 4); w->lam = (float*)calloc(R, 4); w->Ad = (float*)calloc(R, 4);
+    w->sep = (float*)calloc(R, 4); w->dsum = (float*)calloc(R, 4); w->ubar = (float*)calloc(nv + 1, 4);
     w->rkind = (int*)calloc(R, 4); w->rcon = (int*)calloc(R, 4);
     const int nc = m->npts + (m->self_on ? m->P : 0) + 1;   /* contact capacity */
     w->cpt = (float*)calloc((size_t)nc * 3, 4); w->clink = (int*)calloc(nc, 4);
@@ -401,7 +402,7 @@ static ws_t* ws_new(const model_t* m) {
 static void ws_free(ws_t* w) {
     void* p[] = {w->R, w->o, w->aw, w->I6, w->Iw, w->S, w->V, w->A, w->J, w->M, w->Gc, w->C, w->u,
                  w->rhs, w->ud, w->Jr, w->W, w->b, w->lam, w->Ad, w->rkind, w->rcon, w->cpt,
-                 w->clink, w->clink2, w->cdir, w->tmp};
+                 w->clink, w->clink2, w->cdir, w->tmp, w->sep, w->dsum, w->ubar};
     for (size_t i = 0; i < sizeof p / sizeof p[0]; ++i) free(p[i]);
     free(w);
 }
@@ -664,6 +665,7 @@ static void artic_substep(const model_t* m, const mi_sim_params* p, ws_t* w, flo
             w->rkind[nrows] = t;          /* 0 normal, 1/2 friction */
             w->rcon[nrows] = nrows - t;   /* index of the contact's normal row */
             w->b[nrows] = t == 0 ? bn : 0.0f;
+            w->sep[nrows] = d;
             ++nrows;
         }
         ++ncon;
@@ -708,6 +710,7 @@ static void artic_substep(const model_t* m, const mi_sim_params* p, ws_t* w, flo
                 w->rkind[nrows] = t;
                 w->rcon[nrows] = nrows - t;
                 w->b[nrows] = t == 0 ? bn : 0.0f;
+                w->sep[nrows] = d;
                 ++nrows;
             }
             ++ncon;
@@ -730,6 +733,7 @@ static void artic_substep(const model_t* m, const mi_sim_params* p, ws_t* w, flo
         float bl = d >= 0.0f ? -d / dt : -p->erp * d / dt;
         if (bl > p->max_depenetration_velocity) bl = p->max_depenetration_velocity;
         w->b[nrows] = bl;
+        w->sep[nrows] = d;
         w->rkind[nrows] = 3;
         w->rcon[nrows] = nrows;
         ++nrows;
@@ -742,9 +746,24 @@ static void artic_substep(const model_t* m, const mi_sim_params* p, ws_t* w, flo
         w->Ad[r] = a > 1e-12f ? a : 1e-12f;
         w->lam[r] = 0.0f;
     }
-    /* ---- projected Gauss-Seidel ---- */
+    /* ---- projected Gauss-Seidel sweeps (PGS: over dt; TGS: position sub-steps) ---- */
     const float mu = p->friction;
-    for (int it = 0; it < p->solver_iterations; ++it) {
+    const int tgs = p->solver_type == MI_SOLVER_TGS;
+    const int npos = p->solver_iterations, nvel = tgs ? p->velocity_iterations : 0;
+    const float h = tgs ? dt / (float)npos : dt;
+    for (int r = 0; r < nrows; ++r) w->dsum[r] = 0.0f;
+    for (int k = 0; k < nv; ++k) w->ubar[k] = 0.0f;
+    for (int it = 0; it < npos + nvel; ++it) {
+        if (tgs) {   /* this sub-step's bias from the row's current separation (friction: 0) */
+            for (int r = 0; r < nrows; ++r) {
+                if (w->rkind[r] == 1 || w->rkind[r] == 2) continue;
+                const float e = w->sep[r] + w->dsum[r];
+                float bb;
+                if (it < npos) bb = e >= 0.0f ? -e / h : -p->erp * e / h;
+                else bb = e >= 0.0f ? -e / h : 0.0f;            /* velocity iterations */
+                w->b[r] = bb > p->max_depenetration_velocity ? p->max_depenetration_velocity : bb;
+            }
+        }
         for (int r = 0; r < nrows; ++r) {
             const float* Jr = w->Jr + (size_t)r * nv;
             float jv = 0.0f;
@@ -762,6 +781,21 @@ static void artic_substep(const model_t* m, const mi_sim_params* p, ws_t* w, flo
             for (int k = 0; k < nv; ++k) u[k] += Wr[k] * dl;
             w->lam[r] = ln;
         }
+        if (tgs && it < npos) {   /* the sub-step moves the rows by h J u; positions by h u */
+            for (int r = 0; r < nrows; ++r) {
+                const float* Jr = w->Jr + (size_t)r * nv;
+                float jv = 0.0f;
+                for (int k = 0; k < nv; ++k) jv += Jr[k] * u[k];
+                w->dsum[r] += h * jv;
+            }
+            for (int k = 0; k < nv; ++k) w->ubar[k] += u[k];
+        }
+    }
+    /* the velocity the positions integrate with: the final one (PGS) or the sub-steps' mean */
+    float* ui = u;
+    if (tgs) {
+        for (int k = 0; k < nv; ++k) w->ubar[k] = w->ubar[k] / (float)npos;
+        ui = w->ubar;
     }
     /* ---- force sensors: contact wrench on the sensor link, link frame ---- */
     for (int si = 0; si < m->S; ++si) {
@@ -783,16 +817,24 @@ static void artic_substep(const model_t* m, const mi_sim_params* p, ws_t* w, flo
         m3_tvec(w->R + 9 * l, F, sens + 6 * si);
         m3_tvec(w->R + 9 * l, T, sens + 6 * si + 3);
     }
-    /* ---- integrate (semi-implicit Euler) ---- */
+    /* ---- integrate (semi-implicit Euler; TGS: positions with the sub-steps' mean velocity) ---- */
     if (m->root_free) {
-        float* om = u + 3;
+        if (tgs) {   /* the velocity state's angular velocity cap */
+            float* om = u + 3;
+            const float wn = sqrtf(dot3(om, om));
+            if (wn > p->max_angular_velocity) {
+                const float sc = p->max_angular_velocity / wn;
+                om[0] *= sc; om[1] *= sc; om[2] *= sc;
+            }
+        }
+        float* om = ui + 3;
         float wn = sqrtf(dot3(om, om));
         if (wn > p->max_angular_velocity) {
             float sc = p->max_angular_velocity / wn;
             om[0] *= sc; om[1] *= sc; om[2] *= sc;
             wn = p->max_angular_velocity;
         }
-        for (int k = 0; k < 3; ++k) rp[k] += dt * u[k];
+        for (int k = 0; k < 3; ++k) rp[k] += dt * ui[k];
         float th = wn * dt;
         if (th > 0.0f) {
             float sh = sinf(0.5f * th) / wn, ch = cosf(0.5f * th);
@@ -810,7 +852,7 @@ static void artic_substep(const model_t* m, const mi_sim_params* p, ws_t* w, flo
     }
     for (int j = 0; j < D; ++j) {
         qd[j] = u[nr + j];
-        q[j] = q[j] + dt * qd[j];
+        q[j] = q[j] + dt * ui[nr + j];
     }
 }
 

@@ -161,7 +161,8 @@ def check_pair(name, task, obs, rew, obs_ref, rew_ref, tol, margin, sens=None, p
         bad |= ~np.isclose(rew, rew_ref, rtol=tol, atol=tol)
         assert not bad.any(), f"{name}: envs {np.nonzero(bad)[0]}"
         return None
-    return parity_bounds.check(name, obs_groups(task), obs, rew, obs_ref, rew_ref, margin, sens=sens,
+    key = parity_bounds.bounds_key(name, task.get_robot().sim_params.solver_type)
+    return parity_bounds.check(key, obs_groups(task), obs, rew, obs_ref, rew_ref, margin, sens=sens,
                                pot=pot, quantiles=quantiles)
 
 
@@ -483,4 +484,54 @@ def test_returned_obs_contract(gpu, name):
         torch.cuda.synchronize()
         assert o3["obs"].data_ptr() == out[0].data_ptr() != t.obs_buf.data_ptr()
         assert torch.equal(o3["obs"], torch.clamp(t.obs_buf, -t.clip_obs, t.clip_obs))
+    env.close()
+
+
+@pytest.mark.parametrize("z,min_contacts", [(0.08, 11), (0.05, 18)])   # 33+ rows: wide; 54+ rows
+@pytest.mark.parametrize("solver", [0, 1])
+def test_wide_pgs_pair_with_empty_partner(gpu, solver, z, min_contacts):
+    """The paired kernel's wide PGS (a half with 33..64 rows) next to a partner env with no rows
+    at all: even envs lie flat on the ground (many contacts), odd envs float (no contact, no
+    limit). Both solvers; TGS must still integrate the empty partner with u-bar = u* (the wide
+    path skips an empty half). One fused step against the oracle from identical state."""
+    n = 64
+    env = make_env("Humanoid", num_envs=n, device="cuda:0", seed=9, overrides=[f"solver_type={solver}"])
+    task = env.task
+    view = task.get_robot()
+    assert view.sim_params.solver_type == solver
+    env.reset()
+    torch.cuda.synchronize()
+    pos0, _ = view.get_world_poses()
+    pos = pos0.clone()
+    s = float(np.sqrt(0.5))
+    rot = torch.tensor([[s, 0.0, s, 0.0]] * n, device="cuda:0")      # 90 deg about y: lying
+    pos[0::2, 2] = z
+    pos[1::2, 2] = 5.0
+    rot[1::2] = torch.tensor([1.0, 0.0, 0.0, 0.0], device="cuda:0")
+    view.set_world_poses(pos, rot)
+    view.set_velocities(torch.zeros((n, 6), device="cuda:0"))
+    view.set_joint_positions(torch.zeros((n, task.num_actions), device="cuda:0"))
+    view.set_joint_velocities(torch.zeros((n, task.num_actions), device="cuda:0"))
+    task.reset_buf.zero_()
+    torch.cuda.synchronize()
+    orc = oracle_twin(env, 9)
+    b = task_buffers(env)
+    acts = torch.zeros((n, task.num_actions))
+    orc.env_step(acts.numpy(), task.control_frequency_inv, b)
+    heavy = [orc.contact_count(e) for e in range(0, n, 2)]
+    assert min(heavy) >= min_contacts, heavy        # >= 33 rows: past the narrow path
+    assert max(orc.contact_count(e) for e in range(1, n, 2)) == 0
+    sync_oracle(env, orc)
+    b = task_buffers(env)
+    sens = oracle_sens(env, 9, acts.numpy(), b)
+    obs_dict, rew, resets, _ = env.step(acts.to("cuda:0"))
+    torch.cuda.synchronize()
+    orc.env_step(acts.numpy(), task.control_frequency_inv, b)
+    check_pair("Humanoid", task, obs_dict["obs"].cpu().numpy(), rew.cpu().numpy(), b["obs"], b["rew"],
+               2e-3, orc.decision_margin(), sens=sens, pot=pot_mag(b), quantiles=False)
+    assert np.array_equal(resets.cpu().numpy(), b["reset"])
+    p_dev, _ = view.get_world_poses()
+    p_orc = orc.root_state()[0]
+    np.testing.assert_allclose(p_dev.cpu().numpy()[1::2], p_orc[1::2], rtol=1e-5, atol=1e-5)
+    orc.close()
     env.close()

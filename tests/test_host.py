@@ -111,7 +111,7 @@ def test_library_exports_every_header_symbol():
     for s in syms:
         assert hasattr(lib, s), s
     assert set(syms) == set(N.EXPORTED_SYMBOLS)
-    assert lib.mi_abi_version() == 3
+    assert lib.mi_abi_version() == 4
 
 
 def test_rl_library_exports_every_header_symbol():

@@ -81,10 +81,11 @@ def test_energy_drift_bounded():
         assert abs(sim.energy(e) - e0[e]) < 0.02 * max(1.0, abs(e0[e]))
 
 
-def test_joint_limits_hold():
+@pytest.mark.parametrize("solver", [0, 1])
+def test_joint_limits_hold(solver):
     m = load_robot("Humanoid")
     n = 8
-    sim = OracleSim(m, sim_params(), n, np.zeros((n, 3), np.float32))
+    sim = OracleSim(m, sim_params(solver_type=solver), n, np.zeros((n, 3), np.float32))
     sim.set_root_state(np.tile([0, 0, 1.34], (n, 1)).astype(np.float32),
                        np.tile([1, 0, 0, 0], (n, 1)).astype(np.float32), np.zeros((n, 6), np.float32))
     sim.set_dof_state(np.zeros((n, 21), np.float32), np.zeros((n, 21), np.float32))
@@ -119,10 +120,11 @@ def test_articulation_matches_analytic_cartpole():
     np.testing.assert_allclose(outs[0][1], outs[1][1], rtol=1e-3, atol=1e-3)
 
 
-def test_humanoid_settles_without_nan():
+@pytest.mark.parametrize("solver", [0, 1])
+def test_humanoid_settles_without_nan(solver):
     m = load_robot("Humanoid")
     n = 4
-    sim = OracleSim(m, sim_params(), n, np.zeros((n, 3), np.float32))
+    sim = OracleSim(m, sim_params(solver_type=solver), n, np.zeros((n, 3), np.float32))
     sim.set_root_state(np.tile([0, 0, 1.34], (n, 1)).astype(np.float32),
                        np.tile([1, 0, 0, 0], (n, 1)).astype(np.float32), np.zeros((n, 6), np.float32))
     sim.set_dof_state(np.zeros((n, 21), np.float32), np.zeros((n, 21), np.float32))
@@ -137,7 +139,8 @@ def test_humanoid_settles_without_nan():
     assert np.isfinite(s).all()
 
 
-def test_self_collision_limits_penetration():
+@pytest.mark.parametrize("solver", [0, 1])
+def test_self_collision_limits_penetration(solver):
     """Humanoid self-collision (Humanoid.yaml:80): with the pair contacts on, limbs stay
     (nearly) apart under random actions; with them off they pass through each other."""
     from oracle.oracle import OracleSim, make_buffers
@@ -149,7 +152,8 @@ def test_self_collision_limits_penetration():
     worst = {}
     for esc in (1, 0):
         n = 32
-        orc = OracleSim(m, sim_params(enable_self_collisions=esc), n, np.zeros((n, 3), np.float32), seed=3)
+        orc = OracleSim(m, sim_params(enable_self_collisions=esc, solver_type=solver), n,
+                        np.zeros((n, 3), np.float32), seed=3)
         tp, _, keep = task_params_from_cfg("Humanoid")
         orc.configure(tp, keep=keep)
         b = make_buffers(n, tp.num_obs, tp.num_actions)
@@ -193,3 +197,50 @@ def test_link_angular_damping_decays_spin(tmp_path, damp):
     _, _, vel = sim.root_state()
     np.testing.assert_allclose(vel[0, 3:], w0 * (1.0 - damp * dt) ** n, rtol=2e-4, atol=1e-6)
     np.testing.assert_allclose(vel[0, :3], v0, rtol=1e-5, atol=1e-6)
+
+
+def test_tgs_without_constraints_equals_pgs():
+    """No constraint rows (free flight): every TGS sub-step sees the same velocity u*, so the
+    sub-steps' mean is u* and TGS integrates exactly as PGS (include/mi_sim.h MI_SOLVER_TGS)."""
+    m = load_robot("Humanoid")
+    n = 4
+    rng = np.random.default_rng(2)
+    states = []
+    for solver in (0, 1):
+        sim = OracleSim(m, sim_params(gravity=(0.0, 0.0, -9.81), solver_type=solver), n,
+                        np.zeros((n, 3), np.float32))
+        sim.set_root_state(np.tile([0, 0, 50.0], (n, 1)).astype(np.float32),
+                           np.tile([1, 0, 0, 0], (n, 1)).astype(np.float32),
+                           rng.uniform(-1, 1, (n, 6)).astype(np.float32) * 0 + 0.3)
+        sim.set_dof_state(np.zeros((n, 21), np.float32), np.full((n, 21), 0.05, np.float32))
+        sim.set_efforts(np.full((n, 21), 1.0, np.float32))
+        for _ in range(3):        # short: no joint reaches a limit (no limit rows either)
+            sim.step(2)
+        assert sim.contact_count(0) == 0
+        states.append((sim.root_state(), sim.dof_state()))
+    for a, b in zip(states[0][0] + states[0][1], states[1][0] + states[1][1]):
+        assert np.array_equal(a, b)
+
+
+def test_tgs_resolves_penetration_within_the_substep():
+    """A sphere placed 2 cm into the ground: TGS's sub-steps re-evaluate the separation, so one
+    substep pushes it out by more than PGS's single Baumgarte correction (erp 0.2) does, and
+    neither overshoots above the rest offset by more than the max depenetration allows."""
+    import os
+    import tempfile
+    xml = SPHERE_XML
+    with tempfile.TemporaryDirectory() as d:
+        path = os.path.join(d, "ball.xml")
+        open(path, "w").write(xml)
+        m = compile_mjcf(path)
+    heights = {}
+    for solver in (0, 1):
+        sim = OracleSim(m, sim_params(gravity=(0.0, 0.0, 0.0), solver_type=solver), 1, np.zeros((1, 3), np.float32))
+        sim.set_root_state(np.array([[0, 0, 0.3 + 0.001 - 0.02]], np.float32), np.array([[1, 0, 0, 0]], np.float32),
+                           np.zeros((1, 6), np.float32))
+        sim.step(1)
+        heights[solver] = float(sim.root_state()[0][0, 2])
+    pen0 = 0.02
+    moved = {k: v - (0.3 + 0.001 - pen0) for k, v in heights.items()}
+    assert moved[0] > 0 and moved[1] > moved[0], moved
+    assert heights[1] <= 0.3 + 0.001 + 1e-4, heights

@@ -196,9 +196,9 @@ def test_ppo_learns_cartpole(gpu):
 def test_ppo_learns_ant_on_reference_schedule(gpu):
     """AntPPO.yaml as shipped (4096 envs, horizon 16, minibatch 32768, 4 mini-epochs, adaptive
     LR) through the learner and the fused Ant step: after 100 epochs the mean episode reward
-    must have grown from the first finished episodes' (8.1 at epoch 5) to >= 1000. The committed
-    curve (profiles/r04/train_curve_ant.jsonl, same seed) reads 2199 at epoch 101 and peaks at
-    5901 (epoch 313); the bound leaves room for GEMM / box differences."""
+    must be >= 1000 and >= 20x the first finished episodes'. Under PGS the first episodes read
+    8.1 and epoch 101 2199 (profiles/r04/train_curve_ant.jsonl); under TGS (the default since
+    round 5) 48.7-50.6 and 1870-2059 (two runs); the bound leaves room for GEMM / box drift."""
     from omniisaacgymenvs_amd.rlg.a2c_continuous import A2CAgent
     from omniisaacgymenvs_amd.utils.rlgames.rlgames_utils import RLGPUEnv, register_env
     from omniisaacgymenvs_amd.utils.task_util import make_env
@@ -218,7 +218,7 @@ def test_ppo_learns_ant_on_reference_schedule(gpu):
         if first is None and st["games"] > 0:
             first = st["mean_rewards"]
     assert ag.graph is not None and ag.upd_graphs
-    assert st["mean_rewards"] >= 1000.0 and st["mean_rewards"] > 50.0 * max(first, 1.0), (first, st["mean_rewards"])
+    assert st["mean_rewards"] >= 1000.0 and st["mean_rewards"] > 20.0 * max(first, 1.0), (first, st["mean_rewards"])
     env.close()
 
 

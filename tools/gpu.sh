@@ -102,7 +102,7 @@ recipe() {
       run calw_$N 60 $RP --pmc WRITE_SIZE --kernel-trace -d gpurun_out/calw_$N -o run -- tools/fetch_calib $N 6
     done ;;
   pstats)
-    for T in ${TASKS:-Humanoid Ant}; do run pstats_${T}_$TAG 300 python -u tools/parity_stats.py $T 4096 4; done ;;
+    for T in ${TASKS:-Humanoid Ant}; do run pstats_${T}_$TAG 300 python -u tools/parity_stats.py $T 4096 4 ${SOLVER:-config}; done ;;
   freerun)
     for T in Humanoid Ant Cartpole; do run free_run_${T}_$TAG 300 python -u tools/free_run.py $T 4096; done ;;
   stamps)
@@ -110,7 +110,7 @@ recipe() {
     for T in ${TASKS:-Humanoid Ant}; do run stamps_${T}_$TAG 150 python -u tools/phase_stamps.py $T 4096; done ;;
   tail)   # slowest-wave phase stamps of the paired kernel
     stamps_lib
-    for T in ${TASKS:-Humanoid}; do run tail_${T}_$TAG 150 python -u tools/pair_tail.py $T 4096 3; done ;;
+    for T in ${TASKS:-Humanoid}; do run tail_${T}_$TAG 150 python -u tools/pair_tail.py $T 4096 3 ${SOLVER:-config}; done ;;
   patha)
     run path_a 200 python -u tools/path_a_timing.py ;;
   pathaprof)   # kernel trace of path (A): every backend launch and its duration

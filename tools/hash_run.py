@@ -4,7 +4,7 @@ Ant (4096 envs, fixed seeds and actions), SHA-256 of every returned obs / reward
 per build (MI_SIM_LIB=<path> selects the library) and compare the printed HASH lines; a change
 that only moves data (e.g. a different cross-lane broadcast) must leave the hash unchanged.
 
-usage: [MI_SIM_LIB=...] python tools/hash_run.py"""
+usage: [MI_SIM_LIB=...] python tools/hash_run.py [pgs|tgs]   (solver override; default: the config's)"""
 import hashlib
 import os
 import sys
@@ -18,7 +18,8 @@ from omniisaacgymenvs_amd.utils.task_util import make_env  # noqa: E402
 def main():
     h = hashlib.sha256()
     for task in ("Humanoid", "Ant"):
-        env = make_env(task, num_envs=4096, device="cuda:0", seed=3)
+        ov = {"pgs": ["solver_type=0"], "tgs": ["solver_type=1"]}.get(sys.argv[1] if len(sys.argv) > 1 else "", [])
+        env = make_env(task, num_envs=4096, device="cuda:0", seed=3, overrides=ov)
         env.reset()
         g = torch.Generator(device="cuda:0").manual_seed(0)
         for _ in range(40):

@@ -80,6 +80,10 @@ def run(task: str):
     meta = {"task": task, "num_envs": N_ENVS, "seed": SEED, "steps": STEPS + 1, "substeps": 2,
             "enable_self_collisions": int(sp.enable_self_collisions),
             "contact_offset": float(sp.contact_offset),
+            # the contact / limit solver the fixture was stepped with (include/mi_sim.h)
+            "solver_type": int(sp.solver_type), "solver": "TGS" if sp.solver_type == 1 else "PGS",
+            "solver_iterations": int(sp.solver_iterations),
+            "velocity_iterations": int(sp.velocity_iterations),
             "model_sha256": sha256(os.path.join(ROOT, "omniisaacgymenvs_amd", "robots", "assets",
                                                 ASSETS[task])),
             "task_cfg_sha256": sha256(os.path.join(ROOT, "omniisaacgymenvs_amd", "cfg", "task",

@@ -34,7 +34,9 @@ def main():
     task = sys.argv[1] if len(sys.argv) > 1 else "Humanoid"
     n = int(sys.argv[2]) if len(sys.argv) > 2 else 4096
     launches = int(sys.argv[3]) if len(sys.argv) > 3 else 1
-    env = make_env(task, num_envs=n, device="cuda:0", seed=1)
+    solver = sys.argv[4] if len(sys.argv) > 4 else "config"
+    ov = {"pgs": ["solver_type=0"], "tgs": ["solver_type=1"]}.get(solver, [])
+    env = make_env(task, num_envs=n, device="cuda:0", seed=1, overrides=ov)
     lib = N.lib()
     lib.mi_debug_stamps_raw.argtypes = [C.POINTER(C.c_ulonglong), C.c_int]
     pair = env.task.get_robot().sim_kernel_path()[0] == 2

@@ -27,7 +27,9 @@ def main():
     task_name = sys.argv[1] if len(sys.argv) > 1 else "Humanoid"
     n = int(sys.argv[2]) if len(sys.argv) > 2 else 4096
     steps = int(sys.argv[3]) if len(sys.argv) > 3 else 4
-    env = make_env(task_name, num_envs=n, device="cuda:0", seed=3)
+    solver = sys.argv[4] if len(sys.argv) > 4 else "config"
+    env = make_env(task_name, num_envs=n, device="cuda:0", seed=3,
+                   overrides={"pgs": ["solver_type=0"], "tgs": ["solver_type=1"]}.get(solver, []))
     task = env.task
     view = task.get_robot()
 
@@ -82,7 +84,7 @@ def main():
         errs.append(e)
         margins.append(orc.decision_margin().copy())
         if task_name != "Cartpole":   # the bounded check of tests/parity_bounds.py, reported per step
-            ev = PB.evaluate(task_name, groups, o["obs"].cpu().numpy(), r.cpu().numpy(), b["obs"], b["rew"],
+            ev = PB.evaluate(PB.bounds_key(task_name, env.task.get_robot().sim_params.solver_type), groups, o["obs"].cpu().numpy(), r.cpu().numpy(), b["obs"], b["rew"],
                              margins[-1], sens=senss[-1],
                              pot=np.maximum(np.abs(b["pot"]), np.abs(b["prev"])))
             need_b = np.concatenate([ev["bound"][g][ev["needed_widening"][g]] for g in ev["err"]])
@@ -128,7 +130,7 @@ def main():
             "max_frac_per_step": max(w["frac"] for w in widen_steps),
             "widest_bound_applied": max(w["widest_bound_applied"] for w in widen_steps),
             "over_bound_far_total": sum(w["over_bound_far"] for w in widen_steps),
-            "far_tol": PB.FAR_TOL[task_name]}
+            "far_tol": PB.FAR_TOL[PB.bounds_key(task_name, env.task.get_robot().sim_params.solver_type)]}
     for g in groups:
         rel = np.concatenate(grel[g])
         mag = np.concatenate(gmag[g])
