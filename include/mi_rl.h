@@ -15,6 +15,8 @@
  *   mi_rl_policy_step  — the rollout's whole policy evaluation (normalisation, MLP, heads,
  *                        sampling, action rescale) as one f32-MFMA launch
  *   mi_rl_record_step  — the rollout's per-step bookkeeping after env.step
+ *   mi_rl_adam_step    — rl_games a2c_common trancate_gradients_and_step (GradScaler unscale,
+ *                        grad-norm clip, Adam, scaler update) + the adaptive LR, two launches
  * The training minibatch GEMMs stay in hipBLASLt (torch.nn.Linear, autograd).
  *
  * Conventions: as mi_sim.h — 0 on success or a negative MI_E_* code (mi_rl_last_error());
@@ -29,7 +31,7 @@
 extern "C" {
 #endif
 
-#define MI_RL_ABI_VERSION 1
+#define MI_RL_ABI_VERSION 2
 
 int32_t mi_rl_abi_version(void);
 /* SHA-256 (hex) of the sources this library was compiled from (csrc/mi_rl.hip, the csrc .hpp headers,
@@ -132,6 +134,47 @@ int32_t mi_rl_record_step(const float* obs_in, int32_t num_obs, const float* rew
                           float* obs_state, float* rewards_out, float* dones_state,
                           float* cur_rewards, float* cur_lengths, double* episode_sums,
                           double* scratch, uint32_t* ticket, void* stream);
+
+/* The learner's optimizer step over its flat fp32 parameter buffer, as rl-games a2c_common
+ * (rl_games 1.5.2 calc_gradients -> trancate_gradients_and_step with truncate_grads: True and
+ * mixed precision) runs it through torch: GradScaler.unscale_, clip_grad_norm_(grad_norm),
+ * GradScaler.step(Adam), GradScaler.update, then the legacy adaptive LR on the minibatch KL
+ * (AdaptiveScheduler.update). Two launches, no host synchronisation (graph-capturable):
+ *   pass 1: g = grads * (1 / scale); found_inf = any g non-finite, or any f16-formed scaled
+ *           gradient beyond f16 range (only with a scaler, as GradScaler's); norm = ||g||_2 (f64 sums of
+ *           f32 squares, per-block partials added in block order by the last block);
+ *           coef = max_grad_norm > 0 ? min(max_grad_norm / (norm + 1e-6), 1) : 1
+ *   pass 2: unless found_inf, with t = *step + 1 (torch Adam, weight_decay as L2):
+ *             g' = (g * coef) + weight_decay * p
+ *             m = beta1 m + (1 - beta1) g';  v = beta2 v + (1 - beta2) g'^2
+ *             p -= (lr / (1 - beta1^t)) * m / (sqrt(v) / sqrt(1 - beta2^t) + eps)
+ *           then (the last block, after every block has read them): *step = t unless found_inf;
+ *           GradScaler.update on *scale / *growth_tracker (scale == NULL: no scaler); and with
+ *           adaptive_lr, lr <- lr / 1.5 (>= min_lr) if *kl > 2 kl_threshold, lr * 1.5
+ *           (<= max_lr) if *kl < kl_threshold / 2.
+ * params / grads / exp_avg / exp_avg_sq: n f32 (grads are read, not modified); step, lr, scale:
+ * device f32 scalars; growth_tracker: device int32; kl: device f32 (NULL: no LR update).
+ * scratch: f64, at least 1028 entries; tickets: 5 device uint32 — [0] and [4] launch tickets, 0
+ * before the first call and left 0 (graph-capturable); [1] counts the skipped (found_inf) steps,
+ * [2] holds the lowest offending flat index of the latest one, [3] is 0xFFFFFFFF between calls. */
+typedef struct {
+    float beta1, beta2, eps, weight_decay;
+    float max_grad_norm;               /* <= 0: no clipping */
+    float growth_factor, backoff_factor;
+    int32_t growth_interval;
+    int32_t adaptive_lr;
+    float kl_threshold, min_lr, max_lr;
+    /* > 0: grads[i] for i >= f16_begin were formed in f16 under autocast by the reference (its
+     * Linear weight / bias gradients); a scaled value with |g| >= f16_overflow (65520: rounds to
+     * f16 inf) makes found_inf, as the reference's f16 gradient would be inf */
+    float f16_overflow;
+    int64_t f16_begin;
+} mi_rl_adam_cfg;
+
+int32_t mi_rl_adam_step(const mi_rl_adam_cfg* cfg, float* params, const float* grads, float* exp_avg,
+                        float* exp_avg_sq, int64_t n, float* step, float* lr, float* scale,
+                        int32_t* growth_tracker, const float* kl, double* scratch, int64_t scratch_len,
+                        uint32_t* tickets, void* stream);
 
 #ifdef __cplusplus
 }

@@ -573,6 +573,141 @@ __global__ __launch_bounds__(kRecBlock) void k_record_step(
 }
 }  // namespace
 
+// ---------------------------------------------------------------------------------------
+// The learner's optimizer step (include/mi_rl.h mi_rl_adam_step): GradScaler.unscale_ +
+// clip_grad_norm_ + Adam + GradScaler.update + the adaptive LR over the flat parameter buffer.
+// Pass 1 reduces the squared unscaled gradient (f64 per block, blocks added in order by the
+// last one, which leaves coef / found_inf / inv_scale in the scratch tail); pass 2 applies Adam
+// and its last block updates step, scale, growth tracker and LR after every block has read them.
+// ---------------------------------------------------------------------------------------
+namespace {
+constexpr int kAdamBlock = 256, kAdamMaxBlocks = 1024;
+
+__device__ double block_sum_f64(double v, double* red) {
+    for (int o = 32; o > 0; o >>= 1) v += __shfl_down(v, o);
+    const int w = threadIdx.x >> 6, l = threadIdx.x & 63;
+    if (l == 0) red[w] = v;
+    __syncthreads();
+    double t = 0.0;
+    if (threadIdx.x == 0)
+        for (int k = 0; k < (int)(blockDim.x >> 6); ++k) t += red[k];
+    return t;   // valid on thread 0
+}
+
+__global__ __launch_bounds__(kAdamBlock) void k_adam_norm(const float* __restrict__ g, int64_t n,
+                                                          const float* __restrict__ scale,
+                                                          float max_norm, float f16_overflow, int64_t f16_begin,
+                                                          double* __restrict__ scratch,
+                                                          uint32_t* __restrict__ ticket) {
+    __shared__ double red[kAdamBlock / 64];
+    __shared__ bool last;
+    // torch's unscale_: inv_scale = 1 / scale in f64, rounded to f32
+    const float inv = scale ? (float)(1.0 / (double)*scale) : 1.0f;
+    double acc = 0.0;
+    bool bad = false;
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+        const float gi = g[i], x = gi * inv;
+        const bool b = !isfinite(x) || (f16_overflow > 0.0f && i >= f16_begin && fabsf(gi) >= f16_overflow);
+        if (b && scale) atomicMin(ticket + 3, (uint32_t)(i < 0xFFFFFFFFll ? i : 0xFFFFFFFEll));
+        bad |= b;
+        acc += (double)x * (double)x;
+    }
+    const int anybad = __syncthreads_or(bad);
+    const double t = block_sum_f64(acc, red);
+    if (threadIdx.x == 0) {
+        scratch[blockIdx.x] = anybad ? __builtin_nan("") : t;
+        __threadfence();
+        last = atomicAdd(ticket, 1u) == gridDim.x - 1;
+    }
+    __syncthreads();
+    if (last && threadIdx.x == 0) {
+        __threadfence();
+        double tot = 0.0;
+        for (unsigned b = 0; b < gridDim.x; ++b) tot += ((volatile double*)scratch)[b];
+        // found_inf is GradScaler's: without a scaler torch steps whatever the gradients hold
+        const bool found = scale && !isfinite(tot);
+        // clip_grad_norm_: total norm in f32, coef = max_norm / (norm + 1e-6) clamped to 1
+        const float norm = (float)sqrt(tot);
+        const float coef = max_norm > 0.0f ? fminf(max_norm / (norm + 1e-6f), 1.0f) : 1.0f;
+        scratch[kAdamMaxBlocks + 0] = coef;
+        scratch[kAdamMaxBlocks + 1] = found ? 1.0 : 0.0;
+        scratch[kAdamMaxBlocks + 2] = inv;
+        scratch[kAdamMaxBlocks + 3] = norm;
+        if (found) {   // skipped-step statistics: count, first offending index of the latest
+            ticket[1] += 1u;
+            ticket[2] = ticket[3];
+        }
+        ticket[3] = 0xFFFFFFFFu;
+        *ticket = 0u;
+    }
+}
+
+__global__ __launch_bounds__(kAdamBlock) void k_adam_apply(mi_rl_adam_cfg c, float* __restrict__ p,
+                                                           const float* __restrict__ g,
+                                                           float* __restrict__ m, float* __restrict__ v,
+                                                           int64_t n, float* __restrict__ step,
+                                                           float* __restrict__ lr, float* __restrict__ scale,
+                                                           int32_t* __restrict__ tracker,
+                                                           const float* __restrict__ kl,
+                                                           const double* __restrict__ scratch,
+                                                           uint32_t* __restrict__ ticket) {
+    __shared__ bool last;
+    const bool found = scratch[kAdamMaxBlocks + 1] != 0.0;
+    const float s_old = *step;
+    if (!found) {
+        const float coef = (float)scratch[kAdamMaxBlocks + 0], inv = (float)scratch[kAdamMaxBlocks + 2];
+        const float t = s_old + 1.0f;
+        const float bc1 = 1.0f - powf(c.beta1, t), bc2 = 1.0f - powf(c.beta2, t);
+        const float step_size = *lr / bc1, bc2s = sqrtf(bc2);
+        for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+            float gi = (g[i] * inv) * coef;          // unscale_, then the clip's multiply
+            float pi = p[i];
+            if (c.weight_decay != 0.0f) gi = gi + c.weight_decay * pi;
+            const float mi = c.beta1 * m[i] + (1.0f - c.beta1) * gi;
+            const float vi = c.beta2 * v[i] + (1.0f - c.beta2) * gi * gi;
+            const float denom = sqrtf(vi) / bc2s + c.eps;
+            pi = pi - step_size * mi / denom;
+            m[i] = mi;
+            v[i] = vi;
+            p[i] = pi;
+        }
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        __threadfence();
+        last = atomicAdd(ticket, 1u) == gridDim.x - 1;
+    }
+    __syncthreads();
+    if (last && threadIdx.x == 0) {
+        __threadfence();
+        if (!found) *step = s_old + 1.0f;
+        if (scale) {   // GradScaler.update (torch._amp_update_scale_)
+            if (found) {
+                *scale = *scale * c.backoff_factor;
+                *tracker = 0;
+            } else {
+                const int32_t tr = *tracker + 1;
+                if (tr == c.growth_interval) {
+                    const float grown = *scale * c.growth_factor;
+                    if (isfinite(grown)) *scale = grown;
+                    *tracker = 0;
+                } else {
+                    *tracker = tr;
+                }
+            }
+        }
+        if (c.adaptive_lr && kl) {   // a2c_continuous _lr_update_device (legacy AdaptiveScheduler)
+            const float k = *kl, l0 = *lr;
+            const float down = fmaxf(l0 / 1.5f, c.min_lr);
+            const float l1 = k > 2.0f * c.kl_threshold ? down : l0;
+            const float up = fminf(l1 * 1.5f, c.max_lr);
+            *lr = k < 0.5f * c.kl_threshold ? up : l1;
+        }
+        *ticket = 0u;
+    }
+}
+}  // namespace
+
 extern "C" {
 
 int32_t mi_rl_abi_version(void) { return MI_RL_ABI_VERSION; }
@@ -705,6 +840,27 @@ int32_t mi_rl_record_step(const float* obs_in, int32_t num_obs, const float* rew
                        rewards, dones, num_envs, reward_scale, obs_state, rewards_out, dones_state,
                        cur_rewards, cur_lengths, episode_sums, scratch, ticket, nb_env, vec4);
     return launch_check("mi_rl_record_step");
+}
+
+int32_t mi_rl_adam_step(const mi_rl_adam_cfg* cfg, float* params, const float* grads, float* exp_avg,
+                        float* exp_avg_sq, int64_t n, float* step, float* lr, float* scale,
+                        int32_t* growth_tracker, const float* kl, double* scratch, int64_t scratch_len,
+                        uint32_t* tickets, void* stream) {
+    if (!cfg || !params || !grads || !exp_avg || !exp_avg_sq || !step || !lr || !scratch || !tickets)
+        return fail(kNull, "mi_rl_adam_step: null buffer");
+    if (scale && !growth_tracker) return fail(kNull, "mi_rl_adam_step: scale without growth tracker");
+    if (n <= 0) return fail(kShape, "mi_rl_adam_step: n=%lld", (long long)n);
+    if (scratch_len < kAdamMaxBlocks + 4)
+        return fail(kShape, "mi_rl_adam_step: scratch %lld < %d doubles", (long long)scratch_len, kAdamMaxBlocks + 4);
+    int nb = (int)((n + kAdamBlock * 4 - 1) / (kAdamBlock * 4));
+    nb = nb < 1 ? 1 : (nb > kAdamMaxBlocks ? kAdamMaxBlocks : nb);
+    hipLaunchKernelGGL(k_adam_norm, dim3(nb), dim3(kAdamBlock), 0, (hipStream_t)stream, grads, n, scale,
+                       cfg->max_grad_norm, scale ? cfg->f16_overflow : 0.0f, cfg->f16_begin, scratch, tickets);
+    int32_t rc = launch_check("mi_rl_adam_step (norm)");
+    if (rc) return rc;
+    hipLaunchKernelGGL(k_adam_apply, dim3(nb), dim3(kAdamBlock), 0, (hipStream_t)stream, *cfg, params, grads,
+                       exp_avg, exp_avg_sq, n, step, lr, scale, growth_tracker, kl, scratch, tickets + 4);
+    return launch_check("mi_rl_adam_step (apply)");
 }
 
 }  // extern "C"

@@ -215,6 +215,20 @@ class A2CAgent:
                 if isinstance(m, RunningMeanStd):
                     m.all_reduce = True
         wd = float(cfg.get("weight_decay", 0.0))
+        self._flat_params = None
+        if self.device.type == "cuda":
+            # every parameter in one flat f32 buffer (before the optimizer and the fused policy
+            # take their storage): the fused optimizer step runs over it, and under mixed
+            # precision its fp16 copy (one cast launch per minibatch) feeds the minibatch GEMMs
+            self._flat_params = ops.flatten_parameters(self.model.parameters())
+        fused_opt = (self._flat_params is not None
+                     and bool(cfg.get("fused_optimizer", os.environ.get("MI_RL_FUSED_OPT", "1") != "0")))
+        # the shadow weights' gradients are f32 sums; only the fused optimizer step reproduces
+        # the f16 overflow of the reference's autocast gradients (GradScaler's skipped steps)
+        self._shadow = (fused_opt and self.mixed_precision
+                        and bool(cfg.get("shadow_weights", os.environ.get("MI_RL_SHADOW", "1") != "0")))
+        if self._shadow:
+            self.model.a2c_network.shadow_weights(torch.float16, self._flat_params)
         if self.device.type == "cuda":
             # LR lives on the device and the legacy adaptive schedule updates it there (no
             # kl.item() per minibatch); fused Adam takes the tensor LR and GradScaler's
@@ -229,6 +243,18 @@ class A2CAgent:
         self.scaler = torch.amp.GradScaler("cuda", enabled=self.mixed_precision)
         if self.mixed_precision:     # materialise the device scale now (the fused loss reads it)
             self.scaler.scale(torch.zeros((), device=self.device))
+        # GradScaler unscale + grad-norm clip + Adam + scaler update + adaptive LR as two
+        # launches over the flat buffer (mi_rl_adam_step) instead of ~20 torch kernels
+        self.fused_opt = None
+        if fused_opt:
+            f16_begin = None
+            if self._shadow:   # the Linear parameters follow the log-std in parameters() order
+                net = self.model.a2c_network
+                f16_begin = min((p.data_ptr() - self._flat_params.data_ptr()) // 4
+                                for m in net._linears() for p in (m.weight, m.bias))
+            self.fused_opt = ops.FusedAdamStep(self.model.parameters(), self._flat_params, self.optimizer,
+                                               self.scaler, self.lr_t, self.grad_norm if self.truncate_grads else 0.0,
+                                               self.scheduler, f16_begin)
         # loss + head gradients as one HIP launch (mi_rl_ppo_loss); needs the fixed log-std head
         self.fused_loss = (self.device.type == "cuda" and bool(cfg.get("fused_loss", True))
                            and self.model.a2c_network.fixed_sigma)
@@ -532,6 +558,14 @@ class A2CAgent:
     def _mb_apply(self, i: int) -> None:
         """Second half: (data-parallel: the all-reduced flat buffer / world back into p.grad and
         the KL) GradScaler + Adam step, adaptive LR on the (averaged) KL."""
+        if self.fused_opt is not None:     # one flat gradient buffer in, two launches
+            if self.dp:
+                self._flat.mul_(1.0 / self.world)
+                self._mb_out[i, 3].copy_(self._flat[self.fused_opt.n])
+                self.fused_opt.step(self._flat, kl=self._mb_out[i, 3])
+            else:
+                self.fused_opt.step(None, kl=self._mb_out[i, 3])
+            return
         if self.dp:
             self._flat.mul_(1.0 / self.world)
             o = 0
@@ -580,6 +614,9 @@ class A2CAgent:
         self._mb_apply(i)
 
     def _optimizer_step(self) -> None:
+        if self.fused_opt is not None:
+            self.fused_opt.step()          # no KL here: the LR stays (as below)
+            return
         if self.truncate_grads:
             self.scaler.unscale_(self.optimizer)
             nn.utils.clip_grad_norm_(self.model.parameters(), self.grad_norm)
@@ -792,6 +829,8 @@ class A2CAgent:
         self.last_lr = float(ck.get("last_lr", self.last_lr))
         if "optimizer" in ck:
             self.optimizer.load_state_dict(ck["optimizer"])
+            if self.fused_opt is not None:
+                self.fused_opt.bind()      # the restored moments into the flat buffers
         if "scaler" in ck:
             self.scaler.load_state_dict(ck["scaler"])
         self.update_lr(self.last_lr)   # re-binds the device LR tensor to the param groups

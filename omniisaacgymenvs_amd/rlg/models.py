@@ -74,10 +74,52 @@ class _LinearSplitK(torch.autograd.Function):
         return gx, gw, gb, None
 
 
-def linear_train(x: torch.Tensor, layer: nn.Linear, splits: int = 32) -> torch.Tensor:
+class _LinearSplitKShadow(torch.autograd.Function):
+    """_LinearSplitK on a pre-cast low-precision copy (w16, b16) of the fp32 master weights
+    (w, b): the GEMMs run in the copy's dtype, the weight / bias gradients are summed in fp32
+    straight into the masters' dtype. Under autocast this replaces a cast launch per weight and
+    bias in the forward and another per gradient in the backward (one copy of the whole flat
+    weight buffer per minibatch instead: ActorCriticMLP.shadow_weights)."""
+
+    @staticmethod
+    def forward(ctx, x, w, b, w16, b16, splits: int):
+        ctx.save_for_backward(x, w16)
+        ctx.splits = splits
+        return torch.nn.functional.linear(x, w16, b16)
+
+    @staticmethod
+    def backward(ctx, gy):
+        x, w16 = ctx.saved_tensors
+        S = ctx.splits
+        gx = gy @ w16 if ctx.needs_input_grad[0] else None
+        K, O = x.shape[0], gy.shape[1]
+        split = S > 1 and K % S == 0
+        f32 = torch.float32
+        if split:
+            gys = gy.reshape(S, K // S, O)
+            gw = torch.bmm(gys.transpose(1, 2), x.reshape(S, K // S, -1)).sum(0, dtype=f32)
+        else:
+            gw = (gy.t() @ x).to(f32)
+        if split and gy.is_cuda:
+            # every width as a split-K GEMM against ones: torch's column reductions over the
+            # 32768 rows take multi-block (global staging) paths that, replayed from the update
+            # graph, now and then returned overflowing sums for the 100-wide layer (GradScaler
+            # skips seen by mi_rl_adam_step's counters; the eager update had none)
+            gb = torch.bmm(_ones(S, K // S, gy), gys).sum(0, dtype=f32).reshape(O)
+        else:
+            gb = gy.sum(0, dtype=f32)
+        return gx, gw, gb, None, None, None
+
+
+def linear_train(x: torch.Tensor, layer: nn.Linear, splits: int = 32, shadow=None) -> torch.Tensor:
     """nn.Linear for the learner's minibatch forward (autocast-aware: runs in the autocast dtype
-    when autocast is on, as nn.Linear would), with the split-K weight gradient."""
+    when autocast is on, as nn.Linear would), with the split-K weight gradient. shadow: the
+    layer's (w16, b16) views of ActorCriticMLP's refreshed low-precision weight copy."""
     w, b = layer.weight, layer.bias
+    if shadow is not None:
+        w16, b16 = shadow
+        with torch.autocast(device_type=x.device.type, enabled=False):
+            return _LinearSplitKShadow.apply(x.to(w16.dtype), w, b, w16, b16, splits)
     if torch.is_autocast_enabled(x.device.type):
         dt = torch.get_autocast_dtype(x.device.type)
         x, w = x.to(dt), w.to(dt)
@@ -185,12 +227,42 @@ class ActorCriticMLP(nn.Module):
             else:
                 self.sigma.weight.fill_(sigma_init)
 
+    def _linears(self):
+        return [m for m in self.actor_mlp if isinstance(m, nn.Linear)] + [self.mu, self.value]
+
+    def shadow_weights(self, dtype: torch.dtype, flat: torch.Tensor) -> None:
+        """Keep a flat low-precision copy of ``flat``, the f32 buffer every Linear weight and
+        bias is a view of (rlg.ops.flatten_parameters): heads_train under autocast refreshes the
+        copy with one cast launch per minibatch and runs the layers on its views
+        (_LinearSplitKShadow)."""
+        low = torch.empty_like(flat, dtype=dtype)
+        views = {}
+        base, n = flat.data_ptr(), flat.numel()
+        for m in self._linears():
+            for p in (m.weight, m.bias):
+                o = (p.data_ptr() - base) // flat.element_size()
+                if p.data_ptr() < base or o + p.numel() > n:
+                    raise ValueError("shadow_weights: a Linear parameter is not a view of the flat buffer")
+                views[id(p)] = low[o:o + p.numel()].view_as(p)
+        self._flat32, self._flat_low, self._low_views = flat, low, views
+
     def heads_train(self, obs: torch.Tensor, splits: int = 32):
         """(mu, value) of the minibatch forward through linear_train (split-K weight grads)."""
+        low = getattr(self, "_flat_low", None)
+        sh = None
+        if (low is not None and torch.is_autocast_enabled(obs.device.type)
+                and torch.get_autocast_dtype(obs.device.type) == low.dtype):
+            low.copy_(self._flat32)          # every layer's low-precision weights: one launch
+            v = self._low_views
+            sh = {id(m): (v[id(m.weight)], v[id(m.bias)]) for m in self._linears()}
         out = obs
         for m in self.actor_mlp:
-            out = linear_train(out, m, splits) if isinstance(m, nn.Linear) else m(out)
-        return linear_train(out, self.mu, splits), linear_train(out, self.value, splits)
+            if isinstance(m, nn.Linear):
+                out = linear_train(out, m, splits, sh[id(m)] if sh else None)
+            else:
+                out = m(out)
+        return (linear_train(out, self.mu, splits, sh[id(self.mu)] if sh else None),
+                linear_train(out, self.value, splits, sh[id(self.value)] if sh else None))
 
     def forward(self, obs: torch.Tensor):
         out = self.actor_mlp(obs)

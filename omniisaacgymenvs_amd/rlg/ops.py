@@ -39,6 +39,15 @@ class MiRlMlp(C.Structure):
                 ("w", C.c_void_p * (MI_RL_MAX_HIDDEN + 2)), ("b", C.c_void_p * (MI_RL_MAX_HIDDEN + 2))]
 
 
+class MiRlAdamCfg(C.Structure):
+    """include/mi_rl.h mi_rl_adam_cfg."""
+    _fields_ = [("beta1", C.c_float), ("beta2", C.c_float), ("eps", C.c_float), ("weight_decay", C.c_float),
+                ("max_grad_norm", C.c_float), ("growth_factor", C.c_float), ("backoff_factor", C.c_float),
+                ("growth_interval", C.c_int32), ("adaptive_lr", C.c_int32), ("kl_threshold", C.c_float),
+                ("min_lr", C.c_float), ("max_lr", C.c_float), ("f16_overflow", C.c_float),
+                ("f16_begin", C.c_int64)]
+
+
 def load_library() -> C.CDLL:
     """Load libmi_rl.so and declare every prototype of include/mi_rl.h (no GPU needed)."""
     global _LIB
@@ -68,6 +77,9 @@ def load_library() -> C.CDLL:
                                           + [vp] * 10)
         lib.mi_rl_record_step.restype = i32
         lib.mi_rl_record_step.argtypes = [vp, i32, vp, vp, i32, f] + [vp] * 9
+        lib.mi_rl_adam_step.restype = i32
+        lib.mi_rl_adam_step.argtypes = [C.POINTER(MiRlAdamCfg), vp, vp, vp, vp, C.c_int64, vp, vp, vp, vp, vp,
+                                        vp, C.c_int64, vp, vp]
         _LIB = lib
     return _LIB
 
@@ -310,3 +322,106 @@ class RolloutRecorder:
             obs_state.data_ptr(), rewards_out.data_ptr(), dones_state.data_ptr(), cur_rewards.data_ptr(),
             cur_lengths.data_ptr(), episode_sums.data_ptr(), self.scratch.data_ptr(), self.ticket.data_ptr(),
             _stream(obs_in)), "mi_rl_record_step")
+
+
+# ------------------------------------------------------------------------------ optimizer step
+def flatten_parameters(params) -> torch.Tensor:
+    """Re-home the given parameters into ONE flat f32 buffer in the given order (each becomes a
+    view of it) and return the buffer; call before an optimizer or a FusedPolicy takes their
+    storage."""
+    ps = list(params)
+    if not ps or any(p.dtype != torch.float32 for p in ps):
+        raise ValueError("flatten_parameters: f32 parameters expected")
+    flat = torch.empty((sum(p.numel() for p in ps),), device=ps[0].device, dtype=torch.float32)
+    o = 0
+    for p in ps:
+        k = p.numel()
+        flat[o:o + k].copy_(p.data.reshape(-1))
+        p.data = flat[o:o + k].view_as(p)
+        o += k
+    return flat
+
+
+class FusedAdamStep:
+    """rl-games' trancate_gradients_and_step (GradScaler.unscale_, clip_grad_norm_, Adam,
+    GradScaler.update) plus the legacy adaptive LR, over a flat f32 parameter buffer, as two
+    launches (mi_rl_adam_step). Adam's moments live in flat buffers too; the torch optimizer's
+    per-parameter state is bound to views of them (and a shared device step), so its
+    state_dict saves and restores them (call :meth:`bind` again after load_state_dict)."""
+
+    def __init__(self, params, flat: torch.Tensor, optimizer: torch.optim.Adam, scaler, lr_t: torch.Tensor,
+                 max_grad_norm: float = 0.0, scheduler=None, f16_begin: Optional[int] = None) -> None:
+        """f16_begin: the flat index from which the gradients are the f32 sums that the reference
+        forms in f16 under autocast (models._LinearSplitKShadow): a scaled one beyond f16 range
+        counts as an overflow (GradScaler skips the step), as the reference's f16 gradient would
+        be inf. None: no such gradients."""
+        self.params = list(params)
+        n = sum(p.numel() for p in self.params)
+        if flat.numel() != n or flat.dtype != torch.float32 or not flat.is_contiguous():
+            raise ValueError("FusedAdamStep: flat buffer does not hold the parameters")
+        if self.params[0].data_ptr() != flat.data_ptr():
+            raise ValueError("FusedAdamStep: parameters are not views of the flat buffer (flatten_parameters)")
+        g = optimizer.param_groups[0]
+        if len(optimizer.param_groups) != 1 or g.get("amsgrad") or g.get("maximize"):
+            raise ValueError("FusedAdamStep: one plain Adam param group expected")
+        b1, b2 = g["betas"]
+        self.cfg = MiRlAdamCfg(beta1=b1, beta2=b2, eps=g["eps"], weight_decay=g["weight_decay"],
+                               max_grad_norm=float(max_grad_norm) if max_grad_norm else 0.0,
+                               growth_factor=scaler.get_growth_factor() if scaler.is_enabled() else 2.0,
+                               backoff_factor=scaler.get_backoff_factor() if scaler.is_enabled() else 0.5,
+                               growth_interval=scaler.get_growth_interval() if scaler.is_enabled() else 2000,
+                               adaptive_lr=int(scheduler is not None),
+                               kl_threshold=float(getattr(scheduler, "kl_threshold", 0.0)),
+                               min_lr=float(getattr(scheduler, "min_lr", 0.0)),
+                               max_lr=float(getattr(scheduler, "max_lr", 0.0)),
+                               f16_overflow=65520.0 if f16_begin is not None else 0.0,
+                               f16_begin=int(f16_begin or 0))
+        dev = flat.device
+        self.flat, self.n, self.optimizer, self.scaler, self.lr_t = flat, n, optimizer, scaler, lr_t
+        self.grads = torch.zeros((n,), device=dev, dtype=torch.float32)
+        self.exp_avg = torch.zeros((n,), device=dev, dtype=torch.float32)
+        self.exp_avg_sq = torch.zeros((n,), device=dev, dtype=torch.float32)
+        self.step_t = torch.zeros((), device=dev, dtype=torch.float32)
+        self.scratch = torch.zeros((1028,), device=dev, dtype=torch.float64)
+        # [0] / [4] launch tickets, [1] skipped steps, [2] first offending index of the latest
+        self.tickets = torch.tensor([0, 0, -1, -1, 0], device=dev, dtype=torch.int32)
+        self.bind()
+
+    def bind(self) -> None:
+        """Point the torch optimizer's state at the flat moments (after construction or after
+        optimizer.load_state_dict, whose restored values are copied in first)."""
+        st = self.optimizer.state
+        o = 0
+        for p in self.params:
+            k = p.numel()
+            s = st.get(p, {})
+            m, v = self.exp_avg[o:o + k].view_as(p), self.exp_avg_sq[o:o + k].view_as(p)
+            if "exp_avg" in s and s["exp_avg"].data_ptr() != m.data_ptr():
+                m.copy_(s["exp_avg"])
+                v.copy_(s["exp_avg_sq"])
+                self.step_t.copy_(torch.as_tensor(s["step"], dtype=torch.float32).reshape(()))
+            st[p] = {"step": self.step_t, "exp_avg": m, "exp_avg_sq": v}
+            o += k
+
+    def step(self, grads: Optional[torch.Tensor] = None, kl: Optional[torch.Tensor] = None) -> None:
+        """One optimizer step. grads: a flat f32 gradient buffer in parameter order (at least n
+        entries; default: the parameters' .grad gathered into self.grads); kl: device f32 scalar
+        for the adaptive LR (None: LR unchanged)."""
+        if grads is None:
+            torch.cat([p.grad.reshape(-1) for p in self.params], out=self.grads)
+            grads = self.grads
+        if grads.dtype != torch.float32 or not grads.is_contiguous() or grads.numel() < self.n:
+            raise ValueError("FusedAdamStep.step: flat f32 gradients expected")
+        sc = self.scaler
+        scale = tracker = None
+        if sc.is_enabled():
+            if sc._scale is None:
+                sc._lazy_init_scale_growth_tracker(self.flat.device)
+            scale, tracker = sc._scale, sc._growth_tracker
+        if kl is not None and (kl.dtype != torch.float32 or kl.numel() != 1):
+            raise ValueError("FusedAdamStep.step: kl must be a device f32 scalar")
+        _check(kernels().mi_rl_adam_step(
+            C.byref(self.cfg), self.flat.data_ptr(), grads.data_ptr(), self.exp_avg.data_ptr(),
+            self.exp_avg_sq.data_ptr(), self.n, self.step_t.data_ptr(), self.lr_t.data_ptr(), _ptr(scale),
+            _ptr(tracker), _ptr(kl) if self.cfg.adaptive_lr else None, self.scratch.data_ptr(),
+            self.scratch.numel(), self.tickets.data_ptr(), _stream(self.flat)), "mi_rl_adam_step")

@@ -222,3 +222,120 @@ def test_record_step_matches_torch_statements(gpu):
         assert torch.equal(cur_r, ref_r) and torch.equal(cur_l, ref_l)
         assert torch.allclose(sums, want, rtol=1e-12, atol=1e-9), (sums, want)
         assert int(rec.ticket.item()) == 0
+
+
+@pytest.mark.parametrize("clip", [1.0, 0.0])
+def test_fused_adam_step_matches_torch(gpu, clip):
+    """ops.FusedAdamStep (mi_rl_adam_step) against rl-games' torch sequence on a twin model:
+    GradScaler.unscale_, clip_grad_norm_ (when clipping), GradScaler.step(fused capturable
+    Adam), GradScaler.update, then the legacy adaptive LR on a KL. Ten steps with random
+    scaled gradients, one of them non-finite (skipped step, scale backed off), scale growth
+    every 3 clean steps: parameters and moments within 1e-5 relative, step / scale / growth
+    tracker / LR exactly."""
+    from omniisaacgymenvs_amd.rlg.a2c_continuous import AdaptiveScheduler
+    from omniisaacgymenvs_amd.rlg.models import ActorCriticMLP
+
+    torch.manual_seed(3)
+    net_f, net_t = ActorCriticMLP(87, 21).cuda(), ActorCriticMLP(87, 21).cuda()
+    net_t.load_state_dict(net_f.state_dict())
+    flat = ops.flatten_parameters(net_f.parameters())
+    sched = AdaptiveScheduler(0.008)
+    mk = lambda net, lr: (torch.optim.Adam(net.parameters(), lr=lr, eps=1e-8, fused=True, capturable=True),
+                          torch.amp.GradScaler("cuda", init_scale=2.0 ** 10, growth_interval=3))
+    lr_f = torch.tensor(3e-4, device="cuda")
+    lr_t = torch.tensor(3e-4, device="cuda")
+    opt_f, sc_f = mk(net_f, lr_f)
+    opt_t, sc_t = mk(net_t, lr_t)
+    for sc in (sc_f, sc_t):
+        sc.scale(torch.zeros((), device="cuda"))
+    fo = ops.FusedAdamStep(net_f.parameters(), flat, opt_f, sc_f, lr_f, clip, sched)
+    ps_f, ps_t = list(net_f.parameters()), list(net_t.parameters())
+    for k in range(10):
+        grads = [torch.randn_like(p) * (0.05 if k % 2 else 3.0) * sc_t._scale for p in ps_t]
+        if k == 4:
+            grads[2].view(-1)[5] = float("inf")
+        kl = torch.tensor([0.001, 0.02, 0.008][k % 3], device="cuda")
+        for p, g in zip(ps_t, grads):
+            p.grad = g.clone()
+        sc_t.unscale_(opt_t)
+        if clip:
+            torch.nn.utils.clip_grad_norm_(net_t.parameters(), clip)
+        sc_t.step(opt_t)
+        sc_t.update()
+        down = torch.clamp(lr_t / 1.5, min=sched.min_lr)
+        lr1 = torch.where(kl > 2.0 * sched.kl_threshold, down, lr_t)
+        up = torch.clamp(lr1 * 1.5, max=sched.max_lr)
+        lr_t.copy_(torch.where(kl < 0.5 * sched.kl_threshold, up, lr1))
+        fo.step(torch.cat([g.reshape(-1) for g in grads]), kl=kl)
+        torch.cuda.synchronize()
+        assert float(sc_f._scale) == float(sc_t._scale), k
+        assert int(sc_f._growth_tracker) == int(sc_t._growth_tracker), k
+        assert float(lr_f) == float(lr_t), k
+        st_t = opt_t.state[ps_t[0]]
+        assert float(fo.step_t) == float(st_t["step"]), k
+        for pf, pt in zip(ps_f, ps_t):
+            torch.testing.assert_close(pf, pt, rtol=1e-5, atol=1e-6)
+            torch.testing.assert_close(opt_f.state[pf]["exp_avg"], opt_t.state[pt]["exp_avg"], rtol=1e-5, atol=1e-6)
+            torch.testing.assert_close(opt_f.state[pf]["exp_avg_sq"], opt_t.state[pt]["exp_avg_sq"], rtol=5e-5, atol=1e-9)
+    assert float(fo.step_t) == 9.0                     # the non-finite step was skipped
+    t = fo.tickets.tolist()
+    assert t[0] == 0 and t[4] == 0 and t[1] == 1 and t[3] == -1   # tickets left 0, one skip
+    assert t[2] == sum(p.numel() for p in ps_f[:2]) + 5           # grads[2].view(-1)[5]
+
+
+def test_fused_adam_step_state_dict_round_trip(gpu):
+    """The torch optimizer's state is bound to the flat moments: its state_dict saves them,
+    and load_state_dict + bind() restores them into the flat buffers."""
+    from omniisaacgymenvs_amd.rlg.models import ActorCriticMLP
+
+    net = ActorCriticMLP(87, 21).cuda()
+    flat = ops.flatten_parameters(net.parameters())
+    lr = torch.tensor(1e-3, device="cuda")
+    opt = torch.optim.Adam(net.parameters(), lr=lr, eps=1e-8, fused=True, capturable=True)
+    sc = torch.amp.GradScaler("cuda")
+    sc.scale(torch.zeros((), device="cuda"))
+    fo = ops.FusedAdamStep(net.parameters(), flat, opt, sc, lr, 1.0, None)
+    for _ in range(3):
+        fo.step(torch.randn_like(flat) * sc._scale)
+    import copy
+
+    sd = copy.deepcopy(opt.state_dict())   # (the live state dict holds views of the flat buffers)
+    saved = (fo.exp_avg.clone(), fo.exp_avg_sq.clone(), float(fo.step_t))
+    fo.exp_avg.zero_(); fo.exp_avg_sq.zero_(); fo.step_t.zero_()
+    opt.load_state_dict(sd)
+    fo.bind()
+    torch.testing.assert_close(fo.exp_avg, saved[0], rtol=0, atol=0)
+    torch.testing.assert_close(fo.exp_avg_sq, saved[1], rtol=0, atol=0)
+    assert float(fo.step_t) == saved[2] == 3.0
+
+
+def test_fused_adam_step_reproduces_f16_gradient_overflow(gpu):
+    """Gradients the reference forms in f16 under autocast (the Linear ones, from f16_begin on)
+    are f32 sums here; a scaled value at or beyond 65520 (f16 inf) must skip the step and back
+    the scale off as GradScaler does for the reference's inf gradient — below f16_begin (the
+    log-std, f32 in the reference too) it must not."""
+    from omniisaacgymenvs_amd.rlg.models import ActorCriticMLP
+
+    net = ActorCriticMLP(87, 21).cuda()
+    flat = ops.flatten_parameters(net.parameters())
+    lr = torch.tensor(1e-3, device="cuda")
+    opt = torch.optim.Adam(net.parameters(), lr=lr, eps=1e-8, fused=True, capturable=True)
+    sc = torch.amp.GradScaler("cuda", init_scale=2.0 ** 16)
+    sc.scale(torch.zeros((), device="cuda"))
+    fo = ops.FusedAdamStep(net.parameters(), flat, opt, sc, lr, 1.0, None, f16_begin=21)
+    g = torch.zeros_like(flat)
+    g[5] = 70000.0                     # the log-std's: f32 in the reference too
+    before = flat.clone()
+    fo.step(g)
+    torch.cuda.synchronize()
+    assert float(fo.step_t) == 1.0 and float(sc._scale) == 2.0 ** 16 and not torch.equal(flat, before)
+    g.zero_()
+    g[100] = 65520.0                   # a Linear weight's: inf in f16
+    before = flat.clone()
+    fo.step(g)
+    torch.cuda.synchronize()
+    assert float(fo.step_t) == 1.0 and float(sc._scale) == 2.0 ** 15 and torch.equal(flat, before)
+    g[100] = 65519.0                   # still finite in f16 (rounds to 65504)
+    fo.step(g)
+    torch.cuda.synchronize()
+    assert float(fo.step_t) == 2.0 and float(sc._scale) == 2.0 ** 15

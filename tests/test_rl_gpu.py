@@ -155,7 +155,16 @@ def test_fused_loss_matches_torch_loss(gpu, mixed):
     torch.testing.assert_close(mb_f["mu"], cmu, rtol=tol, atol=1e-5)
     torch.testing.assert_close(mb_f["sigma"], csig, rtol=1e-6, atol=1e-7)
     for (name, _), gf, gt in zip(ag.model.named_parameters(), g_f, g_t):
-        torch.testing.assert_close(gf, gt, rtol=tol, atol=tol * gt.abs().max().item() + 1e-8, msg=name)
+        # the fused path sums weight / bias gradients in fp32 (models._LinearSplitKShadow); the
+        # fp16 statement's scaled sum can overflow (value.bias: -1.15e5 > 65504 -> -inf, which
+        # GradScaler would answer by skipping the step): there the fused one must be finite
+        fin = torch.isfinite(gt)
+        assert bool(torch.isfinite(gf).all()), name
+        if fin.any():
+            torch.testing.assert_close(gf[fin], gt[fin], rtol=tol,
+                                       atol=tol * gt[fin].abs().max().item() + 1e-8, msg=name)
+        if mixed and not fin.all():
+            assert bool((torch.sign(gf[~fin]) == torch.sign(gt[~fin])).all()), name
     env.close()
 
 

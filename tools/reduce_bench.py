@@ -33,6 +33,12 @@ def timed(fn, reps=20):
 def main():
     K, S = 32768, 32
     dt = torch.float16
+    for out in (1, 21, 100):
+        gy = torch.randn((K, out), device="cuda", dtype=dt)
+        ones_s = torch.ones((S, 1, K // S), device="cuda", dtype=dt)
+        print(json.dumps({"out": out, "bias_sum0_f32acc": round(timed(lambda: gy.sum(0, dtype=torch.float32)), 2),
+                          "bias_splitk_bmm_f32": round(timed(lambda: torch.bmm(ones_s, gy.reshape(S, K // S, out)).sum(0, dtype=torch.float32)), 2)}),
+              flush=True)
     for out, inn in ((400, 87), (200, 400), (100, 200), (22, 100)):
         gy = torch.randn((K, out), device="cuda", dtype=dt)
         x = torch.randn((K, inn), device="cuda", dtype=dt)
