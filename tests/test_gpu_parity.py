@@ -535,3 +535,46 @@ def test_wide_pgs_pair_with_empty_partner(gpu, solver, z, min_contacts):
     np.testing.assert_allclose(p_dev.cpu().numpy()[1::2], p_orc[1::2], rtol=1e-5, atol=1e-5)
     orc.close()
     env.close()
+
+
+@pytest.mark.parametrize("solver", [1, 0])
+@pytest.mark.parametrize("name", ["Ant", "Humanoid"])
+def test_velocity_iterations_match_oracle(gpu, name, solver):
+    """solver_velocity_iteration_count = 2 (the reference configs ship 0, but the knob is part of
+    the physx block every task reads): under TGS, after the 4 position iterations two more sweeps
+    with speculative bias only and no further sub-step motion; under PGS, 6 sweeps
+    (include/mi_sim.h).
+    One fused step from identical state against the oracle, the solver's parity bounds, reset /
+    progress bit-exact; the sweeps must change the result (the knob is not ignored)."""
+    ov = [f"solver_type={solver}", f"task.sim.{name}.solver_velocity_iteration_count=2"]
+    env = make_env(name, num_envs=512, device="cuda:0", seed=17, overrides=ov)
+    ref = make_env(name, num_envs=512, device="cuda:0", seed=17, overrides=[f"solver_type={solver}"])
+    sp, sr = env.task.get_robot().sim_params, ref.task.get_robot().sim_params
+    assert sp.solver_type == sr.solver_type == solver
+    if solver == 1:     # TGS: separate velocity sweeps
+        assert (sp.solver_iterations, sp.velocity_iterations, sr.velocity_iterations) == (4, 2, 0)
+    else:               # PGS: the sum as sweeps (utils/config_utils/sim_config.py)
+        assert (sp.solver_iterations, sp.velocity_iterations, sr.solver_iterations) == (6, 0, 4)
+    orc = oracle_twin(env, 17)
+    task = env.task
+    env.reset()
+    ref.reset()
+    differs = False
+    for step in range(3):
+        sync_oracle(env, orc)
+        b = task_buffers(env)
+        acts = rand_actions(512, task.num_actions, 300 + step)
+        sens = oracle_sens(env, 17, acts.numpy(), b)
+        obs_dict, rew, resets, _ = env.step(acts.to("cuda:0"))
+        ro, _, _, _ = ref.step(acts.to("cuda:0"))
+        torch.cuda.synchronize()
+        orc.env_step(acts.numpy(), task.control_frequency_inv, b)
+        check_pair(name, task, obs_dict["obs"].cpu().numpy(), rew.cpu().numpy(), b["obs"], b["rew"], 2e-3,
+                   orc.decision_margin(), sens=sens, pot=pot_mag(b))
+        assert np.array_equal(resets.cpu().numpy(), b["reset"])
+        assert np.array_equal(task.progress_buf.cpu().numpy(), b["progress"])
+        differs |= not torch.equal(obs_dict["obs"], ro["obs"])
+    assert differs
+    orc.close()
+    env.close()
+    ref.close()
