@@ -276,8 +276,8 @@ MI_D void pair_wcol(const WaveTabs& t, const float* sm, const float* gW, int g0,
 // One articulated substep of the env of this lane's half (env i, LDS region sm, W slab gW).
 template <class TP>
 MI_D void pair_artic_substep(const DevModel& m, const WaveTabs& t, const DevState& st,
-                             const SimP& p, int i, const float* mcb, float* sm, float* gW,
-                             bool load_state, bool store_state, int& prio) {
+                             const SimP& p, int i, int wv_, const float* mcb, float* sm, float* gW,
+                             bool load_state, bool store_state, int& prio, int& load) {
     static_assert(TP::kCT && TP::nv <= 32, "paired kernel: compiled topology, nv <= 32");
     const int lane = pair_l64() & 31;
     const int N = st.N, L = m.L, D = m.D, nv = m.nv, nr = m.nr;
@@ -515,6 +515,7 @@ MI_D void pair_artic_substep(const DevModel& m, const WaveTabs& t, const DevStat
         }
     }
     const int nc = 3 * ncon;
+    load = max(load, nc);                                     // half-uniform: this env's rows
     {
         const int cr = pmax(nc);                              // uniform
         if (cr > MI_PRIO_C3 && prio < 3) { __builtin_amdgcn_s_setprio(3); prio = 3; }
@@ -839,11 +840,11 @@ MI_D void pair_artic_substep(const DevModel& m, const WaveTabs& t, const DevStat
         constexpr int AR = MI_PAIR_WIDE_AREG;   // Delassus rows kept in registers; the rest streamed
         const int l64 = pair_l64(), me = l64 >> 5;
         const int kc = l64 < NV ? l64 : 0;
-        // this wave's scratch (i >> 1: the same for both halves), addressed through a buffer
+        // this wave's scratch (its slot over the launch: the same for both halves), addressed through a buffer
         // resource: one lane offset register for every row (Delassus row s at soffset 256 (s -
         // A0), A0 = 0 with the MFMA set-up (all 64 rows there), else AR); loads past the record
         // range (prefetch beyond the last row) return 0
-        const int wv = __builtin_amdgcn_readfirstlane(i >> 1);
+        const int wv = __builtin_amdgcn_readfirstlane(wv_);   // the wave's slot (pairs may be permuted)
         constexpr int WR = kWideScratchRows > 0 ? kWideScratchRows : 1;
         constexpr int A0 = MI_PAIR_WIDE_MFMA ? 0 : AR;
         const __amdgpu_buffer_rsrc_t ars = __builtin_amdgcn_make_buffer_rsrc(
@@ -862,7 +863,9 @@ MI_D void pair_artic_substep(const DevModel& m, const WaveTabs& t, const DevStat
                 }
                 continue;
             }
-            const float* gWh = gW + (ptrdiff_t)(h - me) * (ptrdiff_t)t.g_row_stride;
+            // the env of half h: its slab (the pair need not be adjacent envs: pairing by load)
+            const int ih = __builtin_amdgcn_readlane(i, 32 * h);
+            const float* gWh = gW + (ptrdiff_t)(ih - i) * (ptrdiff_t)t.g_row_stride;
             const int rl = l64 < nrh ? l64 : 0;
             float Jr[TP::nvc];
             pair_jrow<TP>(mc, t, smh, rl, nr, Jr);

@@ -775,6 +775,31 @@ __device__ __forceinline__ float* pair_env_lds(const WaveTabs& t, float* smem) {
 __device__ __forceinline__ bool pair_live(int N) {
     return (int)(xcd_block() * (blockDim.x >> 5) + ((threadIdx.x >> 6) << 1)) < N;
 }
+// this wave's index over the launch (its wide-PGS scratch slot)
+__device__ __forceinline__ int pair_wave() { return (int)(xcd_block() * (blockDim.x >> 6) + (threadIdx.x >> 6)); }
+// Pairing by load (DevState::pair_by_load): a wave's PGS is as long as its heavier env's and, on
+// the wide path (33..64 rows), as long as BOTH envs' one after the other, so two heavy envs in
+// one wave set the launch's tail. Each wave ranks its workgroup's 16 envs by their contact rows
+// in the last fused env-step (`load`, heavier first, ties by index) and takes ranks w and 15 - w
+// (w = wave in the workgroup): heaviest with lightest. A permutation inside the workgroup, the
+// same for every wave of it (every wave computes it); full workgroups only.
+__device__ __forceinline__ int pair_env_by_load(const DevState& st) {
+    const int e0 = (int)(xcd_block() * (blockDim.x >> 5));
+    const int slot = (int)(threadIdx.x >> 5);
+    if (!st.pair_by_load || blockDim.x != 512 || e0 + 16 > st.N) return e0 + slot;
+    const int l = (int)(threadIdx.x & 63u);
+    const int key = l < 16 ? st.load[e0 + l] : -1;
+    int rank = 0;
+#pragma unroll
+    for (int j = 0; j < 16; ++j) {
+        const int kj = __builtin_amdgcn_readlane(key, j);
+        rank += (kj > key || (kj == key && j < l)) ? 1 : 0;
+    }
+    const int w = slot >> 1;
+    const unsigned long long heavy = __ballot(l < 16 && rank == w);
+    const unsigned long long light = __ballot(l < 16 && rank == 15 - w);
+    return e0 + (int)__builtin_ctzll((slot & 1) ? light : heavy);
+}
 #define MI_PAIR_OCC __attribute__((amdgpu_waves_per_eu(2, 2)))
 
 // row-major state mirrors (mi_sim_set_mirror) a physics launch refreshes itself: pos, quat, vel,
@@ -786,15 +811,18 @@ __global__ __launch_bounds__(512) MI_PAIR_OCC void k_sim_step_pair(const KParams
                                                     Mirrors mir) {
     extern __shared__ __attribute__((aligned(16))) float smem[];
     const WaveTabs& t = kp->t;
-    const int i = pair_env();
+    const bool live = pair_live(kp->st.N);
+    const int i = live ? pair_env_by_load(kp->st) : pair_env();
     stage_model_constants(t, smem);
-    if (!pair_live(kp->st.N)) return;
+    if (!live) return;
     float* gW = kp->rows + (size_t)i * t.g_row_stride;
     float* sm = pair_env_lds(t, smem);
     int prio = 0;                          // issue priority so far (mi_pair.hpp MI_PRIO_C*)
+    int load = 0;                          // this env's most contact rows in a substep (unused here)
     for (int s = 0; s < substeps; ++s) {
         const KParams* k = opaque_kp(kp);
-        pair_artic_substep<T>(k->m, k->t, k->st, k->p, i, smem, sm, gW, s == 0, s == substeps - 1, prio);
+        pair_artic_substep<T>(k->m, k->t, k->st, k->p, i, pair_wave(), smem, sm, gW, s == 0, s == substeps - 1,
+                              prio, load);
     }
     // World.step() then the getters (locomotion.py:81-89): the final state is still in LDS, so the
     // launch writes the getters' row-major mirrors itself (the same values it stored to the
@@ -826,8 +854,8 @@ __global__ __launch_bounds__(512) MI_PAIR_OCC void k_env_step_pair(const KParams
     const WaveTabs& t = kp->t;
     const DevState& st = kp->st;
     const DevTask& tp = kp->tp;
-    const int i = pair_env();
     const bool live = pair_live(st.N);
+    const int i = live ? pair_env_by_load(st) : pair_env();
     STAMP_BEGIN();
     float a_lane = 0.0f;
     if (live)
@@ -838,13 +866,18 @@ __global__ __launch_bounds__(512) MI_PAIR_OCC void k_env_step_pair(const KParams
     float* gW = kp->rows + (size_t)i * t.g_row_stride;
     float* sm = pair_env_lds(t, smem);
     int prio = 0;                          // issue priority so far (mi_pair.hpp MI_PRIO_C*)
+    int load = 0;                          // this env's most contact rows in a substep
     for (int s = 0; s < substeps; ++s) {
         const KParams* k = opaque_kp(kp);
-        pair_artic_substep<T>(k->m, k->t, k->st, k->p, i, smem, sm, gW, s == 0, s == substeps - 1, prio);
+        pair_artic_substep<T>(k->m, k->t, k->st, k->p, i, pair_wave(), smem, sm, gW, s == 0, s == substeps - 1,
+                              prio, load);
     }
     STAMP_RESET();
     pair_loco_post(m, t, st, tp, i, sm, a_lane, obs_out, obs_task, rew, reset_buf, progress_buf,
                    pot, prev, rew_out, reset_out);
+    // the next fused step pairs by it (only the fused step writes it: World.step launches of one
+    // env-step, deferred or not, all see the same pairing)
+    if ((threadIdx.x & 31u) == 0) st.load[i] = load;
     STAMP(14);
 }
 
@@ -1491,6 +1524,11 @@ int mi_sim_create(const mi_model_desc* md, const mi_sim_params* prm, int32_t N, 
         st.sfs = N; st.ses = 1;
     }
     AL(reset_count, uint32_t, N); AL(nan_flag, int32_t, N); AL(dr_state, uint32_t, (size_t)6 * N);
+    AL(load, int32_t, N);
+    {   // MI_PAIR_LOAD=0: the paired kernels keep the index pairing (A/B)
+        const char* e = getenv("MI_PAIR_LOAD");
+        st.pair_by_load = (e && atoi(e) == 0) ? 0 : 1;
+    }
     AL(nan_total, unsigned long long, 1);
     if (s->wave) {
         if ((rc = dev_alloc(s, &p, sizeof(float) * (size_t)N * s->wt.g_row_stride))) return cleanup(rc);
