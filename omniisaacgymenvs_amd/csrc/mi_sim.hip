@@ -782,19 +782,26 @@ __device__ __forceinline__ int pair_wave() { return (int)(xcd_block() * (blockDi
 // one wave set the launch's tail. Each wave ranks its workgroup's 16 envs by their contact rows
 // in the last fused env-step (`load`, heavier first, ties by index) and takes ranks w and 15 - w
 // (w = wave in the workgroup): heaviest with lightest. A permutation inside the workgroup, the
-// same for every wave of it (every wave computes it); full workgroups only.
+// same for every wave of it (every wave computes it); full workgroups only, and only those
+// holding an env above MI_PAIR_LOAD_MIN contact rows.
 __device__ __forceinline__ int pair_env_by_load(const DevState& st) {
     const int e0 = (int)(xcd_block() * (blockDim.x >> 5));
     const int slot = (int)(threadIdx.x >> 5);
     if (!st.pair_by_load || blockDim.x != 512 || e0 + 16 > st.N) return e0 + slot;
     const int l = (int)(threadIdx.x & 63u);
     const int key = l < 16 ? st.load[e0 + l] : -1;
-    int rank = 0;
+    int rank = 0, kmax = 0;
 #pragma unroll
     for (int j = 0; j < 16; ++j) {
         const int kj = __builtin_amdgcn_readlane(key, j);
         rank += (kj > key || (kj == key && j < l)) ? 1 : 0;
+        kmax = max(kmax, kj);
     }
+    // only workgroups with an env above MI_PAIR_LOAD_MIN rows are re-paired (st.pair_by_load =
+    // 1 + MI_PAIR_LOAD_MIN; default 0: all but an all-zero workgroup). Re-pairing costs write
+    // traffic (adjacent envs' obs / reward rows share cache lines and are no longer written by
+    // one wave: 7.29 -> 8.38 MB per launch) but not time
+    if (kmax < st.pair_by_load) return e0 + slot;
     const int w = slot >> 1;
     const unsigned long long heavy = __ballot(l < 16 && rank == w);
     const unsigned long long light = __ballot(l < 16 && rank == 15 - w);
@@ -1525,9 +1532,13 @@ int mi_sim_create(const mi_model_desc* md, const mi_sim_params* prm, int32_t N, 
     }
     AL(reset_count, uint32_t, N); AL(nan_flag, int32_t, N); AL(dr_state, uint32_t, (size_t)6 * N);
     AL(load, int32_t, N);
-    {   // MI_PAIR_LOAD=0: the paired kernels keep the index pairing (A/B)
+    {   // MI_PAIR_LOAD=0: the paired kernels keep the index pairing (A/B); MI_PAIR_LOAD_MIN: a
+        // workgroup is re-paired only when one of its envs had more contact rows than this
         const char* e = getenv("MI_PAIR_LOAD");
-        st.pair_by_load = (e && atoi(e) == 0) ? 0 : 1;
+        const char* mn = getenv("MI_PAIR_LOAD_MIN");
+        // (A/B, round 5: 0 -> 0.1174 ms, 18 -> 0.1177, 24 -> 0.1187, 30 -> 0.1219, off 0.1245)
+        const int minrows = mn ? atoi(mn) : 0;
+        st.pair_by_load = (e && atoi(e) == 0) ? 0 : 1 + (minrows > 0 ? minrows : 0);
     }
     AL(nan_total, unsigned long long, 1);
     if (s->wave) {
