@@ -84,7 +84,7 @@ struct DevState {
     unsigned long long* nan_total;
     uint32_t* dr_state;   // [6][N] obs counter, epoch, draws; act counter, epoch, draws (or null)
     float* ws;            // workspace [N/64][slots][64]
-    int32_t* load;        // [N] contact rows of each env's last fused env-step (paired kernels' pairing)
+    int32_t* load;        // [N] constraint rows of each env's last fused env-step (paired kernels' pairing)
     int pair_by_load;     // paired kernels: pair each workgroup's envs heaviest with lightest by `load`
 };
 
