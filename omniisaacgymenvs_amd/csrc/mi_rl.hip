@@ -620,10 +620,16 @@ __global__ __launch_bounds__(kAdamBlock) void k_adam_norm(const float* __restric
         last = atomicAdd(ticket, 1u) == gridDim.x - 1;
     }
     __syncthreads();
-    if (last && threadIdx.x == 0) {
-        __threadfence();
-        double tot = 0.0;
-        for (unsigned b = 0; b < gridDim.x; ++b) tot += ((volatile double*)scratch)[b];
+    if (!last) return;
+    // the last block adds the partials: each thread a fixed strided share, then the block tree
+    // (a fixed order: deterministic; one thread walking them serially took ~20 us)
+    __threadfence();
+    double part = 0.0;
+    for (unsigned b = threadIdx.x; b < gridDim.x; b += blockDim.x) part += ((volatile double*)scratch)[b];
+    __syncthreads();   // red[] is reused
+    const double tot_all = block_sum_f64(part, red);
+    if (threadIdx.x == 0) {
+        const double tot = tot_all;
         // found_inf is GradScaler's: without a scaler torch steps whatever the gradients hold
         const bool found = scale && !isfinite(tot);
         // clip_grad_norm_: total norm in f32, coef = max_norm / (norm + 1e-6) clamped to 1
