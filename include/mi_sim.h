@@ -190,6 +190,14 @@ int mi_set_dof_state(mi_sim* sim, const float* q /*[n,D]|NULL*/, const float* qd
 int mi_set_root_state(mi_sim* sim, const float* pos /*[n,3]|NULL*/, const float* quat /*[n,4]|NULL*/,
                       const float* vel /*[n,6]|NULL*/, const int64_t* idx /*[n]|NULL*/, int32_t n,
                       void* stream);
+/* The same two setters with int32 env ids: the Cartpole task's reset passes int32 indices
+ * (tasks/cartpole.py:129-130, set_joint_positions / set_joint_velocities), so the view forwards
+ * them without an int64 conversion launch per call. */
+int mi_set_dof_state_i32(mi_sim* sim, const float* q /*[n,D]|NULL*/, const float* qd /*[n,D]|NULL*/,
+                         const int32_t* idx /*[n]|NULL*/, int32_t n, void* stream);
+int mi_set_root_state_i32(mi_sim* sim, const float* pos /*[n,3]|NULL*/, const float* quat /*[n,4]|NULL*/,
+                          const float* vel /*[n,6]|NULL*/, const int32_t* idx /*[n]|NULL*/, int32_t n,
+                          void* stream);
 /* State mirrors: row-major copies of the articulation state in caller-owned device buffers, the
  * tensors ArticulationView getters hand out with clone=False (get_world_poses, get_velocities,
  * get_joint_positions / velocities, _physics_view.get_force_sensor_forces: locomotion.py:81-89;

@@ -1788,8 +1788,8 @@ int mi_set_dof_efforts(mi_sim* s, const float* eff, const int32_t* idx, int32_t 
     return scatter_fields<int32_t>(s, f, 1, n, idx, stream);
 }
 
-int mi_set_dof_state(mi_sim* s, const float* q, const float* qd, const int64_t* idx, int32_t n,
-                     void* stream) {
+extern "C++" template <typename IDX>
+static int set_dof_state(mi_sim* s, const float* q, const float* qd, const IDX* idx, int32_t n, void* stream) {
     NEED(s);
     if (n < 0 || n > s->N || (!idx && n != s->N)) return fail(MI_E_SHAPE, "mi_set_dof_state: bad n=%d", n);
     HIP_TRY(hipSetDevice(s->device));
@@ -1799,11 +1799,12 @@ int mi_set_dof_state(mi_sim* s, const float* q, const float* qd, const int64_t* 
     if (q) f.f[nf++] = {q, s->ds.q, s->dm.D};
     if (qd) f.f[nf++] = {qd, s->ds.qd, s->dm.D};
     if (nf && n) s->mir_valid = false;
-    return scatter_fields<int64_t>(s, f, nf, n, idx, stream);
+    return scatter_fields<IDX>(s, f, nf, n, idx, stream);
 }
 
-int mi_set_root_state(mi_sim* s, const float* pos, const float* quat, const float* vel,
-                      const int64_t* idx, int32_t n, void* stream) {
+extern "C++" template <typename IDX>
+static int set_root_state(mi_sim* s, const float* pos, const float* quat, const float* vel, const IDX* idx,
+                          int32_t n, void* stream) {
     NEED(s);
     if (n < 0 || n > s->N || (!idx && n != s->N)) return fail(MI_E_SHAPE, "mi_set_root_state: bad n=%d", n);
     HIP_TRY(hipSetDevice(s->device));
@@ -1814,7 +1815,24 @@ int mi_set_root_state(mi_sim* s, const float* pos, const float* quat, const floa
     if (quat) f.f[nf++] = {quat, s->ds.root_quat, 4};
     if (vel) f.f[nf++] = {vel, s->ds.root_vel, 6};
     if (nf && n) s->mir_valid = false;
-    return scatter_fields<int64_t>(s, f, nf, n, idx, stream);
+    return scatter_fields<IDX>(s, f, nf, n, idx, stream);
+}
+
+int mi_set_dof_state(mi_sim* s, const float* q, const float* qd, const int64_t* idx, int32_t n,
+                     void* stream) {
+    return set_dof_state<int64_t>(s, q, qd, idx, n, stream);
+}
+int mi_set_dof_state_i32(mi_sim* s, const float* q, const float* qd, const int32_t* idx, int32_t n,
+                         void* stream) {
+    return set_dof_state<int32_t>(s, q, qd, idx, n, stream);
+}
+int mi_set_root_state(mi_sim* s, const float* pos, const float* quat, const float* vel,
+                      const int64_t* idx, int32_t n, void* stream) {
+    return set_root_state<int64_t>(s, pos, quat, vel, idx, n, stream);
+}
+int mi_set_root_state_i32(mi_sim* s, const float* pos, const float* quat, const float* vel,
+                          const int32_t* idx, int32_t n, void* stream) {
+    return set_root_state<int32_t>(s, pos, quat, vel, idx, n, stream);
 }
 
 int mi_sim_set_mirror(mi_sim* s, float* pos, float* quat, float* vel, float* q, float* qd, float* sens) {

@@ -108,6 +108,10 @@ _SIGS = {
                                    C.c_void_p]),
     "mi_set_root_state": (C.c_int, [C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p,
                                     C.c_int32, C.c_void_p]),
+    "mi_set_dof_state_i32": (C.c_int, [C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p, C.c_int32,
+                                       C.c_void_p]),
+    "mi_set_root_state_i32": (C.c_int, [C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p,
+                                        C.c_int32, C.c_void_p]),
     "mi_sim_set_mirror": (C.c_int, [C.c_void_p] + [C.c_void_p] * 6),
     "mi_get_state_mirror": (C.c_int, [C.c_void_p, C.c_void_p]),
     "mi_sim_step": (C.c_int, [C.c_void_p, C.c_int32, C.c_void_p]),

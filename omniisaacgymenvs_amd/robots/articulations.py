@@ -209,14 +209,26 @@ class ArticulationView:
     def _idx(self, indices, dtype) -> (Optional[torch.Tensor], int):
         if indices is None:
             return None, self.count
-        if (isinstance(indices, torch.Tensor) and indices.dtype is dtype and indices.device == self.device
-                and indices.is_contiguous()):
+        if (isinstance(indices, torch.Tensor) and indices.dtype is dtype and indices.is_cuda
+                and indices.get_device() == self._dev_index and indices.is_contiguous()):
             return indices, indices.numel()
         idx = torch.as_tensor(indices, device=self.device).to(dtype).contiguous()
         return idx, int(idx.numel())
 
-    def _idx64(self, indices) -> (Optional[torch.Tensor], int):
-        return self._idx(indices, torch.int64)
+    def _state_idx(self, indices) -> (Optional[torch.Tensor], int, bool):
+        """(ids, count, int32?) for the state setters: int64 device ids (locomotion.py:130-134)
+        and int32 ones (cartpole.py:129-130) pass as they are (the library takes both:
+        mi_set_*_state / mi_set_*_state_i32), anything else becomes int64 ids."""
+        if indices is None:
+            return None, self.count, False
+        if (isinstance(indices, torch.Tensor) and indices.is_cuda and indices.get_device() == self._dev_index
+                and indices.is_contiguous()):
+            if indices.dtype is torch.int32:
+                return indices, indices.numel(), True
+            if indices.dtype is torch.int64:
+                return indices, indices.numel(), False
+        idx = torch.as_tensor(indices, device=self.device).to(torch.int64).contiguous()
+        return idx, int(idx.numel()), False
 
     def set_joint_efforts(self, efforts: torch.Tensor, indices=None) -> None:
         e = self._f32(efforts)
@@ -228,41 +240,36 @@ class ArticulationView:
         if rc:
             N.check(rc, "mi_set_dof_efforts")
 
-    def set_joint_positions(self, positions: torch.Tensor, indices=None) -> None:
-        q = self._f32(positions)
-        idx, n = self._idx64(indices)
+    def _set_dof_state(self, q, qd, indices) -> None:
+        idx, n, i32 = self._state_idx(indices)
         if n == 0:              # empty index list: nothing to write
             return
-        rc = self._lib.mi_set_dof_state(self.handle, q.data_ptr(), None, N.ptr(idx), n, self.stream())
+        fn = self._lib.mi_set_dof_state_i32 if i32 else self._lib.mi_set_dof_state
+        rc = fn(self.handle, N.ptr(q), N.ptr(qd), None if idx is None else idx.data_ptr(), n, self.stream())
         if rc:
             N.check(rc, "mi_set_dof_state")
+
+    def _set_root_state(self, pos, quat, vel, indices) -> None:
+        idx, n, i32 = self._state_idx(indices)
+        if n == 0:              # empty index list: nothing to write
+            return
+        fn = self._lib.mi_set_root_state_i32 if i32 else self._lib.mi_set_root_state
+        rc = fn(self.handle, N.ptr(pos), N.ptr(quat), N.ptr(vel), None if idx is None else idx.data_ptr(), n,
+                self.stream())
+        if rc:
+            N.check(rc, "mi_set_root_state")
+
+    def set_joint_positions(self, positions: torch.Tensor, indices=None) -> None:
+        self._set_dof_state(self._f32(positions), None, indices)
 
     def set_joint_velocities(self, velocities: torch.Tensor, indices=None) -> None:
-        qd = self._f32(velocities)
-        idx, n = self._idx64(indices)
-        if n == 0:              # empty index list: nothing to write
-            return
-        rc = self._lib.mi_set_dof_state(self.handle, None, qd.data_ptr(), N.ptr(idx), n, self.stream())
-        if rc:
-            N.check(rc, "mi_set_dof_state")
+        self._set_dof_state(None, self._f32(velocities), indices)
 
     def set_world_poses(self, positions=None, orientations=None, indices=None) -> None:
-        p, r = self._f32(positions), self._f32(orientations)
-        idx, n = self._idx64(indices)
-        if n == 0:              # empty index list: nothing to write
-            return
-        rc = self._lib.mi_set_root_state(self.handle, N.ptr(p), N.ptr(r), None, N.ptr(idx), n, self.stream())
-        if rc:
-            N.check(rc, "mi_set_root_state")
+        self._set_root_state(self._f32(positions), self._f32(orientations), None, indices)
 
     def set_velocities(self, velocities: torch.Tensor, indices=None) -> None:
-        v = self._f32(velocities)
-        idx, n = self._idx64(indices)
-        if n == 0:              # empty index list: nothing to write
-            return
-        rc = self._lib.mi_set_root_state(self.handle, None, None, v.data_ptr(), N.ptr(idx), n, self.stream())
-        if rc:
-            N.check(rc, "mi_set_root_state")
+        self._set_root_state(None, None, self._f32(velocities), indices)
 
     # ---- physics ----
     def sim_step(self, substeps: int = 1) -> None:

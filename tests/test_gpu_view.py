@@ -79,6 +79,16 @@ def test_setter_edge_cases(gpu):
     exp = ref["q"].copy()
     exp[3], exp[200] = q[0].cpu().numpy(), q[4].cpu().numpy()
     assert np.array_equal(got["q"], exp)
+    # the same through the int32 setters (mi_set_dof_state_i32 / mi_set_root_state_i32)
+    ids32 = torch.tensor([4, -1, NENV, 201], dtype=torch.int32, device="cuda:0")
+    view.set_joint_positions(q[:4] + 0.5, indices=ids32)
+    view.set_velocities(torch.ones((4, 6), device="cuda:0"), indices=ids32)
+    got = _state(view)
+    exp[4], exp[201] = (q[0] + 0.5).cpu().numpy(), (q[3] + 0.5).cpu().numpy()
+    assert np.array_equal(got["q"], exp)
+    expv = ref["vel"].copy()
+    expv[[4, 201]] = 1.0
+    assert np.array_equal(got["vel"], expv)
     # duplicate ids: element-wise scatter (one lane per (row, column), mi_sim.hip k_rows_to_soa),
     # so each column of the env takes its value from one of the duplicate rows, unspecified
     # which — torch's own index_put_ leaves duplicates undefined, and so does PhysX's indexed
@@ -255,6 +265,13 @@ def test_state_mirrors_track_every_state_write(gpu, name, n, pair, path, monkeyp
     same()
     if name != "Cartpole":
         view.set_velocities(torch.full((3, 6), 0.5, device="cuda:0"), indices=ids)
+        same()
+    # int32 ids (Cartpole's, cartpole.py:129-130) take the library's _i32 setters: they mark the
+    # mirrors stale as well
+    view.set_joint_positions(torch.full((3, D), 0.125, device="cuda:0"), indices=ids.to(torch.int32))
+    same()
+    if name != "Cartpole":
+        view.set_velocities(torch.full((3, 6), -0.5, device="cuda:0"), indices=ids.to(torch.int32))
         same()
     g = torch.Generator().manual_seed(2)
     for fused in (True, False):
