@@ -54,6 +54,15 @@ def main():
         res["w_sum0"] = timed(lambda: part.sum(0))
         res["w_sum0_f32acc"] = timed(lambda: part.sum(0, dtype=torch.float32))
         res["w_single_gemm"] = timed(lambda: gy.t() @ x)
+        f32 = torch.float32
+        res["w_splitk_bmm_sum_f32"] = timed(lambda: torch.bmm(gy.reshape(S, K // S, out).transpose(1, 2),
+                                                              x.reshape(S, K // S, inn)).sum(0, dtype=f32))
+        res["b_splitk_bmm_sum_f32"] = timed(lambda: torch.bmm(ones_s, gy.reshape(S, K // S, out)).sum(0, dtype=f32))
+        try:   # one GEMM with f32 output (aten::mm.dtype): no split-K partials, no reduction launch
+            res["w_mm_out_f32"] = timed(lambda: torch.mm(gy.t(), x, out_dtype=f32))
+            res["b_mm_out_f32"] = timed(lambda: torch.mm(ones, gy, out_dtype=f32))
+        except Exception as e:   # noqa: BLE001 - report the op's absence
+            res["mm_out_f32_error"] = f"{type(e).__name__}: {str(e)[:120]}"
         xa = torch.cat([x, torch.ones((K, 1), device="cuda", dtype=dt)], 1)
         res["w_bias_fused_bmm"] = timed(lambda: torch.bmm(gy.reshape(S, K // S, out).transpose(1, 2),
                                                           xa.reshape(S, K // S, inn + 1)).sum(0))
