@@ -83,8 +83,19 @@ class _LinearSplitKShadow(torch.autograd.Function):
 
     @staticmethod
     def forward(ctx, x, w, b, w16, b16, splits: int):
-        ctx.save_for_backward(x, w16)
+        K, I = x.shape
         ctx.splits = splits
+        ctx.fused = splits > 1 and K % splits == 0 and x.is_cuda
+        if ctx.fused:
+            # the input with a ones column appended: the backward forms the weight AND the bias
+            # gradient in ONE split-K GEMM (tools/reduce_bench.py, profiles/r05: 12-29 us vs
+            # 30-41 us for the weight GEMM plus the bias GEMM against ones, per layer)
+            xa = torch.empty((K, I + 1), dtype=x.dtype, device=x.device)
+            xa[:, :I].copy_(x)
+            xa[:, I].fill_(1.0)
+            ctx.save_for_backward(xa, w16)
+        else:
+            ctx.save_for_backward(x, w16)
         return torch.nn.functional.linear(x, w16, b16)
 
     @staticmethod
@@ -93,21 +104,24 @@ class _LinearSplitKShadow(torch.autograd.Function):
         S = ctx.splits
         gx = gy @ w16 if ctx.needs_input_grad[0] else None
         K, O = x.shape[0], gy.shape[1]
-        split = S > 1 and K % S == 0
         f32 = torch.float32
+        if ctx.fused:
+            # [gW | gb] = gy^T [x | 1], split-K in S row blocks (fp16 block partials, as the
+            # autocast GEMM's output, summed in f32). Every bias gradient is a GEMM: torch's
+            # column reductions over the 32768 rows take multi-block (global staging) paths that,
+            # replayed from the update graph, now and then returned overflowing sums for the
+            # 100-wide layer (GradScaler skips seen by mi_rl_adam_step's counters)
+            I = x.shape[1] - 1
+            gys = gy.reshape(S, K // S, O)
+            gwb = torch.bmm(gys.transpose(1, 2), x.reshape(S, K // S, I + 1)).sum(0, dtype=f32)
+            return gx, gwb[:, :I], gwb[:, I], None, None, None
+        split = S > 1 and K % S == 0
         if split:
             gys = gy.reshape(S, K // S, O)
             gw = torch.bmm(gys.transpose(1, 2), x.reshape(S, K // S, -1)).sum(0, dtype=f32)
         else:
             gw = (gy.t() @ x).to(f32)
-        if split and gy.is_cuda:
-            # every width as a split-K GEMM against ones: torch's column reductions over the
-            # 32768 rows take multi-block (global staging) paths that, replayed from the update
-            # graph, now and then returned overflowing sums for the 100-wide layer (GradScaler
-            # skips seen by mi_rl_adam_step's counters; the eager update had none)
-            gb = torch.bmm(_ones(S, K // S, gy), gys).sum(0, dtype=f32).reshape(O)
-        else:
-            gb = gy.sum(0, dtype=f32)
+        gb = gy.sum(0, dtype=f32)
         return gx, gw, gb, None, None, None
 
 
