@@ -319,6 +319,13 @@ int mi_get_reset_count(mi_sim* sim, uint32_t* out /*[N] host*/);
  * so the next reset draws the same Philox noise; no reference counterpart: torch's global
  * generator state plays this role there, locomotion.py:120-124). Blocks the host. */
 int mi_set_reset_count(mi_sim* sim, const uint32_t* in /*[N] host*/);
+/* Pairing by load of the two-envs-per-wavefront kernels (no reference counterpart: tests and
+ * diagnostics). Each 16-env workgroup ranks its envs by a per-env load key — the most constraint
+ * rows of any substep in the env's last fused env-step — and pairs ranks w and 15 - w in wave w.
+ * out: host [N] <- the keys; in: host [N] -> the keys (either may be NULL; in after out);
+ * pairing: 0 index pairing (envs 2w, 2w + 1), 1 by load, -1 unchanged. Blocks the host. */
+int mi_sim_pair_load(mi_sim* sim, int32_t* out /*[N] host|NULL*/, const int32_t* in /*[N] host|NULL*/,
+                     int32_t pairing);
 /* Number of env-steps whose physics produced a non-finite state and were forced to reset
  * (issues deferred substeps first and waits for them: blocks the host). */
 int mi_sim_nan_count(mi_sim* sim, int64_t* count);

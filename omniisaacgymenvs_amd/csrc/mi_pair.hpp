@@ -277,7 +277,8 @@ MI_D void pair_wcol(const WaveTabs& t, const float* sm, const float* gW, int g0,
 template <class TP>
 MI_D void pair_artic_substep(const DevModel& m, const WaveTabs& t, const DevState& st,
                              const SimP& p, int i, int wv_, const float* mcb, float* sm, float* gW,
-                             bool load_state, bool store_state, int& prio, int& load) {
+                             bool load_state, bool store_state, int& prio, int& load,
+                             bool store_sens = true) {
     static_assert(TP::kCT && TP::nv <= 32, "paired kernel: compiled topology, nv <= 32");
     const int lane = pair_l64() & 31;
     const int N = st.N, L = m.L, D = m.D, nv = m.nv, nr = m.nr;
@@ -997,8 +998,11 @@ MI_D void pair_artic_substep(const DevModel& m, const WaveTabs& t, const DevStat
                 int nrow_it = nrh;
                 asm volatile("" : "+s"(nrow_it));
                 float lamn = 0.0f;
-                // rows rr .. rr + PA - 1 of A in flight (rows past the env's count are loaded but
-                // never used: the scratch is allocated for rows AR..63 and zeroed at creation)
+                // rows rr .. rr + PA - 1 of A in flight. The scratch is NOT zeroed (no memset at
+                // creation): correctness rests on the invariant that the set-up writes every row
+                // of every group of four it processes ((rr & ~3) < nrh, the sweeps' condition),
+                // so a row the sweeps use is always written before it is read; rows loaded past
+                // the last processed group are never used (a stale value there never reaches v)
                 // a fresh pointer each sweep: the loads must not be hoisted out of the sweep loop
                 // (they would all stay live: the register peak this scratch is here to remove)
                 int vo = avo, lw = l64;
@@ -1337,7 +1341,9 @@ MI_D void pair_artic_substep(const DevModel& m, const WaveTabs& t, const DevStat
         sm[t.s_q + lane] = qn;
         finite = isfinite(v) && isfinite(qn);
     }
-    if (store_state && lane < 6 * m.S) st.sens[ssx(st, lane, i)] = sm[t.s_rb + lane];
+    // (store_sens false: the staged fused step's workgroup writes the sensor rows from s_rb
+    // after its barrier, pair_stage_flush)
+    if (store_state && store_sens && lane < 6 * m.S) st.sens[ssx(st, lane, i)] = sm[t.s_rb + lane];
     if (nr && lane == 0) {
         float u6[6], p6[6], rp[3], rq[4];
 #pragma unroll
@@ -1408,7 +1414,8 @@ MI_D void pair_artic_substep(const DevModel& m, const WaveTabs& t, const DevStat
 // of this lane's half (lane = lane & 31; the half's lane 0 does the sequential parts).
 MI_D float pair_task_pre(const DevModel& m, const DevState& st, const DevTask& tp, int i,
                          const float* actions, int64_t* reset_buf, int64_t* progress_buf,
-                         float* potentials, float* prev_potentials, float* actions_out) {
+                         float* potentials, float* prev_potentials, float* actions_out,
+                         bool staged = false) {
 #pragma clang fp contract(off)
     const int lane = pair_l64() & 31, N = st.N, D = m.D, A = tp.A;
     const bool flagged = reset_buf[i] != 0;      // half-uniform
@@ -1453,7 +1460,7 @@ MI_D float pair_task_pre(const DevModel& m, const DevState& st, const DevTask& t
         const int j = lane;
         a = clampf(actions[(size_t)A * i + j], -tp.clip_actions, tp.clip_actions);
         if (tp.dr_act) a = dr_col(st, tp, 1, dre, i, j, a);
-        if (actions_out) actions_out[(size_t)A * i + j] = a;
+        if (actions_out && !staged) actions_out[(size_t)A * i + j] = a;   // staged: post-step
         st.eff[sx(st, j, i)] = a * tp.gears[j] * tp.power_scale;
     }
     if (tp.dr_act && lane == 0) dr_store(st, 1, i, dre);
@@ -1464,9 +1471,13 @@ MI_D void pair_loco_post(const DevModel& m, const WaveTabs& t, const DevState& s
                          const DevTask& tp, int i, float* sm, float a_lane,
                          float* obs_out, float* obs_task, float* rew, int64_t* reset_buf,
                          int64_t* progress_buf, float* potentials, float* prev_potentials,
-                         float* rew_out, int64_t* reset_out) {
+                         float* rew_out, int64_t* reset_out, bool staged = false) {
 #pragma clang fp contract(off)
     const int lane = pair_l64() & 31, D = m.D, S = m.S, O = tp.O;
+    // staged (t.stage_out, the fused step): the env's outputs go to its dead W rows — obs row
+    // [0, O) unclamped, reward / done / progress / potentials at O.., task.actions at O + 8 ..,
+    // the env index at O + 7 — and pair_stage_flush writes the workgroup's rows in env order
+    float* stg = sm + t.s_W;
     const int h0 = pair_l64() & 32;
     const float co = tp.clip_obs;
     const float* us = sm + t.s_us;
@@ -1487,6 +1498,10 @@ MI_D void pair_loco_post(const DevModel& m, const WaveTabs& t, const DevState& s
     if (tp.dr_obs) dre = dr_begin(st, tp, 0, i, done != 0);
     auto put = [&](int k, float v) {
         if (tp.dr_obs) v = dr_col(st, tp, 0, dre, i, k, v);
+        if (staged) {
+            stg[k] = v;
+            return;
+        }
         if (raw) raw[k] = v;
         out[k] = clampf(v, -co, co);
     };
@@ -1499,6 +1514,7 @@ MI_D void pair_loco_post(const DevModel& m, const WaveTabs& t, const DevState& s
         put(12 + j, pos);
         put(12 + D + j, vel);
         put(12 + 2 * D + 6 * S + j, a);
+        if (staged) stg[O + 8 + j] = a;   // task.actions (locomotion: A == D)
         terms[j] = a * a;
         terms[D + j] = fabsf(a * vel) * tp.ratio[j];
         if (tp.kind == MI_TASK_HUMANOID) {
@@ -1574,19 +1590,30 @@ MI_D void pair_loco_post(const DevModel& m, const WaveTabs& t, const DevState& s
         put(6, al[2] * tp.angular_velocity_scale);
         put(10, o10);
         put(11, o11);
-        potentials[i] = new_p;
-        prev_potentials[i] = prev_p;
+        if (!staged) {
+            potentials[i] = new_p;
+            prev_potentials[i] = prev_p;
+        }
         const float heading = o11 > 0.8f ? tp.heading_weight : tp.heading_weight * o11 / 0.8f;
         const float upr = o10 > 0.93f ? 0.0f + tp.up_weight : 0.0f;
         float total = (new_p - prev_p) + tp.alive_reward_scale + upr + heading -
                       tp.actions_cost * act_cost - tp.energy_cost * elec - limit_cost;
         if (rp[2] < tp.termination_height) total = tp.death_cost;
-        rew[i] = total;
         if (nan_env) {
             st.nan_flag[i] = 0;
             atomicAdd(st.nan_total, 1ull);
         }
         if (tp.dr_obs) dr_store(st, 0, i, dre);
+        if (staged) {
+            stg[O + 0] = total;
+            stg[O + 1] = __int_as_float((int)done);
+            stg[O + 2] = __int_as_float((int)progress);
+            stg[O + 3] = new_p;
+            stg[O + 4] = prev_p;
+            stg[O + 7] = __int_as_float(i);
+            return;
+        }
+        rew[i] = total;
         reset_buf[i] = done;
         progress_buf[i] = progress;
         if (rew_out) rew_out[i] = total;

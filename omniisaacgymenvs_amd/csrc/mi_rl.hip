@@ -250,6 +250,11 @@ struct PolDesc {
 
 int pad16(int x) { return (x + 15) & ~15; }
 
+constexpr size_t kPolMaxLds = 65536;   // default dynamic-LDS limit of a launch
+size_t pol_lds_bytes(const PolDesc& d) {
+    return sizeof(float) * ((size_t)2 * kPolRows * d.xs + (size_t)kPolRows * 64);
+}
+
 int pol_desc(const mi_rl_mlp* m, PolDesc* d) {
     if (!m) return fail(kNull, "mi_rl: null mlp");
     if (m->num_obs <= 0 || m->num_actions <= 0 || m->num_actions > 64 || m->num_hidden < 1 ||
@@ -273,6 +278,13 @@ int pol_desc(const mi_rl_mlp* m, PolDesc* d) {
     }
     d->xs = mx + 4;               // +4 floats: rows start on different LDS banks
     d->total = off;
+    // k_policy_step's dynamic LDS (two activation tiles + the head scratch) must fit the default
+    // 64 KB per-launch limit: refuse the layout here, so mi_rl_mlp_packed_size fails and the
+    // caller (FusedPolicy) falls back to the torch policy instead of a failed launch later
+    const size_t lds = pol_lds_bytes(*d);
+    if (lds > kPolMaxLds)
+        return fail(kShape, "mi_rl: mlp needs %zu B of LDS (widest padded layer / obs %d; max %zu B)", lds,
+                    mx, kPolMaxLds);
     return kOk;
 }
 
@@ -817,7 +829,7 @@ int32_t mi_rl_policy_step(const mi_rl_mlp* mlp, const float* packed, const float
     if (num_rows <= 0) return fail(kShape, "mi_rl_policy_step: R=%d", num_rows);
     if ((neglogp || env_actions) && !actions) return fail(kNull, "mi_rl_policy_step: neglogp / env_actions need actions");
     if (env_actions && (!action_low || !action_high)) return fail(kNull, "mi_rl_policy_step: env_actions need the action bounds");
-    const size_t lds = sizeof(float) * ((size_t)2 * kPolRows * d.xs + (size_t)kPolRows * 64);
+    const size_t lds = pol_lds_bytes(d);   // <= kPolMaxLds (pol_desc)
     hipLaunchKernelGGL(k_policy_step, dim3((num_rows + kPolRows - 1) / kPolRows), dim3(64 * kPolWaves),
                        lds, (hipStream_t)stream, d, packed, obs, num_rows, obs_mean, obs_var,
                        value_mean, value_var, eps, logstd, seed, counter_base, counter_offset,

@@ -135,6 +135,7 @@ _SIGS = {
                                   C.c_float, C.c_float, C.c_void_p]),
     "mi_get_reset_count": (C.c_int, [C.c_void_p, C.c_void_p]),
     "mi_set_reset_count": (C.c_int, [C.c_void_p, C.c_void_p]),
+    "mi_sim_pair_load": (C.c_int, [C.c_void_p, C.c_void_p, C.c_void_p, C.c_int32]),
     "mi_sim_nan_count": (C.c_int, [C.c_void_p, _i64p]),
     "mi_sim_kernel_path": (C.c_int, [C.c_void_p, _i32p, _i32p, _i32p]),
     "mi_abi_version": (C.c_int, []),

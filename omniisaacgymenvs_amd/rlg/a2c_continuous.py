@@ -246,6 +246,7 @@ class A2CAgent:
         # GradScaler unscale + grad-norm clip + Adam + scaler update + adaptive LR as two
         # launches over the flat buffer (mi_rl_adam_step) instead of ~20 torch kernels
         self.fused_opt = None
+        self._f16_begin = None
         if fused_opt:
             f16_begin = None
             if self._shadow:   # the Linear parameters follow the log-std in parameters() order
@@ -255,6 +256,7 @@ class A2CAgent:
             self.fused_opt = ops.FusedAdamStep(self.model.parameters(), self._flat_params, self.optimizer,
                                                self.scaler, self.lr_t, self.grad_norm if self.truncate_grads else 0.0,
                                                self.scheduler, f16_begin)
+            self._f16_begin = f16_begin
         # loss + head gradients as one HIP launch (mi_rl_ppo_loss); needs the fixed log-std head
         self.fused_loss = (self.device.type == "cuda" and bool(cfg.get("fused_loss", True))
                            and self.model.a2c_network.fixed_sigma)
@@ -554,6 +556,19 @@ class A2CAgent:
                                            b_loss.float()]))
         if self.dp:
             torch.cat([p.grad.reshape(-1) for p in self._params] + [self._mb_out[i, 3:4]], out=self._flat)
+            self._f16_overflow_to_inf()
+
+    def _f16_overflow_to_inf(self) -> None:
+        """Data-parallel + fp16 shadow weights: the reference's autocast Linear gradients are f16
+        on every rank, so one rank's overflow is inf BEFORE the all-reduce and the sum carries it
+        to every replica (GradScaler skips the step and backs off the scale everywhere). Here the
+        gradients are f32 sums: apply the f16 range rule (|scaled grad| >= 65520 is f16 inf,
+        mi_rl_adam_step's f16_overflow) per rank before the all-reduce, else an overflow on one
+        rank could be averaged back under the threshold. Capturable (no host sync)."""
+        if self._f16_begin is None:
+            return
+        seg = self._flat[self._f16_begin:self.fused_opt.n]
+        seg.masked_fill_(seg.abs() >= 65520.0, float("inf"))
 
     def _mb_apply(self, i: int) -> None:
         """Second half: (data-parallel: the all-reduced flat buffer / world back into p.grad and

@@ -33,6 +33,14 @@ default_physx_params: Dict[str, Any] = {
     # PhysX articulation-link default angular damping 0.05
     # (docs/transfering_policies_from_isaac_gym.md:74); the task YAMLs do not set it
     "angular_damping": 0.05,
+    # accepted and validated, not modelled by the native solver (PHYSX_UNMODELLED below)
+    "bounce_threshold_velocity": 0.2,
+    "friction_offset_threshold": 0.04,
+    "friction_correlation_distance": 0.025,
+    "enable_sleeping": True,
+    "enable_stabilization": True,
+    "sleep_threshold": 0.0,
+    "stabilization_threshold": 0.0,
 }
 default_physics_material = {"static_friction": 1.0, "dynamic_friction": 1.0, "restitution": 0.0}
 default_sim_params: Dict[str, Any] = {
@@ -48,10 +56,42 @@ default_actor_options: Dict[str, Any] = {
     "enable_gyroscopic_forces": -1,
     "solver_position_iteration_count": -1,
     "solver_velocity_iteration_count": -1,
+    "sleep_threshold": -1,
+    "stabilization_threshold": -1,
     "max_depenetration_velocity": -1,
     "contact_offset": -1,
     "rest_offset": -1,
 }
+
+
+# PhysX knobs of the task YAMLs (cfg/task/Humanoid.yaml:57-61,86-87; Ant.yaml:62-63,88-89;
+# Cartpole.yaml:45-46,71-72; defaults utils/config_utils/default_scene_params.py:34-63) that the
+# native solver accepts but does not model, with the reason (DESIGN §5 "PhysX knobs"):
+PHYSX_UNMODELLED = {
+    "enable_sleeping": "articulations are never put to sleep: the task loop writes actuation "
+                       "forces every step, and PhysX's articulation cache write wakes the "
+                       "articulation (applyCache autowake), so a driven env does not sleep there "
+                       "either; sleep_threshold is validated and ignored",
+    "enable_stabilization": "PhysX's experimental stabilization pass (extra damping of bodies "
+                            "below stabilization_threshold, mass-normalised kinetic energy) is not "
+                            "modelled; stabilization_threshold is validated and ignored",
+    "bounce_threshold_velocity": "no effect: every task's restitution is 0, so no contact bounces",
+    "friction_offset_threshold": "no effect while contact_offset <= friction_offset_threshold "
+                                 "(0.02 <= 0.04 in every task): every speculative contact within "
+                                 "contact_offset already carries friction rows",
+    "friction_correlation_distance": "friction is per contact point (two pyramid rows each), not "
+                                     "merged into patch anchors",
+}
+_warned = set()
+
+
+def _warn_unmodelled(keys) -> None:
+    new = [k for k in keys if k not in _warned]
+    if new:
+        import warnings
+        _warned.update(new)
+        warnings.warn("mi_sim: PhysX settings accepted but not modelled: " +
+                      "; ".join(f"{k} ({PHYSX_UNMODELLED[k]})" for k in new), stacklevel=3)
 
 
 class SimConfig:
@@ -138,4 +178,32 @@ class SimConfig:
         p.enable_self_collisions = 1 if esc is True or esc == 1 else 0
         p.max_angular_velocity = float(px.get("max_angular_velocity", math.radians(5729.58)))
         p.angular_damping = float(a.get("angular_damping", px.get("angular_damping", 0.05)))
+        self.unmodelled(actor_name)
         return p
+
+    def unmodelled(self, actor_name: str) -> Dict[str, Any]:
+        """The PhysX settings of this actor that the native solver accepts but does not model
+        (PHYSX_UNMODELLED), validated the way PhysX would (thresholds in [0, inf), booleans);
+        warns once per key and process. Returns {key: value} of those in effect."""
+        a = self.parse_actor_config(actor_name)
+        px = self._physx_params
+        out: Dict[str, Any] = {}
+        for k in ("sleep_threshold", "stabilization_threshold"):
+            v = float(a[k])
+            if not (0.0 <= v < math.inf):
+                raise ValueError(f"{actor_name}.{k} = {v}: allowed range [0, max_float)")
+            out[k] = v
+        for k in ("enable_sleeping", "enable_stabilization"):
+            if not isinstance(px[k], bool) and px[k] not in (0, 1):
+                raise ValueError(f"physx.{k} = {px[k]!r}: a boolean")
+            out[k] = bool(px[k])
+        for k in ("bounce_threshold_velocity", "friction_offset_threshold", "friction_correlation_distance"):
+            out[k] = float(px[k])
+        if float(self._sim_params["default_physics_material"].get("restitution", 0.0)) != 0.0:
+            raise ValueError("default_physics_material.restitution != 0: restitution is not modelled")
+        active = [k for k in ("enable_sleeping", "enable_stabilization") if out[k]]
+        if out["friction_offset_threshold"] < float(a["contact_offset"]):
+            active.append("friction_offset_threshold")
+        active.append("friction_correlation_distance")
+        _warn_unmodelled(active)
+        return out

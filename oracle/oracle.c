@@ -211,6 +211,7 @@ struct orc_sim {
     int32_t* nan_flag;
     int64_t nan_total;
     float* margin; /* per env: ws_t.margin over the last physics call */
+    float* pmargin; /* per env: ws_t.pmargin over the last physics call (diagnostic) */
     mi_dr_params dr;   /* observation / action noise DR (randomize.py:176-306) */
     int dr_obs, dr_act;
     uint32_t* dr_state; /* [N][6]: obs counter, epoch, draws; act counter, epoch, draws */
@@ -291,6 +292,7 @@ orc_sim* orc_sim_create(const mi_model_desc* md, const mi_sim_params* params, in
     s->reset_count = (uint32_t*)dupmem(NULL, (size_t)N * 4);
     s->nan_flag = (int32_t*)dupmem(NULL, (size_t)N * 4);
     s->margin = (float*)dupmem(NULL, (size_t)N * 4);
+    s->pmargin = (float*)dupmem(NULL, (size_t)N * 4);
     for (int i = 0; i < N; ++i) {
         s->root_quat[4 * i] = 1.0f;
         for (int c = 0; c < 3; ++c) s->root_pos[3 * i + c] = s->origins[3 * i + c];
@@ -306,7 +308,7 @@ void orc_sim_destroy(orc_sim* s) {
                     m->geom_p0, m->geom_p1, m->geom_radius, m->sensor_link, m->sensor_pos,
                     m->pairs, m->pt_geom, m->pt_end, s->origins, s->root_pos, s->root_quat,
                     s->root_vel, s->q, s->qd, s->eff, s->sens, s->reset_count, s->nan_flag, s->margin,
-                    s->dr_state};
+                    s->pmargin, s->dr_state};
     for (size_t i = 0; i < sizeof ptrs / sizeof ptrs[0]; ++i) free(ptrs[i]);
     free(s);
 }
@@ -373,9 +375,13 @@ static void cartpole_substep(const model_t* m, const mi_sim_params* p, float* q,
 typedef struct {
     float *R, *o, *aw, *I6, *Iw, *S, *V, *A, *J, *M, *Gc, *C, *u, *rhs, *ud;
     float *Jr, *W, *b, *lam, *Ad, *cpt, *cdir, *tmp, *sep, *dsum, *ubar;
+    float *Dl, *vr, *ia, *ls;   /* TGS, Delassus space: A = J W^T [R][R], row velocities,
+                                 * 1 / A_rr, each row's lambda summed over the sub-steps */
     int *rkind, *rcon, *clink, *clink2;
     int nrows, ncon;
     float margin; /* min distance of any activation decision from its threshold (test aid) */
+    float pmargin; /* min distance of a row's unprojected lambda from a projection bound, in
+                    * row-velocity units (|x - bound| A_rr, m/s or rad/s; diagnostic only) */
 } ws_t;
 
 static ws_t* ws_new(const model_t* m) {
@@ -392,6 +398,8 @@ static ws_t* ws_new(const model_t* m) {
     w->Jr = (float*)calloc((size_t)R * nv + 1, 4); w->W = (float*)calloc((size_t)R * nv + 1, 4);
     w->b = (float*)calloc(R, 4); w->lam = (float*)calloc(R, 4); w->Ad = (float*)calloc(R, 4);
     w->sep = (float*)calloc(R, 4); w->dsum = (float*)calloc(R, 4); w->ubar = (float*)calloc(nv + 1, 4);
+    w->Dl = (float*)calloc((size_t)R * R, 4); w->vr = (float*)calloc(R, 4); w->ia = (float*)calloc(R, 4);
+    w->ls = (float*)calloc(R, 4);
     w->rkind = (int*)calloc(R, 4); w->rcon = (int*)calloc(R, 4);
     const int nc = m->npts + (m->self_on ? m->P : 0) + 1;   /* contact capacity */
     w->cpt = (float*)calloc((size_t)nc * 3, 4); w->clink = (int*)calloc(nc, 4);
@@ -402,7 +410,8 @@ static ws_t* ws_new(const model_t* m) {
 static void ws_free(ws_t* w) {
     void* p[] = {w->R, w->o, w->aw, w->I6, w->Iw, w->S, w->V, w->A, w->J, w->M, w->Gc, w->C, w->u,
                  w->rhs, w->ud, w->Jr, w->W, w->b, w->lam, w->Ad, w->rkind, w->rcon, w->cpt,
-                 w->clink, w->clink2, w->cdir, w->tmp, w->sep, w->dsum, w->ubar};
+                 w->clink, w->clink2, w->cdir, w->tmp, w->sep, w->dsum, w->ubar,
+                 w->Dl, w->vr, w->ia, w->ls};
     for (size_t i = 0; i < sizeof p / sizeof p[0]; ++i) free(p[i]);
     free(w);
 }
@@ -619,6 +628,95 @@ static int is_finite_state(int D, const float* rp, const float* rq, const float*
     return acc == 0.0f;
 }
 
+/* Diagnostic (not a decision margin): how close row r's unprojected lambda x came to a bound
+ * of its projection, in row-velocity units (|x - bound| A_rr). A projection is continuous, so a
+ * rounding-level difference across it moves lambda by a rounding-level amount; tools/
+ * parity_stats.py reports this next to the errors to show whether far errors sit at clamps.
+ * A friction row whose bound is 0 (its normal row inactive) projects everything to 0: no
+ * decision, skipped. */
+static void proj_margin(ws_t* w, int r, float x, float lo, float hi, int two_sided) {
+    float d = fabsf(x - lo);
+    if (two_sided) {
+        if (!(hi > 0.0f)) return;
+        d = fminf(d, fabsf(x - hi));
+    }
+    w->pmargin = fminf(w->pmargin, d * w->Ad[r]);
+}
+
+/* TGS in the Delassus-space form of the device's sweeps (mi_pair.hpp P10, narrow and wide
+ * paths; VERDICT r5 "next" #1). The row velocities v_r = J_r.u* are carried through
+ * A = J W^T (v_c += A[c][r] dl per row step) instead of being re-formed from u; each sub-step's
+ * bias comes from the row's separation plus h x its carried velocity after each earlier
+ * sub-step (friction rows: bias 0; velocity iterations: speculative bias only); the owner's
+ * step is x = lambda + (b - v_r) / A_rr with the reciprocal formed once, projected onto
+ * [0, inf) or +-mu lambda_n. At the end u = u* + sum_r W_r lambda_r and the positions'
+ * velocity u-bar = u* + sum_r W_r (sum_k lambda_r^(k) / iters), each summed in row order per
+ * DOF. Mathematically the u-space statement (u-bar = the sub-steps' mean velocity); in
+ * rounding it is the device's path — the carried v drifts by the rounding of every A dl, which
+ * grows with the total variation of lambda in stacked contacts — so the oracle's own 2-ulp
+ * conditioning response (tests/helpers.py oracle_sensitivity) now measures that drift too. */
+static void tgs_delassus(const model_t* m, const mi_sim_params* p, ws_t* w, float* u) {
+    const int nv = m->nv, nrows = w->nrows, nnorm = 3 * w->ncon;
+    const float mu = p->friction;
+    const int npos = p->solver_iterations, nvel = p->velocity_iterations;
+    const float h = p->dt / (float)npos;
+    for (int r = 0; r < nrows; ++r) {
+        const float* Jr = w->Jr + (size_t)r * nv;
+        float v = 0.0f;
+        for (int k = 0; k < nv; ++k) v += Jr[k] * u[k];
+        w->vr[r] = v;
+        for (int c = 0; c < nrows; ++c) {
+            const float* Wc = w->W + (size_t)c * nv;
+            float a = 0.0f;
+            for (int k = 0; k < nv; ++k) a += Jr[k] * Wc[k];
+            w->Dl[(size_t)r * nrows + c] = a;   /* A[r][c]: row r's velocity per unit lambda_c */
+        }
+        w->ia[r] = 1.0f / w->Ad[r];
+        w->lam[r] = 0.0f;
+        w->dsum[r] = 0.0f;
+        w->ls[r] = 0.0f;
+    }
+    for (int it = 0; it < npos + nvel; ++it) {
+        for (int r = 0; r < nrows; ++r) {   /* this sub-step's bias (friction rows: 0) */
+            if (w->rkind[r] == 1 || w->rkind[r] == 2) { w->b[r] = 0.0f; continue; }
+            const float e = w->sep[r] + w->dsum[r];
+            const float bb = e >= 0.0f ? -e / h : (it < npos ? -p->erp * e / h : 0.0f);
+            w->b[r] = bb > p->max_depenetration_velocity ? p->max_depenetration_velocity : bb;
+        }
+        float lamn = 0.0f;   /* the latest normal row's lambda: its friction rows' bound */
+        for (int r = 0; r < nrows; ++r) {
+            const int kd = w->rkind[r];
+            const int fric = kd == 1 || kd == 2;
+            const float l0 = w->lam[r];
+            const float x = l0 + (w->b[r] - w->vr[r]) * w->ia[r];
+            const float lim = mu * lamn;
+            const float lo = fric ? -lim : 0.0f;
+            proj_margin(w, r, x, lo, lim, fric);
+            float ln = x > lo ? x : lo;
+            if (fric) ln = ln < lim ? ln : lim;
+            if (kd == 0 && r < nnorm) lamn = ln;
+            const float dl = ln - l0;
+            for (int c = 0; c < nrows; ++c) w->vr[c] += w->Dl[(size_t)c * nrows + r] * dl;
+            w->lam[r] = ln;
+        }
+        if (it < npos)   /* the sub-step moves each row by h v_r; its lambda joins the sum */
+            for (int r = 0; r < nrows; ++r) {
+                w->dsum[r] += h * w->vr[r];
+                w->ls[r] += w->lam[r];
+            }
+    }
+    for (int k = 0; k < nv; ++k) {
+        float uk = u[k], ub = u[k];
+        for (int r = 0; r < nrows; ++r) {
+            const float wk = w->W[(size_t)r * nv + k];
+            uk = uk + wk * w->lam[r];
+            ub = ub + wk * (w->ls[r] / (float)npos);
+        }
+        u[k] = uk;
+        w->ubar[k] = ub;
+    }
+}
+
 /* one articulated substep for one env; state arrays are that env's rows */
 static void artic_substep(const model_t* m, const mi_sim_params* p, ws_t* w, float* rp, float* rq,
                           float* rv, float* q, float* qd, const float* eff, float* sens) {
@@ -746,56 +844,36 @@ static void artic_substep(const model_t* m, const mi_sim_params* p, ws_t* w, flo
         w->Ad[r] = a > 1e-12f ? a : 1e-12f;
         w->lam[r] = 0.0f;
     }
-    /* ---- projected Gauss-Seidel sweeps (PGS: over dt; TGS: position sub-steps) ---- */
-    const float mu = p->friction;
+    /* ---- projected Gauss-Seidel sweeps (PGS: over dt, u space; TGS: position sub-steps in
+     * Delassus space, tgs_delassus) ---- */
     const int tgs = p->solver_type == MI_SOLVER_TGS;
-    const int npos = p->solver_iterations, nvel = tgs ? p->velocity_iterations : 0;
-    const float h = tgs ? dt / (float)npos : dt;
-    for (int r = 0; r < nrows; ++r) w->dsum[r] = 0.0f;
-    for (int k = 0; k < nv; ++k) w->ubar[k] = 0.0f;
-    for (int it = 0; it < npos + nvel; ++it) {
-        if (tgs) {   /* this sub-step's bias from the row's current separation (friction: 0) */
-            for (int r = 0; r < nrows; ++r) {
-                if (w->rkind[r] == 1 || w->rkind[r] == 2) continue;
-                const float e = w->sep[r] + w->dsum[r];
-                float bb;
-                if (it < npos) bb = e >= 0.0f ? -e / h : -p->erp * e / h;
-                else bb = e >= 0.0f ? -e / h : 0.0f;            /* velocity iterations */
-                w->b[r] = bb > p->max_depenetration_velocity ? p->max_depenetration_velocity : bb;
-            }
-        }
-        for (int r = 0; r < nrows; ++r) {
-            const float* Jr = w->Jr + (size_t)r * nv;
-            float jv = 0.0f;
-            for (int k = 0; k < nv; ++k) jv += Jr[k] * u[k];
-            float l0 = w->lam[r];
-            float ln = l0 + (w->b[r] - jv) / w->Ad[r];
-            if (w->rkind[r] == 1 || w->rkind[r] == 2) {
-                float lim = mu * w->lam[w->rcon[r]];
-                ln = ln > lim ? lim : (ln < -lim ? -lim : ln);
-            } else {
-                ln = ln > 0.0f ? ln : 0.0f;
-            }
-            float dl = ln - l0;
-            const float* Wr = w->W + (size_t)r * nv;
-            for (int k = 0; k < nv; ++k) u[k] += Wr[k] * dl;
-            w->lam[r] = ln;
-        }
-        if (tgs && it < npos) {   /* the sub-step moves the rows by h J u; positions by h u */
+    float* ui = u;   /* the velocity the positions integrate with (TGS: the sub-steps' mean) */
+    if (tgs) {
+        tgs_delassus(m, p, w, u);
+        ui = w->ubar;
+    } else {
+        const float mu = p->friction;
+        for (int it = 0; it < p->solver_iterations; ++it) {
             for (int r = 0; r < nrows; ++r) {
                 const float* Jr = w->Jr + (size_t)r * nv;
                 float jv = 0.0f;
                 for (int k = 0; k < nv; ++k) jv += Jr[k] * u[k];
-                w->dsum[r] += h * jv;
+                float l0 = w->lam[r];
+                float ln = l0 + (w->b[r] - jv) / w->Ad[r];
+                if (w->rkind[r] == 1 || w->rkind[r] == 2) {
+                    float lim = mu * w->lam[w->rcon[r]];
+                    proj_margin(w, r, ln, -lim, lim, 1);
+                    ln = ln > lim ? lim : (ln < -lim ? -lim : ln);
+                } else {
+                    proj_margin(w, r, ln, 0.0f, 0.0f, 0);
+                    ln = ln > 0.0f ? ln : 0.0f;
+                }
+                float dl = ln - l0;
+                const float* Wr = w->W + (size_t)r * nv;
+                for (int k = 0; k < nv; ++k) u[k] += Wr[k] * dl;
+                w->lam[r] = ln;
             }
-            for (int k = 0; k < nv; ++k) w->ubar[k] += u[k];
         }
-    }
-    /* the velocity the positions integrate with: the final one (PGS) or the sub-steps' mean */
-    float* ui = u;
-    if (tgs) {
-        for (int k = 0; k < nv; ++k) w->ubar[k] = w->ubar[k] / (float)npos;
-        ui = w->ubar;
     }
     /* ---- force sensors: contact wrench on the sensor link, link frame ---- */
     for (int si = 0; si < m->S; ++si) {
@@ -909,6 +987,7 @@ static void env_physics(orc_sim* s, ws_t* w, int i, int substeps) {
     float* qd = s->qd + (size_t)D * i;
     const float* eff = s->eff + (size_t)D * i;
     w->margin = INFINITY;
+    w->pmargin = INFINITY;
     for (int st = 0; st < substeps; ++st) {
         if (m->dyn == MI_DYN_CARTPOLE)
             cartpole_substep(m, &s->p, q, qd, eff);
@@ -919,12 +998,14 @@ static void env_physics(orc_sim* s, ws_t* w, int i, int substeps) {
     if (!is_finite_state(D, s->root_pos + 3 * i, s->root_quat + 4 * i, s->root_vel + 6 * i, q, qd))
         s->nan_flag[i] = 1;
     s->margin[i] = w->margin;
+    s->pmargin[i] = w->pmargin;
 }
 
 /* Per env: how close (in metres / radians) any contact or joint-limit activation decision of
  * the last physics call came to its threshold. Test aid: a device whose float summation
  * order differs can take the other branch only where this is within rounding. */
 void orc_decision_margin(const orc_sim* s, float* out) { memcpy(out, s->margin, (size_t)s->N * 4); }
+void orc_projection_margin(const orc_sim* s, float* out) { memcpy(out, s->pmargin, (size_t)s->N * 4); }
 
 void orc_sim_step(orc_sim* s, int substeps) {
 #pragma omp parallel num_threads(g_threads)

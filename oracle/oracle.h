@@ -86,6 +86,9 @@ void orc_momentum(orc_sim* s, int env, double* out6 /* angular about world origi
 int orc_contact_count(orc_sim* s, int env);
 float orc_self_min_gap(orc_sim* s, int env);
 void orc_decision_margin(const orc_sim* s, float* out /*[N]*/);
+/* per env: how close any row's unprojected lambda came to a bound of its projection in the last
+ * physics call, in row-velocity units (diagnostic for tools/parity_stats.py; not an exemption) */
+void orc_projection_margin(const orc_sim* s, float* out /*[N]*/);
 
 #ifdef __cplusplus
 }

@@ -72,6 +72,7 @@ def lib() -> C.CDLL:
             "orc_contact_count": (C.c_int, [C.c_void_p, C.c_int]),
             "orc_self_min_gap": (C.c_float, [C.c_void_p, C.c_int]),
             "orc_decision_margin": (None, [C.c_void_p, C.c_void_p]),
+            "orc_projection_margin": (None, [C.c_void_p, C.c_void_p]),
         }
         for name, (res, args) in sig.items():
             fn = getattr(L, name)
@@ -245,6 +246,13 @@ class OracleSim:
         physics call (contact gap vs contact_offset, q and q + dt*qd vs limits)."""
         out = np.empty(self.N, np.float32)
         lib().orc_decision_margin(self.h, out.ctypes.data)
+        return out
+
+    def projection_margin(self) -> np.ndarray:
+        """[N] min |x - bound| x A_rr over every row projection of the last physics call (x the
+        row's unprojected lambda; m/s or rad/s). Diagnostic: projections are continuous."""
+        out = np.empty(self.N, np.float32)
+        lib().orc_projection_margin(self.h, out.ctypes.data)
         return out
 
     def nan_count(self) -> int:

@@ -115,32 +115,48 @@ def task_params_from_cfg(task_name: str):
     return tp, m, (gears, ratio, init)
 
 
-def oracle_sensitivity(env, seed, actions, substeps, bufs_before, groups, rel=2.0 ** -22, rng_seed=0):
+def oracle_sensitivity(env, seed, actions, substeps, bufs_before, groups, rel=2.0 ** -22, rng_seed=0,
+                       probes=None, per_probe=None):
     """Oracle-side estimate of how much this step amplifies rounding-level differences, per env
-    and observation group: an oracle twin of the device's CURRENT state (call before the device
-    steps) with root pose / velocity, q and qd each scaled by (1 + rel * u), u ~ U(-1, 1) (2 ulp
-    of float32), stepped with the same actions; returns ({group: [N] max |obs_pert - obs_ref|},
-    [N] |rew_pert - rew_ref|, the unperturbed twin's buffers). Contact / PGS conditioning
-    (stacked contacts, near-singular Delassus blocks) shows up here as a large value, so a
-    device-vs-oracle difference can be judged against the step's own conditioning rather than
-    against the device's measured error."""
+    and observation group: oracle twins of the device's CURRENT state (call before the device
+    steps) with root pose (quaternion included) / velocity, q and qd each scaled by
+    (1 + rel * u), u ~ U(-1, 1) (2 ulp of float32), stepped with the same actions; the response
+    is the largest over `probes` independent perturbations (default tests/parity_bounds.py
+    SENS_PROBES: one random direction under-reads an ill-conditioned step's worst direction).
+    Returns ({group: [N] max |obs_pert - obs_ref|}, [N] |rew_pert - rew_ref|, the unperturbed
+    twin's buffers); per_probe (a list) receives each probe's ({group: ...}, rew) too. Contact /
+    PGS conditioning (stacked contacts, near-singular Delassus blocks) shows up here as a large
+    value, so a device-vs-oracle difference can be judged against the step's own conditioning
+    rather than against the device's measured error."""
     import copy
 
+    from tests.parity_bounds import SENS_PROBES
+
+    probes = SENS_PROBES if probes is None else int(probes)
     rng = np.random.default_rng(rng_seed)
     ref = oracle_twin(env, seed)
-    pert = oracle_twin(env, seed)
-    p, q, v = pert.root_state()
-    jq, jqd = pert.dof_state()
-    f = lambda a: (a * (1.0 + rel * rng.uniform(-1, 1, a.shape))).astype(np.float32)
-    if env.task.model.root_free:
-        pert.set_root_state(f(p), q, f(v))
-    pert.set_dof_state(f(jq), f(jqd))
-    b_ref, b_pert = copy.deepcopy(bufs_before), copy.deepcopy(bufs_before)
+    b_ref = copy.deepcopy(bufs_before)
     ref.env_step(actions, substeps, b_ref)
-    pert.env_step(actions, substeps, b_pert)
-    d = np.abs(b_pert["obs"] - b_ref["obs"])
-    out = {g: d[:, sl].max(axis=1) for g, sl in groups.items()}
-    rew = np.abs(b_pert["rew"] - b_ref["rew"])
     ref.close()
-    pert.close()
+    out = {g: np.zeros(len(b_ref["rew"])) for g in groups}
+    rew = np.zeros(len(b_ref["rew"]))
+    for _ in range(probes):
+        pert = oracle_twin(env, seed)
+        p, q, v = pert.root_state()
+        jq, jqd = pert.dof_state()
+        f = lambda a: (a * (1.0 + rel * rng.uniform(-1, 1, a.shape))).astype(np.float32)
+        if env.task.model.root_free:
+            pert.set_root_state(f(p), f(q), f(v))
+        pert.set_dof_state(f(jq), f(jqd))
+        b_pert = copy.deepcopy(bufs_before)
+        pert.env_step(actions, substeps, b_pert)
+        pert.close()
+        d = np.abs(b_pert["obs"] - b_ref["obs"])
+        og = {g: d[:, sl].max(axis=1) for g, sl in groups.items()}
+        rg = np.abs(b_pert["rew"] - b_ref["rew"])
+        if per_probe is not None:
+            per_probe.append((og, rg))
+        for g in groups:
+            out[g] = np.maximum(out[g], og[g])
+        rew = np.maximum(rew, rg)
     return out, rew, b_ref

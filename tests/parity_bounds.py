@@ -27,6 +27,7 @@ import numpy as np
 DECISION_EPS = 1e-4          # m or rad: a decision this close to its threshold may flip
 NEAR_MAX_FRAC = 0.02         # envs at a threshold that may differ
 SENS_K = 4.0                 # conditioning allowance: this many times the oracle's 2-ulp response
+SENS_PROBES = 1              # ... the largest over this many independent 2-ulp perturbations
 SENS_CAP = 1e-2              # ... never above this x max(1, |oracle value|)
 WIDEN_MAX_FRAC = 0.01        # envs per step that may need the conditioning allowance
 CARTPOLE_TOL = 1e-4

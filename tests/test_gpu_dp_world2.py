@@ -102,3 +102,87 @@ def test_data_parallel_graphed_world2_replicas_identical(gpu):
         assert all(res["equal"]), res["equal"]            # bit-identical replicas every epoch
         assert res["finite"] and res["obs_differ"]        # distinct shards, sane training state
     assert out[0]["lrs"] == out[1]["lrs"]                  # one adaptive LR sequence
+
+
+def _overflow_worker(rank, world, port, q):
+    """an f16-range overflow of a Linear gradient on ONE rank must make BOTH
+    replicas skip the step (the reference's f16 gradient is inf before the all-reduce)."""
+    try:
+        import torch.distributed as dist
+        os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+        os.environ.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+        torch.cuda.set_device(0)
+        dist.init_process_group("gloo", rank=rank, world_size=world)
+        from omniisaacgymenvs_amd.rlg.a2c_continuous import A2CAgent
+        from omniisaacgymenvs_amd.utils.rlgames.rlgames_utils import RLGPUEnv, register_env
+        from omniisaacgymenvs_amd.utils.task_util import make_env
+
+        env = make_env("Humanoid", num_envs=N_ENVS, device="cuda:0", seed=42,
+                       env_id_offset=rank * N_ENVS, global_num_envs=world * N_ENVS,
+                       overrides=[f"train.params.config.minibatch_size={N_ENVS * 8}"])
+        register_env(f"rlgpu_dpo{rank}", lambda **kw: env)
+        params = env.task_cfg["train"]["params"]
+        params["config"].update(multi_gpu=True, multi_gpu_mode="data_parallel", graph_rollout=True,
+                                graph_update=False, save_frequency=0, save_best_after=10 ** 9)
+        agent = A2CAgent(RLGPUEnv(f"rlgpu_dpo{rank}", N_ENVS), params, run_dir=f"/tmp/dpo_{port}_{rank}")
+        assert agent.dp and agent._f16_begin is not None and agent.fused_opt is not None
+        agent.env_reset()
+        idx = agent._f16_begin + 5
+        inject_at = 2 * agent.num_minibatches * agent.mini_epochs - 3   # a late minibatch of epoch 2
+        calls = {"n": 0}
+        rec = []
+        orig_mask, orig_apply = agent._f16_overflow_to_inf, agent._mb_apply
+
+        def mask():
+            if calls["n"] == inject_at:
+                rec.append(("rank0_small_entry", float(agent._flat[idx].abs())))
+                if rank == 1:
+                    agent._flat[idx] = 1.0e5     # over f16 range here, under it once averaged
+            orig_mask()
+
+        def apply(i):
+            before = int(agent.fused_opt.tickets[1])
+            orig_apply(i)
+            torch.cuda.synchronize()
+            if calls["n"] == inject_at:
+                rec.append(("delta", int(agent.fused_opt.tickets[1]) - before))
+                rec.append(("index", int(agent.fused_opt.tickets[2])))
+            calls["n"] += 1
+
+        agent._f16_overflow_to_inf, agent._mb_apply = mask, apply
+        for _ in range(2):
+            agent.train_epoch()
+        res = {"rec": rec, "idx": idx, "calls": calls["n"], "inject_at": inject_at}
+        dist.barrier()
+        dist.destroy_process_group()
+        env.close()
+        q.put((rank, res))
+    except Exception as e:          # noqa: BLE001 - report, do not hang the parent
+        import traceback
+        q.put((rank, {"error": f"{e!r}\n{traceback.format_exc()}"}))
+
+
+def test_data_parallel_f16_overflow_on_one_rank_skips_everywhere(gpu):
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_overflow_worker, args=(r, WORLD, port, q)) for r in range(WORLD)]
+    for p in procs:
+        p.start()
+    try:
+        out = dict(q.get(timeout=240) for _ in range(WORLD))
+    finally:
+        for p in procs:
+            p.join(timeout=60)
+            if p.is_alive():
+                p.kill()
+    for r in range(WORLD):
+        assert "error" not in out[r], out[r].get("error")
+    for r in range(WORLD):
+        res = out[r]
+        assert res["calls"] > res["inject_at"], res
+        rec = dict(res["rec"])
+        if r == 0:   # rank 0's own gradient is in range: the skip can only come from rank 1
+            assert rec["rank0_small_entry"] < 65520.0, rec
+        assert rec["delta"] == 1, (r, rec)              # the step was skipped on this replica
+        assert rec["index"] == res["idx"], (r, rec)     # ... for the injected entry

@@ -71,6 +71,26 @@ def test_fused_policy_matches_torch_fp32(gpu, task, rows):
     assert torch.equal(out["act"], act) and torch.equal(out["nlp"].squeeze(-1), nlp)
 
 
+def test_fused_policy_lds_limit(gpu):
+    """k_policy_step's dynamic LDS grows with the widest padded layer. A layout past
+    the 64 KB launch limit ([512, 256, 128]: 70 144 B) is refused at construction (ValueError,
+    the agent then keeps the torch policy); the widest layout that fits (464: 64 000 B) runs and
+    matches the torch statement."""
+    with pytest.raises(ValueError, match="LDS"):
+        ops.FusedPolicy(_model(87, 21, [512, 256, 128], seed=1))
+    m = _model(87, 21, [464, 256, 128], seed=2)
+    fp = ops.FusedPolicy(m)
+    fp.pack()
+    obs = torch.randn((300, 87), device="cuda")
+    mu_o = torch.empty((300, 21), device="cuda")
+    val_o = torch.empty((300, 1), device="cuda")
+    fp.step(obs, mu=mu_o, values=val_o)
+    torch.cuda.synchronize()
+    mu, _, val = _ref(m, obs)
+    _close(mu_o, mu, "mu (464 wide)")
+    _close(val_o.squeeze(-1), val, "value (464 wide)")
+
+
 def test_fused_policy_without_normalisation_and_partial_outputs(gpu):
     O, A, units = NETS["Humanoid"]
     m = _model(O, A, units, seed=5, norm=False)

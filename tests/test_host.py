@@ -62,6 +62,28 @@ def test_sim_config_params():
     assert cpu.config["sim_device"] == "cpu"
 
 
+def test_sleep_and_stabilization_are_validated_and_reported():
+    """the task YAMLs enable sleeping / stabilization (Humanoid.yaml:60-61,86-87).
+    The native solver does not model them (DESIGN §5 "PhysX knobs"): they are read with the
+    actor overrides, range-checked as PhysX would, and reported once per process."""
+    from omniisaacgymenvs_amd.utils.config_utils import sim_config as SC
+
+    SC._warned.clear()
+    sc = SimConfig(compose(["task=Humanoid"]))
+    with pytest.warns(UserWarning, match="enable_sleeping"):
+        sc.mi_sim_params("Humanoid")
+    u = sc.unmodelled("Humanoid")
+    assert u["enable_sleeping"] and u["enable_stabilization"]
+    assert u["sleep_threshold"] == 0.005 and u["stabilization_threshold"] == 0.001   # :86-87
+    assert u["friction_offset_threshold"] == 0.04 and u["bounce_threshold_velocity"] == 0.2
+    bad = SimConfig(compose(["task=Humanoid", "task.sim.Humanoid.sleep_threshold=-0.5"]))
+    with pytest.raises(ValueError, match="sleep_threshold"):
+        bad.mi_sim_params("Humanoid")
+    off = SimConfig(compose(["task=Ant", "task.sim.physx.enable_sleeping=False",
+                             "task.sim.physx.enable_stabilization=False"])).unmodelled("Ant")
+    assert not off["enable_sleeping"] and not off["enable_stabilization"]
+
+
 # ---------------------------------------------------------------- models
 def test_humanoid_bfs_order_matches_gear_table():
     m = load_robot("Humanoid")

@@ -54,16 +54,25 @@ def main():
                   "sensors": slice(12 + 2 * D, 12 + 2 * D + 6 * S), "actions": slice(12 + 2 * D + 6 * S, None)}
     gerr = {g: [] for g in list(groups) + ["rew"]}
     gsens = {g: [] for g in list(groups) + ["rew"]}
-    errs, margins, senss = [], [], []
+    errs, margins, senss, pmargins = [], [], [], []
     grel = {g: [] for g in groups}
     gmag = {g: [] for g in groups}
     potmag = []
+    rew_refs = []
+    probe_sens = {}
+    n_probes = int(os.environ.get("PARITY_PROBES", "0")) or PB.SENS_PROBES
     widen_steps = []
     for k in range(3, 3 + steps):
         b = task_buffers(env)
         a = acts(k)
         # oracle-side conditioning of this step (tests/helpers.py oracle_sensitivity)
-        sg, sr, _ = oracle_sensitivity(env, 3, a.cpu().numpy(), task.control_frequency_inv, b, groups)
+        pp = []
+        sg, sr, _ = oracle_sensitivity(env, 3, a.cpu().numpy(), task.control_frequency_inv, b, groups,
+                                       probes=n_probes, per_probe=pp)
+        for j, (og, rg) in enumerate(pp):
+            for g in groups:
+                probe_sens.setdefault(f"{g}_p{j}", []).append(og[g].astype(np.float32))
+            probe_sens.setdefault(f"rew_p{j}", []).append(rg.astype(np.float32))
         for g in groups:
             gsens[g].append(sg[g])
         gsens["rew"].append(sr)
@@ -80,9 +89,11 @@ def main():
             gmag[g].append(np.abs(b["obs"][:, sl]).max(axis=1))
         potmag.append(np.maximum(np.abs(b["pot"]), np.abs(b["prev"])))
         gerr["rew"].append(rd)
+        rew_refs.append(np.asarray(b["rew"], np.float64).copy())
         e = np.maximum(od.max(axis=1), rd)
         errs.append(e)
         margins.append(orc.decision_margin().copy())
+        pmargins.append(orc.projection_margin().copy())
         if task_name != "Cartpole":   # the bounded check of tests/parity_bounds.py, reported per step
             ev = PB.evaluate(PB.bounds_key(task_name, env.task.get_robot().sim_params.solver_type), groups, o["obs"].cpu().numpy(), r.cpu().numpy(), b["obs"], b["rew"],
                              margins[-1], sens=senss[-1],
@@ -100,13 +111,19 @@ def main():
     e = np.concatenate(errs)
     m = np.concatenate(margins)
     sens = np.concatenate(senss)
+    pm_all = np.concatenate(pmargins)
     q = {f"q{p}": float(np.quantile(e, p / 100)) for p in (50, 90, 99, 99.9)}
     far = m >= 1e-4
     worst = np.argsort(-np.where(far, e, 0))[:8]
-    out = {"task": task_name, "envs": n, "steps": steps, **q, "max": float(e.max()),
+    out = {"task": task_name, "envs": n, "steps": steps, "sens_probes": n_probes, **q, "max": float(e.max()),
            "max_far_from_threshold": float(e[far].max()) if far.any() else None,
            "frac_gt_2e-3_far": float((e[far] > 2e-3).mean()) if far.any() else None,
-           "worst_far": [(int(i % n), int(i // n), float(e[i]), float(m[i]), float(sens[i])) for i in worst],
+           # (env, step, error, decision margin, oracle 2-ulp sensitivity, projection margin:
+           # min |unprojected lambda - bound| x A_rr over the env's row projections, m/s)
+           "worst_far": [(int(i % n), int(i // n), float(e[i]), float(m[i]), float(sens[i]), float(pm_all[i]))
+                         for i in worst],
+           "projection_margin_quantiles_far": {f"q{p}": float(np.quantile(pm_all[far], p / 100))
+                                               for p in (1, 10, 50)} if far.any() else None,
            # far envs: error vs the oracle's own rounding sensitivity (2-ulp input perturbation)
            "sens_quantiles": {f"q{p}": float(np.quantile(sens, p / 100)) for p in (50, 99, 99.9)},
            "ratio_err_over_sens_far": {f"q{p}": float(np.quantile(e[far] / np.maximum(sens[far], 1e-7), p / 100))
@@ -139,6 +156,19 @@ def main():
         out["groups"][g]["max_far_mixed_rel"] = float(rel[far].max()) if far.any() else None
         out["groups"][g]["worst_far_abs_with_mag"] = [float(ab[w]), float(mag[w])]
     print(json.dumps(out), flush=True)
+    dump = os.environ.get("PARITY_DUMP")
+    if dump:   # per env-step arrays for offline bound analysis (tools/parity_bounds_fit.py)
+        arrs = {"margin": m, "pmargin": pm_all, "sens_env": sens}
+        for g in gerr:
+            arrs[f"err_{g}"] = np.concatenate(gerr[g]).astype(np.float32)
+            arrs[f"sens_{g}"] = np.concatenate(gsens[g]).astype(np.float32)
+        for g in groups:
+            arrs[f"mag_{g}"] = np.concatenate(gmag[g]).astype(np.float32)
+        arrs["mag_rew"] = np.concatenate([np.abs(x) for x in rew_refs]).astype(np.float32)
+        arrs["pot"] = np.concatenate(potmag).astype(np.float32) if potmag else np.zeros(0, np.float32)
+        for k, v in probe_sens.items():
+            arrs[f"probe_{k}"] = np.concatenate(v)
+        np.savez_compressed(dump, **arrs)
     orc.close()
     env.close()
 
