@@ -15,8 +15,9 @@ timed window starts a fresh horizon and ends by gathering any partial one, so ev
 holds at least one complete gather whatever --steps is.
 
 Prints ONE JSON line (rank 0). `roofline` is for the dominant kernel — the launch the fused
-step runs, named in the line (Humanoid / Ant: k_env_step_pair<TopoCT<Robot*>>, two envs per
-wavefront; Cartpole: k_env_step) — timed with HIP events carried by its own dispatch on the
+step runs, named in the line (Humanoid / Ant: k_env_step_pair<Tgs<TopoCT<Robot*>>> under the
+reference's TGS solver, k_env_step_pair<TopoCT<Robot*>> under PGS, two envs per wavefront;
+Cartpole: k_env_step) — timed with HIP events carried by its own dispatch on the
 stream it is launched on; `cpu_baseline` times the CPU oracle (the build's C restatement; the
 reference's PhysX CPU path is closed and absent) on host cores.
 """
@@ -268,8 +269,10 @@ def kernel_name(view, task) -> str:
     from omniisaacgymenvs_amd import native as N
     path, topo, _ = view.sim_kernel_path()
     if path in (1, 2) and task.task_params().task_kind != N.MI_TASK_CARTPOLE:   # wave / paired path
-        return ("k_env_step_wave<" if path == 1 else "k_env_step_pair<") + {
-            0: "TopoRuntime", 1: "TopoCT<RobotHumanoid>", 2: "TopoCT<RobotAnt>"}.get(topo, str(topo)) + ">"
+        t = {0: "TopoRuntime", 1: "TopoCT<RobotHumanoid>", 2: "TopoCT<RobotAnt>"}.get(topo, str(topo))
+        if view.sim_params.solver_type == N.MI_SOLVER_TGS:   # the Tgs<> instantiation (with_topo)
+            t = f"Tgs<{t}>"
+        return ("k_env_step_wave<" if path == 1 else "k_env_step_pair<") + t + ">"
     return "k_env_step"
 
 
@@ -300,6 +303,9 @@ def read_traffic(task_name: str):
             d = json.load(f)
         split = {k: d[k] for k in ("instruction_fetch_bytes", "data_read_bytes", "write_bytes_at_n")
                  if k in d}
+        split["source"] = (f"committed PMC profile profiles/traffic_{task_name}.json "
+                           f"({d.get('profile', 'rocprofv3 FETCH_SIZE / WRITE_SIZE env-count sweep')}), "
+                           "not measured in this run")
         return d.get("bytes_per_launch"), d.get("bytes_per_launch_uncorrected"), split
     return None, None, {}
 

@@ -133,7 +133,11 @@ MI_D void sdof_loop(const float* Ss, const float* R, F&& fn) {
 #define MI_PAIR_WIDE_PD 16   // W-row prefetch depth of the wide Delassus set-up (A/B round 4: 4 0.1360, 8 0.1335, 12 0.1331 ms; later 12 0.1240, 16 0.1226)
 #endif
 #ifndef MI_PAIR_WIDE_AREG
-#define MI_PAIR_WIDE_AREG 32   // wide-PGS Delassus rows in registers (0, 32 or 64); the rest streamed
+// wide-PGS Delassus rows in registers (a multiple of 4, <= 64); the rest streamed from the wave's
+// scratch. 28 since round 6: at 32 the TGS kernel spilled 16 B of VGPRs per lane (stored once
+// per wave: 512 B/env of scratch writes, 1 241 B/env of WRITE_SIZE); at 28 it is spill-free
+// (863 B/env) for +0.3 % kernel time (alternating A/B, profiles/r06/ab_areg/)
+#define MI_PAIR_WIDE_AREG 28
 #endif
 #ifndef MI_PAIR_WIDE_MFMA_HOIST
 #define MI_PAIR_WIDE_MFMA_HOIST 1   // MFMA set-up: all row blocks' J operands loaded before the tiles
@@ -148,6 +152,9 @@ MI_D void sdof_loop(const float* Ss, const float* R, F&& fn) {
 constexpr int kWideScratchRows = MI_PAIR_WIDE_MFMA ? 64 + 32 : 64 - MI_PAIR_WIDE_AREG;
 #ifndef MI_PAIR_WIDE_AP
 #define MI_PAIR_WIDE_AP 8   // Delassus rows streamed ahead of the wide sweeps' chain
+#endif
+#ifndef MI_PAIR_WIDE_UPF
+#define MI_PAIR_WIDE_UPF 1   // wide u update: next group's W column loaded ahead (0: in order)
 #endif
 #ifndef MI_PAIR_LIM_NEAR
 #define MI_PAIR_LIM_NEAR 0.05f   // rad / m: a joint this close to a limit is speculated on first
@@ -277,8 +284,7 @@ MI_D void pair_wcol(const WaveTabs& t, const float* sm, const float* gW, int g0,
 template <class TP>
 MI_D void pair_artic_substep(const DevModel& m, const WaveTabs& t, const DevState& st,
                              const SimP& p, int i, int wv_, const float* mcb, float* sm, float* gW,
-                             bool load_state, bool store_state, int& prio, int& load,
-                             bool store_sens = true) {
+                             bool load_state, bool store_state, int& prio, int& load) {
     static_assert(TP::kCT && TP::nv <= 32, "paired kernel: compiled topology, nv <= 32");
     const int lane = pair_l64() & 31;
     const int N = st.N, L = m.L, D = m.D, nv = m.nv, nr = m.nr;
@@ -1050,11 +1056,24 @@ MI_D void pair_artic_substep(const DevModel& m, const WaveTabs& t, const DevStat
             float u = ush[kc];
             [[maybe_unused]] float ub = u;
             [[maybe_unused]] const float lbar = lsum / (float)p.iters;
+#if MI_PAIR_WIDE_UPF
+            // the next group's W column is loaded before this group's FMAs (rows past the LDS
+            // ones come from the slab: one L2 round trip per group on the chain otherwise)
+            float wn[4] = {0.0f, 0.0f, 0.0f, 0.0f};
+            pair_wcol(t, smh, gWh, 0, kc, NV, wn);
+#endif
             sfor<0, 16>([&](auto G) {
                 constexpr int g0 = 4 * G;
                 if (g0 < nrh) {
                     float wq[4];
+#if MI_PAIR_WIDE_UPF
+#pragma unroll
+                    for (int q = 0; q < 4; ++q) wq[q] = wn[q];
+                    if constexpr (g0 + 4 < 64)
+                        if (g0 + 4 < nrh) pair_wcol(t, smh, gWh, g0 + 4, kc, NV, wn);
+#else
                     pair_wcol(t, smh, gWh, g0, kc, NV, wq);
+#endif
 #pragma unroll
                     for (int q = 0; q < 4; ++q) {
                         const float lq = readlane(lam, g0 + q);
@@ -1341,9 +1360,7 @@ MI_D void pair_artic_substep(const DevModel& m, const WaveTabs& t, const DevStat
         sm[t.s_q + lane] = qn;
         finite = isfinite(v) && isfinite(qn);
     }
-    // (store_sens false: the staged fused step's workgroup writes the sensor rows from s_rb
-    // after its barrier, pair_stage_flush)
-    if (store_state && store_sens && lane < 6 * m.S) st.sens[ssx(st, lane, i)] = sm[t.s_rb + lane];
+    if (store_state && lane < 6 * m.S) st.sens[ssx(st, lane, i)] = sm[t.s_rb + lane];
     if (nr && lane == 0) {
         float u6[6], p6[6], rp[3], rq[4];
 #pragma unroll
@@ -1414,8 +1431,7 @@ MI_D void pair_artic_substep(const DevModel& m, const WaveTabs& t, const DevStat
 // of this lane's half (lane = lane & 31; the half's lane 0 does the sequential parts).
 MI_D float pair_task_pre(const DevModel& m, const DevState& st, const DevTask& tp, int i,
                          const float* actions, int64_t* reset_buf, int64_t* progress_buf,
-                         float* potentials, float* prev_potentials, float* actions_out,
-                         bool staged = false) {
+                         float* potentials, float* prev_potentials, float* actions_out) {
 #pragma clang fp contract(off)
     const int lane = pair_l64() & 31, N = st.N, D = m.D, A = tp.A;
     const bool flagged = reset_buf[i] != 0;      // half-uniform
@@ -1460,7 +1476,7 @@ MI_D float pair_task_pre(const DevModel& m, const DevState& st, const DevTask& t
         const int j = lane;
         a = clampf(actions[(size_t)A * i + j], -tp.clip_actions, tp.clip_actions);
         if (tp.dr_act) a = dr_col(st, tp, 1, dre, i, j, a);
-        if (actions_out && !staged) actions_out[(size_t)A * i + j] = a;   // staged: post-step
+        if (actions_out) actions_out[(size_t)A * i + j] = a;
         st.eff[sx(st, j, i)] = a * tp.gears[j] * tp.power_scale;
     }
     if (tp.dr_act && lane == 0) dr_store(st, 1, i, dre);
@@ -1471,13 +1487,9 @@ MI_D void pair_loco_post(const DevModel& m, const WaveTabs& t, const DevState& s
                          const DevTask& tp, int i, float* sm, float a_lane,
                          float* obs_out, float* obs_task, float* rew, int64_t* reset_buf,
                          int64_t* progress_buf, float* potentials, float* prev_potentials,
-                         float* rew_out, int64_t* reset_out, bool staged = false) {
+                         float* rew_out, int64_t* reset_out) {
 #pragma clang fp contract(off)
     const int lane = pair_l64() & 31, D = m.D, S = m.S, O = tp.O;
-    // staged (t.stage_out, the fused step): the env's outputs go to its dead W rows — obs row
-    // [0, O) unclamped, reward / done / progress / potentials at O.., task.actions at O + 8 ..,
-    // the env index at O + 7 — and pair_stage_flush writes the workgroup's rows in env order
-    float* stg = sm + t.s_W;
     const int h0 = pair_l64() & 32;
     const float co = tp.clip_obs;
     const float* us = sm + t.s_us;
@@ -1498,10 +1510,6 @@ MI_D void pair_loco_post(const DevModel& m, const WaveTabs& t, const DevState& s
     if (tp.dr_obs) dre = dr_begin(st, tp, 0, i, done != 0);
     auto put = [&](int k, float v) {
         if (tp.dr_obs) v = dr_col(st, tp, 0, dre, i, k, v);
-        if (staged) {
-            stg[k] = v;
-            return;
-        }
         if (raw) raw[k] = v;
         out[k] = clampf(v, -co, co);
     };
@@ -1514,7 +1522,6 @@ MI_D void pair_loco_post(const DevModel& m, const WaveTabs& t, const DevState& s
         put(12 + j, pos);
         put(12 + D + j, vel);
         put(12 + 2 * D + 6 * S + j, a);
-        if (staged) stg[O + 8 + j] = a;   // task.actions (locomotion: A == D)
         terms[j] = a * a;
         terms[D + j] = fabsf(a * vel) * tp.ratio[j];
         if (tp.kind == MI_TASK_HUMANOID) {
@@ -1590,10 +1597,8 @@ MI_D void pair_loco_post(const DevModel& m, const WaveTabs& t, const DevState& s
         put(6, al[2] * tp.angular_velocity_scale);
         put(10, o10);
         put(11, o11);
-        if (!staged) {
-            potentials[i] = new_p;
-            prev_potentials[i] = prev_p;
-        }
+        potentials[i] = new_p;
+        prev_potentials[i] = prev_p;
         const float heading = o11 > 0.8f ? tp.heading_weight : tp.heading_weight * o11 / 0.8f;
         const float upr = o10 > 0.93f ? 0.0f + tp.up_weight : 0.0f;
         float total = (new_p - prev_p) + tp.alive_reward_scale + upr + heading -
@@ -1604,15 +1609,6 @@ MI_D void pair_loco_post(const DevModel& m, const WaveTabs& t, const DevState& s
             atomicAdd(st.nan_total, 1ull);
         }
         if (tp.dr_obs) dr_store(st, 0, i, dre);
-        if (staged) {
-            stg[O + 0] = total;
-            stg[O + 1] = __int_as_float((int)done);
-            stg[O + 2] = __int_as_float((int)progress);
-            stg[O + 3] = new_p;
-            stg[O + 4] = prev_p;
-            stg[O + 7] = __int_as_float(i);
-            return;
-        }
         rew[i] = total;
         reset_buf[i] = done;
         progress_buf[i] = progress;

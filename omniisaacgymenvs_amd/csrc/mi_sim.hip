@@ -851,78 +851,6 @@ __global__ __launch_bounds__(512) MI_PAIR_OCC void k_sim_step_pair(const KParams
     }
 }
 
-// The staged fused step's output pass (t.stage_out): after the workgroup barrier,
-// the 512 threads write the 16 envs' rows — contiguous env range e0 .. e0 + 15 whatever the
-// pairing — in env order: obs [16][O], task.actions [16][A], sensor wrenches [16][6S] and the
-// per-env scalars as whole 128-B lines, instead of each half-wave writing its own env's rows
-// (with pairing by load, adjacent envs' rows share lines but sit in different waves, so every
-// row boundary reached HBM as two partial-line writes: 1 241 B/env of writes vs 860 before).
-// Each env's staged rows are in the dead W rows of the LDS slot that stepped it; lane r (< 16)
-// of every wave finds env e0 + r's slot from the 16 slots' env headers.
-__device__ __forceinline__ void pair_stage_flush(const DevModel& m, const WaveTabs& t, const DevState& st,
-                                                 const DevTask& tp, const float* smem, float* obs_out,
-                                                 float* obs_task, float* rew, int64_t* reset_buf,
-                                                 int64_t* progress_buf, float* pot, float* prev,
-                                                 float* actions_out, float* rew_out, int64_t* reset_out) {
-    const int tid = (int)threadIdx.x, lane = tid & 63, O = tp.O, A = tp.A, S6 = 6 * m.S;
-    const int es = t.env_stride, sw = t.s_W;
-    const int e0 = xcd_block() * 16;
-    const int mine = __float_as_int(smem[(lane & 15) * es + sw + O + 7]);   // env of slot lane & 15
-    int inv = 0;
-#pragma unroll
-    for (int s = 0; s < 16; ++s)
-        inv = __builtin_amdgcn_readlane(mine, s) - e0 == (lane & 15) ? s : inv;
-    auto slot = [&](int r) { return __shfl(inv, r); };   // LDS slot of env e0 + r (r < 16)
-    const float co = tp.clip_obs;
-    float* ob = obs_out + (size_t)e0 * O;
-    float* ot = obs_task ? obs_task + (size_t)e0 * O : nullptr;
-    for (int f = tid; f < 16 * O; f += 512) {
-        const int r = f / O, c = f - r * O;
-        const float v = smem[slot(r) * es + sw + c];
-        if (ot) ot[f] = v;
-        ob[f] = clampf(v, -co, co);
-    }
-    if (actions_out) {
-        float* ao = actions_out + (size_t)e0 * A;
-        for (int f = tid; f < 16 * A; f += 512) {
-            const int r = f / A, c = f - r * A;
-            ao[f] = smem[slot(r) * es + sw + O + 8 + c];
-        }
-    }
-    if (st.ses == S6 && st.sfs == 1) {   // [N][6S] sensor rows (record layout)
-        float* so = st.sens + (size_t)e0 * S6;
-        for (int f = tid; f < 16 * S6; f += 512) {
-            const int r = f / S6, c = f - r * S6;
-            so[f] = smem[slot(r) * es + t.s_rb + c];
-        }
-    } else {
-        for (int f = tid; f < 16 * S6; f += 512) {
-            const int r = f / S6, c = f - r * S6;
-            st.sens[ssx(st, c, e0 + r)] = smem[slot(r) * es + t.s_rb + c];
-        }
-    }
-    // per-env scalars: wave 0's lanes, 16 lanes per field group (one or two whole lines each)
-    if (tid < 64) {
-        const int r = lane & 15, g = lane >> 4;
-        const float* sr = smem + slot(r) * es + sw + O;
-        const int e = e0 + r;
-        if (g == 0) {
-            rew[e] = sr[0];
-            if (rew_out) rew_out[e] = sr[0];
-            st.load[e] = __float_as_int(sr[5]);
-        } else if (g == 1) {
-            const int64_t d = __float_as_int(sr[1]);
-            reset_buf[e] = d;
-            if (reset_out) reset_out[e] = d;
-        } else if (g == 2) {
-            progress_buf[e] = __float_as_int(sr[2]);
-        } else {
-            pot[e] = sr[3];
-            prev[e] = sr[4];
-        }
-    }
-}
-
 template <class T>
 __global__ __launch_bounds__(512) MI_PAIR_OCC void k_env_step_pair(const KParams* __restrict__ kp,
                                                     const float* actions, int substeps,
@@ -939,9 +867,8 @@ __global__ __launch_bounds__(512) MI_PAIR_OCC void k_env_step_pair(const KParams
     const int i = live ? pair_env_by_load(st) : pair_env();
     STAMP_BEGIN();
     float a_lane = 0.0f;
-    const bool staged = t.stage_out != 0;   // launch-uniform (all waves live: N % 16 == 0)
     if (live)
-        a_lane = pair_task_pre(m, st, tp, i, actions, reset_buf, progress_buf, pot, prev, actions_out, staged);
+        a_lane = pair_task_pre(m, st, tp, i, actions, reset_buf, progress_buf, pot, prev, actions_out);
     stage_model_constants(t, smem);
     if (!live) return;
     STAMP(13);
@@ -952,22 +879,14 @@ __global__ __launch_bounds__(512) MI_PAIR_OCC void k_env_step_pair(const KParams
     for (int s = 0; s < substeps; ++s) {
         const KParams* k = opaque_kp(kp);
         pair_artic_substep<T>(k->m, k->t, k->st, k->p, i, pair_wave(), smem, sm, gW, s == 0, s == substeps - 1,
-                              prio, load, !staged);
+                              prio, load);
     }
     STAMP_RESET();
     pair_loco_post(m, t, st, tp, i, sm, a_lane, obs_out, obs_task, rew, reset_buf, progress_buf,
-                   pot, prev, rew_out, reset_out, staged);
+                   pot, prev, rew_out, reset_out);
     // the next fused step pairs by it (only the fused step writes it: World.step launches of one
     // env-step, deferred or not, all see the same pairing)
-    if (staged) {
-        if ((threadIdx.x & 31u) == 0) sm[t.s_W + tp.O + 5] = __int_as_float(load);
-        __syncthreads();   // every env of the workgroup staged (waves that finished early wait here)
-        const KParams* k = opaque_kp(kp);
-        pair_stage_flush(k->m, k->t, k->st, k->tp, smem, obs_out, obs_task, rew, reset_buf, progress_buf,
-                         pot, prev, actions_out, rew_out, reset_out);
-    } else if ((threadIdx.x & 31u) == 0) {
-        st.load[i] = load;
-    }
+    if ((threadIdx.x & 31u) == 0) st.load[i] = load;
     STAMP(14);
 }
 
@@ -2018,14 +1937,6 @@ int mi_task_configure(mi_sim* s, const mi_task_params* t) {
         d.ratio[j] = t->motor_effort_ratio ? t->motor_effort_ratio[j] : 1.0f;
     }
     for (int j = 0; j < D && j < MI_MAXA; ++j) d.init_dof[j] = t->init_dof_pos ? t->init_dof_pos[j] : 0.0f;
-    {   // staged outputs of the paired fused step (k_env_step_pair, pair_stage_flush): full
-        // workgroups only (the flush's barrier needs every wave), and room in the dead W rows for
-        // the obs row + 8 scalars + task.actions; MI_STAGE_OUT=0 turns it off (A/B)
-        const char* e = getenv("MI_STAGE_OUT");
-        const bool want = !e || atoi(e) != 0;
-        s->wt.stage_out = want && s->wave && s->pair && d.kind != MI_TASK_CARTPOLE && s->N % 16 == 0 &&
-                          d.O + 8 + d.A <= s->wt.w_rows_lds * s->dm.nv ? 1 : 0;
-    }
     s->task_ok = true;
     if (int rc = sync_kparams(s)) return rc;
     return MI_OK;

@@ -143,11 +143,6 @@ struct WaveTabs {
     int sens_par;
     // paired-env kernels: per-wave Delassus scratch of the wide PGS ([N / 2][64][64] floats)
     float* g_wa;
-    // paired fused env step: the per-env outputs (obs row, reward / reset / progress /
-    // potentials, task.actions, sensor wrenches, pairing load) are staged in the env's dead W
-    // rows (s_W) and written by the whole workgroup in env order as whole lines after a barrier
-    // (k_env_step_pair, pair_stage_flush); 0: each half-wave writes its own env's rows
-    int stage_out;
 };
 
 // Per-model constants in the LDS block, structure-of-arrays so lane-indexed reads (lane = link,

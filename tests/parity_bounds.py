@@ -7,11 +7,15 @@ from a contact / limit decision threshold must be within a per-task, per-field-g
 profiles/r04/parity_stats_<task>.log). Two allowances may widen it, both computed on the ORACLE
 side, never from the device's own error:
   * conditioning: SENS_K x the oracle's response to a 2-ulp perturbation of its own input
-    state (tests/helpers.py oracle_sensitivity) — stacked contacts and near-singular Delassus
-    blocks amplify rounding. Capped at SENS_CAP x max(1, |oracle value|) (1 % of the entry's
-    magnitude: the force sensors read up to ~10 after contactForceScale), and fewer than
-    WIDEN_MAX_FRAC of the envs of a step may NEED it (error above the base bound); the widest
-    bound applied is reported;
+    state, the largest over SENS_PROBES independent perturbations (tests/helpers.py
+    oracle_sensitivity) — stacked contacts and near-singular Delassus blocks amplify rounding.
+    Capped at SENS_CAP x max(1, |oracle value|) (1 % of the entry's magnitude: the force sensors
+    read up to ~10 after contactForceScale), and fewer than WIDEN_MAX_FRAC of the envs of a step
+    may NEED it (error above the base bound); the widest bound applied is reported. The cap
+    cannot be tighter than the reference's own resolution: where the oracle's 2-ulp response
+    ALONE reaches the cap (the entry is undetermined at that level in float32), the bound is
+    SENS_K x that response, and such envs that need it ("beyond the cap") must stay under
+    ILL_MAX_FRAC of the envs (at least one may);
   * the reward carries potentials - prev_potentials with |potentials| ~ 6e4 in float32
     (locomotion.py:223, dt = 1/60): 2 ulp of the potentials is the reward's own quantisation
     (bounded by construction: <= 2 ulp of 1e3 / dt).
@@ -27,7 +31,11 @@ import numpy as np
 DECISION_EPS = 1e-4          # m or rad: a decision this close to its threshold may flip
 NEAR_MAX_FRAC = 0.02         # envs at a threshold that may differ
 SENS_K = 4.0                 # conditioning allowance: this many times the oracle's 2-ulp response
-SENS_PROBES = 1              # ... the largest over this many independent 2-ulp perturbations
+SENS_PROBES = 4              # ... the largest over this many independent 2-ulp perturbations
+                             # (round 6: one random direction under-read the worst direction of
+                             # ill-conditioned steps by up to ~100x, profiles/r06/parity_stats_*)
+ILL_MAX_FRAC = 1e-3          # envs per step whose error passes the cap because the oracle's own
+                             # response does (bound SENS_K x response)
 SENS_CAP = 1e-2              # ... never above this x max(1, |oracle value|)
 WIDEN_MAX_FRAC = 0.01        # envs per step that may need the conditioning allowance
 CARTPOLE_TOL = 1e-4
@@ -52,21 +60,19 @@ GROUP_TOL = {
 }
 GROUP_TOL["AntSelf"] = GROUP_TOL["Humanoid"]
 
-# TGS (include/mi_sim.h MI_SOLVER_TGS; cfg/config.yaml solver_type: 1, the default): the device
-# forms the positions' mean velocity as u* + W (sum of the sub-steps' lambdas) / iters in
-# Delassus space, the oracle as the mean of its u-space sub-step velocities — one more rounding
-# path than PGS, and the sub-steps' biases keep more rows at their projection bounds, where a
-# rounding-level difference flips a clamp. Measured (profiles/r05/parity_stats_<task>_tgs.log,
-# 4 steps x 4096 envs): the bulk is PGS's (median / q99 of every group within 1-4x of PGS's), the
-# far tail is 4-20x PGS's and sits in a handful of envs (Humanoid: dof_vel 5.3e-3 and sensors
-# 1.1e-2 in 2 envs of 16384, error 28x the oracle's own 2-ulp response, so outside the
-# conditioning allowance; Ant: root 1.4e-3). Base bounds: 4x the measured far maximum, or 1.5x
-# where that maximum is a single-env outlier (Humanoid dof_vel / sensors, Ant root / sensors);
-# the median / q99 detectors stay at ~4x the measured bulk. Keyed "<task>/TGS".
-FAR_TOL["Humanoid/TGS"] = {"root": 8e-4, "dof_pos": 6e-4, "dof_vel": 8e-3, "sensors": 1.6e-2, "actions": 0.0,
-                           "rew": 4e-4}
-FAR_TOL["Ant/TGS"] = {"root": 2.2e-3, "dof_pos": 4e-5, "dof_vel": 3e-3, "sensors": 4.5e-3, "actions": 0.0,
-                      "rew": 8e-5}
+# TGS (include/mi_sim.h MI_SOLVER_TGS; cfg/config.yaml solver_type: 1, the default). Round 6:
+# the oracle runs TGS in the device's Delassus-space form (oracle.c tgs_delassus: carried row
+# velocities, u-bar = u* + W (sum of the sub-steps' lambdas) / iters in row order), and the
+# conditioning probe takes the largest of SENS_PROBES perturbations (quaternion included).
+# Measured with both (profiles/r06/parity_stats_<task>_tgs.log, 8 steps x 4096 envs): every far
+# env above the PGS base bound is within 2.0x of its own oracle-side response; TGS's far tail is
+# larger than PGS's because TGS's steps are worse conditioned (position sub-steps at gain 1 / h
+# = 4 / dt), not because the device departs from the oracle (the projection margins of the worst
+# envs are not small: no clamp flips). So the base bounds are PGS's x 1.5, derived like PGS's
+# (the oracle-side allowance covers the ill-conditioned envs); only the median / q99 detectors
+# are TGS's own (~4x its measured bulk). Keyed "<task>/TGS".
+FAR_TOL["Humanoid/TGS"] = {g: 1.5 * v for g, v in FAR_TOL["Humanoid"].items()}
+FAR_TOL["Ant/TGS"] = {g: 1.5 * v for g, v in FAR_TOL["Ant"].items()}
 GROUP_TOL["Humanoid/TGS"] = {"root": (2e-5, 1e-4), "dof_pos": (1e-5, 5e-5), "dof_vel": (5e-5, 1.2e-3),
                              "sensors": (5e-5, 4e-3), "actions": (0.0, 0.0), "rew": (2e-6, 5e-5)}
 GROUP_TOL["Ant/TGS"] = {"root": (6e-6, 2e-4), "dof_pos": (1e-6, 5e-6), "dof_vel": (3e-6, 2.5e-4),
@@ -97,27 +103,34 @@ def evaluate(name: str, groups: Dict[str, slice], obs, rew, obs_ref, rew_ref, ma
     err["rew"] = np.abs(np.asarray(rew, np.float64) - np.asarray(rew_ref, np.float64))
     mag = {g: np.abs(obs_ref[:, sl]).max(axis=1) for g, sl in groups.items()}
     mag["rew"] = np.abs(np.asarray(rew_ref, np.float64))
-    sk = np.zeros(n) if sens is None else SENS_K * np.asarray(sens, np.float64)
-    out = {"err": err, "near": near, "base": {}, "bound": {}, "over": {}, "needed_widening": {}}
+    sraw = np.zeros(n) if sens is None else np.asarray(sens, np.float64)
+    sk = SENS_K * sraw
+    out = {"err": err, "near": near, "base": {}, "bound": {}, "over": {}, "needed_widening": {},
+           "beyond_cap": {}}
     pot_allow = None
     if pot is not None:
         pot_allow = 2.0 * np.spacing(np.asarray(pot, np.float32)).astype(np.float64)
     any_needed = np.zeros(n, bool)
+    any_beyond = np.zeros(n, bool)
     widest = 0.0
     for g, e in err.items():
         base = np.full(n, FAR_TOL[name][g])
         if g == "rew" and pot_allow is not None:
             base = np.maximum(base, pot_allow)
-        widen = np.minimum(sk, SENS_CAP * np.maximum(1.0, mag[g]))
-        bound = np.maximum(base, widen)
+        cap = SENS_CAP * np.maximum(1.0, mag[g])
+        capped = np.maximum(base, np.minimum(sk, cap))
+        bound = np.where(sraw >= cap, np.maximum(base, sk), capped)   # the oracle alone reaches the cap
         needed = (e > base) & (e <= bound) & ~near
+        beyond = (e > capped) & (e <= bound) & ~near
         over = (e > bound) & ~near
         out["base"][g], out["bound"][g] = base, bound
-        out["over"][g], out["needed_widening"][g] = over, needed
+        out["over"][g], out["needed_widening"][g], out["beyond_cap"][g] = over, needed, beyond
         any_needed |= needed
+        any_beyond |= beyond
         if needed.any():
             widest = max(widest, float(bound[needed].max()))
     out["any_needed"] = any_needed
+    out["any_beyond_cap"] = any_beyond
     out["widest_applied"] = widest
     out["near_differ"] = near & np.any(np.stack([e > out["bound"][g] for g, e in err.items()]), axis=0)
     return out
@@ -139,10 +152,12 @@ def check(name: str, groups: Dict[str, slice], obs, rew, obs_ref, rew_ref, margi
             f"{name} {g}: env {np.nonzero(bad)[0][0]} error {e[bad][0]:.3g} > {r['bound'][g][bad][0]:.3g} "
             f"(base {r['base'][g][bad][0]:.3g})")
     k = int(r["any_needed"].sum())
+    kb = int(r["any_beyond_cap"].sum())
     if log is not None:
-        log(f"[parity] {name}: {n} envs, {k} needed the conditioning allowance, widest bound applied "
-            f"{r['widest_applied']:.3g}, {int(r['near'].sum())} at a threshold "
+        log(f"[parity] {name}: {n} envs, {k} needed the conditioning allowance ({kb} beyond the cap), "
+            f"widest bound applied {r['widest_applied']:.3g}, {int(r['near'].sum())} at a threshold "
             f"({int(r['near_differ'].sum())} differ)")
     assert k < max(1.0, WIDEN_MAX_FRAC * n), f"{name}: {k} of {n} envs needed the conditioning allowance"
+    assert kb < max(2.0, ILL_MAX_FRAC * n), f"{name}: {kb} of {n} envs needed an allowance beyond the cap"
     assert r["near_differ"].mean() < NEAR_MAX_FRAC, f"{name}: {int(r['near_differ'].sum())} envs at a threshold differ"
     return r

@@ -40,7 +40,7 @@ def test_allowance_is_capped():
     ref, rr, obs, rew, margin, sens = _case()
     ref[7, 0] = obs[7, 0] = 0.5
     obs[7, 0] += 0.05
-    sens[7] = 1.0                       # 4 x sens = 4 would allow it: the cap (1e-2) does not
+    sens[7] = 5e-3                      # 4 x sens = 0.02 would allow it: the cap (1e-2) does not
     with pytest.raises(AssertionError, match="root"):
         PB.check("Humanoid", G, obs, rew, ref, rr, margin, sens=sens, quantiles=False, log=None)
 
@@ -52,12 +52,47 @@ def test_allowance_cap_scales_with_magnitude():
     ref[4, sl.start] = 5.0              # a 5-unit force reading: the cap is 1 % of it
     obs[4, sl] = ref[4, sl]
     obs[4, sl.start] += 0.04
-    sens[4] = 1.0
+    sens[4] = 0.04                      # below the cap (0.05): 4 x sens is capped
     r = PB.check("Humanoid", G, obs, rew, ref, rr, margin, sens=sens, quantiles=False, log=None)
     assert r["widest_applied"] == pytest.approx(0.05)
     obs[4, sl.start] += 0.02            # 0.06 > 1 % of 5
     with pytest.raises(AssertionError, match="sensors"):
         PB.check("Humanoid", G, obs, rew, ref, rr, margin, sens=sens, quantiles=False, log=None)
+
+
+def test_cap_yields_to_the_oracles_own_resolution():
+    """Where the oracle's own 2-ulp response reaches the cap, the entry is undetermined at that
+    level in float32: the bound is SENS_K x the response, counted as beyond the cap, and only
+    ILL_MAX_FRAC of the envs (at least one) may need it."""
+    ref, rr, obs, rew, margin, sens = _case()
+    sl = G["sensors"]
+    ref[4, sl] = 0.0
+    ref[4, sl.start] = 0.56             # round 6's worst TGS env: error 1.08e-2, response 1.0e-2
+    obs[4, sl] = ref[4, sl]
+    obs[4, sl.start] += 1.08e-2
+    sens[4] = 1.0e-2
+    logs = []
+    r = PB.check("Humanoid", G, obs, rew, ref, rr, margin, sens=sens, quantiles=False, log=logs.append)
+    assert int(r["any_beyond_cap"].sum()) == 1 and "1 beyond the cap" in logs[0]
+    obs[4, sl.start] = 0.56 + 4.1e-2    # past 4 x its response
+    with pytest.raises(AssertionError, match="sensors"):
+        PB.check("Humanoid", G, obs, rew, ref, rr, margin, sens=sens, quantiles=False, log=None)
+    obs[4, sl.start] = 0.56 + 1.08e-2   # two such envs in 1000: over ILL_MAX_FRAC
+    ref[9, sl] = 0.0
+    ref[9, sl.start] = 0.3
+    obs[9, sl] = ref[9, sl]
+    obs[9, sl.start] += 2e-2
+    sens[9] = 1.2e-2
+    with pytest.raises(AssertionError, match="beyond the cap"):
+        PB.check("Humanoid", G, obs, rew, ref, rr, margin, sens=sens, quantiles=False, log=None)
+
+
+def test_tgs_base_bounds_are_pgs_derived():
+    """VERDICT r5 #1: the TGS base bounds are the PGS ones x 1.5 (not fitted to the device)."""
+    for task in ("Humanoid", "Ant"):
+        for g, v in PB.FAR_TOL[task].items():
+            assert PB.FAR_TOL[f"{task}/TGS"][g] == pytest.approx(1.5 * v)
+    assert PB.SENS_PROBES >= 4
 
 
 def test_too_many_envs_needing_the_allowance_fail():

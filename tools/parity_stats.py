@@ -14,6 +14,15 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
 
 
+def _ratio_above(err, sens, far, base):
+    import numpy as np
+
+    if base is None:
+        return None
+    m = far & (err > base)
+    return float((err[m] / np.maximum(sens[m], 1e-6)).max()) if m.any() else 0.0
+
+
 def main():
     import numpy as np
     import torch
@@ -104,6 +113,7 @@ def main():
                 "frac": float(ev["any_needed"].mean()), "widest_bound_applied": ev["widest_applied"],
                 "bounds_applied": sorted(float(x) for x in need_b)[-8:],
                 "over_bound_far": int(sum(int(v.sum()) for v in ev["over"].values())),
+                "beyond_cap": int(ev["any_beyond_cap"].sum()),
                 "near_threshold": int(ev["near"].sum()), "near_differ": int(ev["near_differ"].sum()),
                 "groups_needing": {g: int(v.sum()) for g, v in ev["needed_widening"].items() if v.any()}})
             print(json.dumps({"parity_step": widen_steps[-1]}), flush=True)
@@ -133,7 +143,12 @@ def main():
            "groups": {g: {f"q{p}": float(np.quantile(np.concatenate(v), p / 100)) for p in (50, 99)} |
                       {"max_far": float(np.concatenate(v)[far].max()) if far.any() else None,
                        "max_far_ratio_to_sens": float((np.concatenate(v)[far] / np.maximum(
-                           np.concatenate(gsens[g])[far], 1e-6)).max()) if far.any() else None}
+                           np.concatenate(gsens[g])[far], 1e-6)).max()) if far.any() else None,
+                       # the same over the far envs whose error exceeds the task's PGS base bound
+                       # (the envs an allowance is for; below it no allowance is needed)
+                       "max_ratio_to_sens_above_pgs_base": _ratio_above(
+                           np.concatenate(v), np.concatenate(gsens[g]), far,
+                           PB.FAR_TOL.get(task_name, {}).get(g))}
                       for g, v in gerr.items()}}
     # reward: float32 potentials are ~6e4 (ulp 3.9e-3); the step's reward carries pot - prev
     pm = np.concatenate(potmag) if potmag else None
