@@ -104,6 +104,29 @@ typedef struct {
 int64_t mi_rl_mlp_packed_size(const mi_rl_mlp* mlp);
 /* Repack the network's current weights (stream-ordered; call after every weight update). */
 int32_t mi_rl_mlp_pack(const mi_rl_mlp* mlp, float* packed, void* stream);
+/* The minibatch network of the PPO update (rl_games calc_gradients under autocast fp16,
+ * HumanoidPPO.yaml mixed_precision: True) on fp16 MFMA, one launch each for the forward and for
+ * the dgrad chain; the weight / bias gradients stay split-K GEMMs over the stored layer inputs.
+ * Supported layouts (else packed size -1 and the learner keeps its torch path): 3 hidden ELU
+ * layers 87-400-200-100 with 21 actions (HumanoidPPO.yaml:24-25) or 60-256-128-64 with 8
+ * (AntPPO.yaml). mi_rl_mlp_train_pack: f16 A-operand images of every layer's W (forward) and
+ * W^T (backward) plus the biases, from the f32 masters the descriptor points at (call after every
+ * optimizer step; stream-ordered). */
+int64_t mi_rl_mlp_train_packed_size(const mi_rl_mlp* mlp);   /* halfs, or -1 */
+int32_t mi_rl_mlp_train_pack(const mi_rl_mlp* mlp, void* packed /*f16*/, void* stream);
+/* x [rows][O] f32 (the normalised observations); acts: 4 device buffers, f16 [rows][O + 1],
+ * [rows][H1 + 1], [rows][H2 + 1], [rows][H3 + 1]: each layer's input with a ones column (the
+ * bias column of the weight gradient), each row padded to a multiple of 8 halfs (row stride
+ * (width + 1 + 7) & ~7); mu f16 [rows][A], value f16 [rows] (the heads, as autocast's f16
+ * linears return them). */
+int32_t mi_rl_mlp_train_fwd(const mi_rl_mlp* mlp, const void* packed, const float* x, int32_t rows,
+                            void* const* acts, void* mu, void* value, void* stream);
+/* grad_mu f16 [rows][A], grad_value f16 [rows] (the loss gradient w.r.t. the heads);
+ * grads: 3 device buffers f16 [rows][H1], [rows][H2], [rows][H3], the gradient w.r.t. each hidden
+ * layer's pre-activation (after the ELU derivative, from acts[1..3]). */
+int32_t mi_rl_mlp_train_bwd(const mi_rl_mlp* mlp, const void* packed, void* const* acts,
+                            const void* grad_mu, const void* grad_value, int32_t rows,
+                            void* const* grads, void* stream);
 /* For rows n < num_rows of obs [R][O]: obs_out[n] = obs[n] (the rollout slot; may be NULL);
  * x = clamp((obs - mean) / sqrt(var + eps), +-5) when obs_mean / obs_var (f64 running
  * statistics) are given; mu, v = heads(MLP(x)); values[n] = sqrt(var_v + eps) clamp(v, +-5) +

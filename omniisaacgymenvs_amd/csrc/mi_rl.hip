@@ -726,6 +726,347 @@ __global__ __launch_bounds__(kAdamBlock) void k_adam_apply(mi_rl_adam_cfg c, flo
 }
 }  // namespace
 
+// ---------------------------------------------------------------------------------------
+// Training minibatch MLP on fp16 MFMA (v_mfma_f32_16x16x32_f16): the forward and the dgrad chain
+// of the PPO update's network (rl_games calc_gradients under autocast fp16; HumanoidPPO.yaml
+// mixed_precision: True, units [400, 200, 100], elu), each ONE launch for the whole minibatch.
+//
+// Transposed products, activations in registers. A wave owns 16 minibatch rows and computes
+// D = W . X^T (out features x its 16 rows): the A operand is the weight (packed per minibatch
+// from the f32 masters by mi_rl_mlp_train_pack), the B operand the previous layer's output.
+// D register i of lane l is feature 16 t + 4 (l >> 4) + i of row l & 15, i.e. the layer's output
+// already sits in the lanes the next product's B operand needs, so the layers chain with no LDS
+// round trip: one 32-k step of the next product takes tiles 2 s and 2 s + 1, element j of lane
+// group h being feature 16 (j >> 2) + 4 h + (j & 3) of the step (mlp_perm); the weights are
+// packed in the SAME permuted k order, so every product pairs equal k. Each k-step's weight
+// chunk (T tiles x 1 KB) is staged through LDS by the workgroup's 4 waves (64 rows), double
+// buffered, the next chunk's global loads in flight during the current chunk's MFMAs.
+//
+// Numerics follow torch autocast: f16 operands, f32 accumulation; a linear's bias is added to the
+// f32 accumulator and the sum rounded once to f16; ELU is evaluated in f32 on the f16 value and
+// rounded to f16. Backward: dA = f16(G . W) (f32 accumulation), times the ELU derivative from the
+// stored activation h (1 for h > 0, else h + 1 = exp(z)), rounded once to f16.
+// ---------------------------------------------------------------------------------------
+namespace {
+typedef _Float16 h8 __attribute__((ext_vector_type(8)));
+typedef _Float16 h4 __attribute__((ext_vector_type(4)));
+typedef float mf4 __attribute__((ext_vector_type(4)));
+
+// row stride (halfs) of a stored layer input [rows][N + 1 (ones column)]: padded to 8 halfs, so
+// a lane's 4 consecutive features (D registers 0..3) are one aligned 8-byte access
+__host__ __device__ constexpr int mlp_act_ld(int N) { return (N + 1 + 7) & ~7; }
+
+constexpr int kMlpRows = 64;             // rows per workgroup: 4 waves x 16
+constexpr int kMlpChunk = 512;           // halfs per 16-row tile and 32-k step (64 lanes x 8)
+
+__host__ __device__ constexpr int mlp_perm(int h, int j) { return 16 * (j >> 2) + 4 * h + (j & 3); }
+
+template <int O_, int H1_, int H2_, int H3_, int A_>
+struct MlpShape {
+    static constexpr int O = O_, H1 = H1_, H2 = H2_, H3 = H3_, A = A_, NH = A_ + 1;
+    static constexpr int KS0 = (O + 31) / 32;                  // k-steps of the input
+    static constexpr int T1 = 2 * ((H1 + 31) / 32), T2 = 2 * ((H2 + 31) / 32), T3 = 2 * ((H3 + 31) / 32);
+    static constexpr int TH = (NH + 15) / 16;                  // head tiles (mu rows, value row)
+    static_assert(NH <= 32, "heads: one 32-k step in the backward");
+    // packed sections (halfs), in this order
+    static constexpr long long F1 = 0;
+    static constexpr long long F2 = F1 + (long long)KS0 * T1 * kMlpChunk;
+    static constexpr long long F3 = F2 + (long long)(T1 / 2) * T2 * kMlpChunk;
+    static constexpr long long FH = F3 + (long long)(T2 / 2) * T3 * kMlpChunk;
+    static constexpr long long BH = FH + (long long)(T3 / 2) * TH * kMlpChunk;   // heads^T, 1 k-step
+    static constexpr long long B3 = BH + (long long)T3 * kMlpChunk;
+    static constexpr long long B2 = B3 + (long long)(T3 / 2) * T2 * kMlpChunk;
+    static constexpr long long BIAS = B2 + (long long)(T2 / 2) * T1 * kMlpChunk;
+    static constexpr long long TOTAL = BIAS + 16LL * (T1 + T2 + T3 + TH);
+    static constexpr int LDS = 2 * T1 * kMlpChunk * 2;         // bytes: two chunks of the widest layer
+};
+using MlpHumanoid = MlpShape<87, 400, 200, 100, 21>;   // cfg/train/HumanoidPPO.yaml:24-25
+using MlpAnt = MlpShape<60, 256, 128, 64, 8>;          // cfg/train/AntPPO.yaml
+
+int mlp_shape_id(const mi_rl_mlp* m) {
+    if (!m || m->num_hidden != 3) return 0;
+    auto is = [&](int o, int a, int b, int c, int na) {
+        return m->num_obs == o && m->units[0] == a && m->units[1] == b && m->units[2] == c && m->num_actions == na;
+    };
+    if (is(87, 400, 200, 100, 21)) return 1;
+    if (is(60, 256, 128, 64, 8)) return 2;
+    return 0;
+}
+
+// One packed element: section, k-step s, tile t, lane l, element j. Forward sections pack W
+// [out][in] as the A operand (row 16 t + (l & 15), k 32 s + perm); backward ones W^T (row = in
+// feature 16 t + (l & 15), k = out feature 32 s + perm); the head is the mu rows then the value
+// row. Zero padding everywhere else.
+template <class S>
+__global__ void k_mlp_train_pack(mi_rl_mlp m, _Float16* __restrict__ out) {
+    const long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= S::TOTAL) return;
+    const int in_dim[4] = {S::O, S::H1, S::H2, S::H3};
+    const int out_dim[4] = {S::H1, S::H2, S::H3, S::NH};
+    auto W = [&](int layer, int n, int k) -> float {
+        if (n >= out_dim[layer] || k >= in_dim[layer]) return 0.0f;
+        if (layer < 3) return m.w[layer][(size_t)n * in_dim[layer] + k];
+        return n < S::A ? m.w[3][(size_t)n * in_dim[3] + k] : m.w[4][k];
+    };
+    float v = 0.0f;
+    if (i < S::BIAS) {
+        long long o;
+        int layer, T;
+        bool fwd = true;
+        if (i < S::F2) { o = i - S::F1; layer = 0; T = S::T1; }
+        else if (i < S::F3) { o = i - S::F2; layer = 1; T = S::T2; }
+        else if (i < S::FH) { o = i - S::F3; layer = 2; T = S::T3; }
+        else if (i < S::BH) { o = i - S::FH; layer = 3; T = S::TH; }
+        else if (i < S::B3) { o = i - S::BH; layer = 3; T = S::T3; fwd = false; }
+        else if (i < S::B2) { o = i - S::B3; layer = 2; T = S::T2; fwd = false; }
+        else { o = i - S::B2; layer = 1; T = S::T1; fwd = false; }
+        const int j = (int)(o & 7), l = (int)((o >> 3) & 63);
+        const long long st = o >> 9;                 // k-step major, then tile
+        const int t = (int)(st % T), s = (int)(st / T);
+        const int r = 16 * t + (l & 15), k = 32 * s + mlp_perm(l >> 4, j);
+        v = fwd ? W(layer, r, k) : W(layer, k, r);
+    } else {
+        long long o = i - S::BIAS;
+        const int lens[4] = {16 * S::T1, 16 * S::T2, 16 * S::T3, 16 * S::TH};
+        int layer = 0;
+        while (layer < 3 && o >= lens[layer]) { o -= lens[layer]; ++layer; }
+        const int n = (int)o;
+        if (n < out_dim[layer]) v = layer < 3 ? m.b[layer][n] : (n < S::A ? m.b[3][n] : m.b[4][0]);
+    }
+    out[i] = (_Float16)v;
+}
+
+// this wave's accumulators of one product: acc[t] = sum_s A(s, t) . B[s]; the workgroup stages
+// each k-step's weight chunk (T tiles) into LDS (double buffer, 2 x T x 1 KB)
+template <int T, int KS>
+__device__ __forceinline__ void mlp_mm(const _Float16* __restrict__ Ap, const h8 (&B)[KS], mf4 (&acc)[T],
+                                       _Float16* lds, int tid, int lane) {
+    constexpr int CH = T * kMlpChunk;                 // halfs per chunk
+    constexpr int PER = (CH / 8 + 255) / 256;         // 16-B pieces per thread
+#pragma unroll
+    for (int t = 0; t < T; ++t) acc[t] = mf4{0.0f, 0.0f, 0.0f, 0.0f};
+    h8 stg[PER];
+    __syncthreads();                                  // the previous product's readers are done
+#pragma unroll
+    for (int q = 0; q < PER; ++q) {
+        const int o = (tid + 256 * q) * 8;
+        if (o < CH) stg[q] = *(const h8*)(Ap + o);
+    }
+#pragma unroll
+    for (int q = 0; q < PER; ++q) {
+        const int o = (tid + 256 * q) * 8;
+        if (o < CH) *(h8*)(lds + o) = stg[q];
+    }
+    __syncthreads();
+#pragma unroll
+    for (int s = 0; s < KS; ++s) {
+        const _Float16* cur = lds + (s & 1) * CH;
+        _Float16* nxt = lds + ((s + 1) & 1) * CH;
+        if (s + 1 < KS) {   // the next chunk's global loads in flight during this chunk's MFMAs
+#pragma unroll
+            for (int q = 0; q < PER; ++q) {
+                const int o = (tid + 256 * q) * 8;
+                if (o < CH) stg[q] = *(const h8*)(Ap + (size_t)(s + 1) * CH + o);
+            }
+        }
+#pragma unroll
+        for (int t = 0; t < T; ++t) {
+            const h8 a = *(const h8*)(cur + t * kMlpChunk + lane * 8);
+            acc[t] = __builtin_amdgcn_mfma_f32_16x16x32_f16(a, B[s], acc[t], 0, 0, 0);
+        }
+        if (s + 1 < KS) {
+#pragma unroll
+            for (int q = 0; q < PER; ++q) {
+                const int o = (tid + 256 * q) * 8;
+                if (o < CH) *(h8*)(nxt + o) = stg[q];
+            }
+            __syncthreads();
+        }
+    }
+}
+
+__device__ __forceinline__ float mlp_elu(float v) { return v > 0.0f ? v : expm1f(v); }
+
+// hidden-layer epilogue (forward): y = f16(elu(f16(acc + b))) stored to act [rows][N + 1] (the ones
+// column at N: the bias column of the split-K weight gradient), and the next product's B
+// fragments (features >= N are 0)
+template <int T, int N>
+__device__ __forceinline__ void mlp_fwd_epi(const mf4 (&acc)[T], const _Float16* __restrict__ bias,
+                                            _Float16* __restrict__ act, int row, bool live, int lane,
+                                            h8 (&Bn)[T / 2]) {
+    static_assert(N % 4 == 0, "whole groups of 4 features");
+    constexpr int LD = mlp_act_ld(N);
+    const int h = lane >> 4;
+#pragma unroll
+    for (int t = 0; t < T; ++t) {
+        const int f0 = 16 * t + 4 * h;
+        const h4 b4 = *(const h4*)(bias + f0);
+        h4 y4;
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            const _Float16 z = (_Float16)(acc[t][i] + (float)b4[i]);
+            const _Float16 y = (_Float16)mlp_elu((float)z);
+            y4[i] = f0 < N ? y : (_Float16)0.0f;
+            Bn[t >> 1][4 * (t & 1) + i] = y4[i];
+        }
+        if (live && f0 < N) *(h4*)(act + (size_t)row * LD + f0) = y4;
+    }
+    if (live && h == 0) act[(size_t)row * LD + N] = (_Float16)1.0f;   // the ones column
+}
+
+template <class S>
+__global__ __launch_bounds__(256) void k_mlp_train_fwd(const _Float16* __restrict__ pk, const float* __restrict__ x,
+                                                       int rows, _Float16* __restrict__ xa, _Float16* __restrict__ h1a,
+                                                       _Float16* __restrict__ h2a, _Float16* __restrict__ h3a,
+                                                       _Float16* __restrict__ mu, _Float16* __restrict__ val) {
+    extern __shared__ __attribute__((aligned(16))) _Float16 mlp_lds[];
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, h = lane >> 4;
+    const int row = blockIdx.x * kMlpRows + wave * 16 + (lane & 15);
+    const bool live = row < rows;
+    // the input: f32 -> f16 (autocast's cast) B fragments, and [x | 1] f16 for layer 1's weight
+    // gradient (each (row, k) lies in exactly one lane's fragment)
+    h8 B0[S::KS0];
+#pragma unroll
+    for (int s = 0; s < S::KS0; ++s) {
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+            const int k = 32 * s + mlp_perm(h, j);
+            const float v = (live && k < S::O) ? x[(size_t)row * S::O + k] : 0.0f;
+            const _Float16 hv = (_Float16)v;
+            B0[s][j] = hv;
+            if (live && k < S::O) xa[(size_t)row * mlp_act_ld(S::O) + k] = hv;
+        }
+    }
+    if (live && h == 0) xa[(size_t)row * mlp_act_ld(S::O) + S::O] = (_Float16)1.0f;   // the ones column
+    const _Float16* bias = pk + S::BIAS;
+    h8 B1[S::T1 / 2];
+    {
+        mf4 acc[S::T1];
+        mlp_mm<S::T1, S::KS0>(pk + S::F1, B0, acc, mlp_lds, tid, lane);
+        mlp_fwd_epi<S::T1, S::H1>(acc, bias, h1a, row, live, lane, B1);
+    }
+    h8 B2[S::T2 / 2];
+    {
+        mf4 acc[S::T2];
+        mlp_mm<S::T2, S::T1 / 2>(pk + S::F2, B1, acc, mlp_lds, tid, lane);
+        mlp_fwd_epi<S::T2, S::H2>(acc, bias + 16 * S::T1, h2a, row, live, lane, B2);
+    }
+    h8 B3[S::T3 / 2];
+    {
+        mf4 acc[S::T3];
+        mlp_mm<S::T3, S::T2 / 2>(pk + S::F3, B2, acc, mlp_lds, tid, lane);
+        mlp_fwd_epi<S::T3, S::H3>(acc, bias + 16 * (S::T1 + S::T2), h3a, row, live, lane, B3);
+    }
+    mf4 acc[S::TH];
+    mlp_mm<S::TH, S::T3 / 2>(pk + S::FH, B3, acc, mlp_lds, tid, lane);
+    const _Float16* bh = bias + 16 * (S::T1 + S::T2 + S::T3);
+#pragma unroll
+    for (int t = 0; t < S::TH; ++t) {
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            const int f = 16 * t + 4 * h + i;
+            const _Float16 z = (_Float16)(acc[t][i] + (float)bh[f]);
+            if (live) {
+                if (f < S::A) mu[(size_t)row * S::A + f] = z;
+                else if (f == S::A) val[row] = z;
+            }
+        }
+    }
+}
+
+// backward epilogue: g = f16(f16(acc) * elu'(h)), h the stored activation of this layer
+// (act [rows][N + 1]); stored to g [rows][N] and, when chaining on, the next product's B
+template <int T, int N, bool NEXT>
+__device__ __forceinline__ void mlp_bwd_epi(const mf4 (&acc)[T], const _Float16* __restrict__ act,
+                                            _Float16* __restrict__ g, int row, bool live, int lane,
+                                            h8 (&Bn)[T / 2]) {
+    static_assert(N % 4 == 0, "whole groups of 4 features");
+    constexpr int LD = mlp_act_ld(N);
+    const int h = lane >> 4;
+#pragma unroll
+    for (int t = 0; t < T; ++t) {
+        const int f0 = 16 * t + 4 * h;
+        h4 g4 = {(_Float16)0.0f, (_Float16)0.0f, (_Float16)0.0f, (_Float16)0.0f};
+        if (live && f0 < N) {
+            const h4 a4 = *(const h4*)(act + (size_t)row * LD + f0);
+#pragma unroll
+            for (int i = 0; i < 4; ++i) {
+                const float hv = (float)a4[i];
+                const float d = (float)(_Float16)acc[t][i];
+                g4[i] = (_Float16)(d * (hv > 0.0f ? 1.0f : hv + 1.0f));
+            }
+            *(h4*)(g + (size_t)row * N + f0) = g4;
+        }
+        if constexpr (NEXT) {
+#pragma unroll
+            for (int i = 0; i < 4; ++i) Bn[t >> 1][4 * (t & 1) + i] = g4[i];
+        }
+    }
+}
+
+template <class S>
+__global__ __launch_bounds__(256) void k_mlp_train_bwd(const _Float16* __restrict__ pk, int rows,
+                                                       const _Float16* __restrict__ h1a,
+                                                       const _Float16* __restrict__ h2a,
+                                                       const _Float16* __restrict__ h3a,
+                                                       const _Float16* __restrict__ gmu,
+                                                       const _Float16* __restrict__ gval,
+                                                       _Float16* __restrict__ g1, _Float16* __restrict__ g2,
+                                                       _Float16* __restrict__ g3) {
+    extern __shared__ __attribute__((aligned(16))) _Float16 mlp_lds[];
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, h = lane >> 4;
+    const int row = blockIdx.x * kMlpRows + wave * 16 + (lane & 15);
+    const bool live = row < rows;
+    // the heads' gradient [gmu | gval] as the B fragment of one 32-k step
+    h8 BH[1];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+        const int k = mlp_perm(h, j);
+        _Float16 v = (_Float16)0.0f;
+        if (live) {
+            if (k < S::A) v = gmu[(size_t)row * S::A + k];
+            else if (k == S::A) v = gval[row];
+        }
+        BH[0][j] = v;
+    }
+    h8 B3[S::T3 / 2];
+    {
+        mf4 acc[S::T3];
+        mlp_mm<S::T3, 1>(pk + S::BH, BH, acc, mlp_lds, tid, lane);
+        mlp_bwd_epi<S::T3, S::H3, true>(acc, h3a, g3, row, live, lane, B3);
+    }
+    h8 B2[S::T2 / 2];
+    {
+        mf4 acc[S::T2];
+        mlp_mm<S::T2, S::T3 / 2>(pk + S::B3, B3, acc, mlp_lds, tid, lane);
+        mlp_bwd_epi<S::T2, S::H2, true>(acc, h2a, g2, row, live, lane, B2);
+    }
+    mf4 acc[S::T1];
+    mlp_mm<S::T1, S::T2 / 2>(pk + S::B2, B2, acc, mlp_lds, tid, lane);
+    h8 none[S::T1 / 2];
+    mlp_bwd_epi<S::T1, S::H1, false>(acc, h1a, g1, row, live, lane, none);
+}
+
+template <class S>
+int mlp_train_fwd_launch(const _Float16* pk, const float* x, int rows, void* const* acts, void* mu, void* val,
+                         hipStream_t st) {
+    hipLaunchKernelGGL(k_mlp_train_fwd<S>, dim3((rows + kMlpRows - 1) / kMlpRows), dim3(256), S::LDS, st, pk, x,
+                       rows, (_Float16*)acts[0], (_Float16*)acts[1], (_Float16*)acts[2], (_Float16*)acts[3],
+                       (_Float16*)mu, (_Float16*)val);
+    return launch_check("mi_rl_mlp_train_fwd");
+}
+
+template <class S>
+int mlp_train_bwd_launch(const _Float16* pk, int rows, void* const* acts, const void* gmu, const void* gval,
+                         void* const* grads, hipStream_t st) {
+    hipLaunchKernelGGL(k_mlp_train_bwd<S>, dim3((rows + kMlpRows - 1) / kMlpRows), dim3(256), S::LDS, st, pk, rows,
+                       (const _Float16*)acts[1], (const _Float16*)acts[2], (const _Float16*)acts[3],
+                       (const _Float16*)gmu, (const _Float16*)gval, (_Float16*)grads[0], (_Float16*)grads[1],
+                       (_Float16*)grads[2]);
+    return launch_check("mi_rl_mlp_train_bwd");
+}
+}  // namespace
+
 extern "C" {
 
 int32_t mi_rl_abi_version(void) { return MI_RL_ABI_VERSION; }
@@ -879,6 +1220,51 @@ int32_t mi_rl_adam_step(const mi_rl_adam_cfg* cfg, float* params, const float* g
     hipLaunchKernelGGL(k_adam_apply, dim3(nb), dim3(kAdamBlock), 0, (hipStream_t)stream, *cfg, params, grads,
                        exp_avg, exp_avg_sq, n, step, lr, scale, growth_tracker, kl, scratch, tickets + 4);
     return launch_check("mi_rl_adam_step (apply)");
+}
+
+int64_t mi_rl_mlp_train_packed_size(const mi_rl_mlp* mlp) {
+    switch (mlp_shape_id(mlp)) {
+        case 1: return MlpHumanoid::TOTAL;
+        case 2: return MlpAnt::TOTAL;
+        default: return -1;
+    }
+}
+
+int32_t mi_rl_mlp_train_pack(const mi_rl_mlp* mlp, void* packed, void* stream) {
+    const int id = mlp_shape_id(mlp);
+    if (!id) return fail(kShape, "mi_rl_mlp_train_pack: unsupported network layout");
+    if (!packed) return fail(kNull, "mi_rl_mlp_train_pack: null packed buffer");
+    for (int l = 0; l < 5; ++l)
+        if (!mlp->w[l] || !mlp->b[l]) return fail(kNull, "mi_rl_mlp_train_pack: null weight / bias of layer %d", l);
+    const long long n = id == 1 ? MlpHumanoid::TOTAL : MlpAnt::TOTAL;
+    const dim3 g((unsigned)((n + kBlock - 1) / kBlock));
+    if (id == 1) hipLaunchKernelGGL(k_mlp_train_pack<MlpHumanoid>, g, dim3(kBlock), 0, (hipStream_t)stream, *mlp, (_Float16*)packed);
+    else hipLaunchKernelGGL(k_mlp_train_pack<MlpAnt>, g, dim3(kBlock), 0, (hipStream_t)stream, *mlp, (_Float16*)packed);
+    return launch_check("mi_rl_mlp_train_pack");
+}
+
+int32_t mi_rl_mlp_train_fwd(const mi_rl_mlp* mlp, const void* packed, const float* x, int32_t rows,
+                            void* const* acts, void* mu, void* value, void* stream) {
+    const int id = mlp_shape_id(mlp);
+    if (!id) return fail(kShape, "mi_rl_mlp_train_fwd: unsupported network layout");
+    if (!packed || !x || !acts || !mu || !value) return fail(kNull, "mi_rl_mlp_train_fwd: null buffer");
+    for (int l = 0; l < 4; ++l)
+        if (!acts[l]) return fail(kNull, "mi_rl_mlp_train_fwd: null activation buffer %d", l);
+    if (rows <= 0) return fail(kShape, "mi_rl_mlp_train_fwd: rows=%d", rows);
+    return id == 1 ? mlp_train_fwd_launch<MlpHumanoid>((const _Float16*)packed, x, rows, acts, mu, value, (hipStream_t)stream)
+                   : mlp_train_fwd_launch<MlpAnt>((const _Float16*)packed, x, rows, acts, mu, value, (hipStream_t)stream);
+}
+
+int32_t mi_rl_mlp_train_bwd(const mi_rl_mlp* mlp, const void* packed, void* const* acts, const void* grad_mu,
+                            const void* grad_value, int32_t rows, void* const* grads, void* stream) {
+    const int id = mlp_shape_id(mlp);
+    if (!id) return fail(kShape, "mi_rl_mlp_train_bwd: unsupported network layout");
+    if (!packed || !acts || !grad_mu || !grad_value || !grads) return fail(kNull, "mi_rl_mlp_train_bwd: null buffer");
+    for (int l = 1; l < 4; ++l)
+        if (!acts[l] || !grads[l - 1]) return fail(kNull, "mi_rl_mlp_train_bwd: null buffer of layer %d", l);
+    if (rows <= 0) return fail(kShape, "mi_rl_mlp_train_bwd: rows=%d", rows);
+    return id == 1 ? mlp_train_bwd_launch<MlpHumanoid>((const _Float16*)packed, rows, acts, grad_mu, grad_value, grads, (hipStream_t)stream)
+                   : mlp_train_bwd_launch<MlpAnt>((const _Float16*)packed, rows, acts, grad_mu, grad_value, grads, (hipStream_t)stream);
 }
 
 }  // extern "C"

@@ -125,6 +125,46 @@ class _LinearSplitKShadow(torch.autograd.Function):
         return gx, gw, gb, None, None, None
 
 
+def _split_k_wgrad(gy: torch.Tensor, xa: torch.Tensor, S: int) -> torch.Tensor:
+    """[gW | gb] = gyᵀ [x | 1] as _LinearSplitKShadow forms it: S row blocks (fp16 partials of
+    the batched GEMM), summed in f32."""
+    K, O = gy.shape
+    if S > 1 and K % S == 0:
+        return torch.bmm(gy.reshape(S, K // S, O).transpose(1, 2),
+                         xa.reshape(S, K // S, xa.shape[1])).sum(0, dtype=torch.float32)
+    return (gy.t() @ xa).to(torch.float32)
+
+
+class _FusedMLPTrain(torch.autograd.Function):
+    """The minibatch trunk + heads of the PPO update on fp16 MFMA (ops.FusedTrainMLP, one launch
+    forward, one launch for the dgrad chain), returning (mu, value) in f16 as the autocast Linears
+    do; the weight / bias gradients of the f32 masters are the split-K GEMMs of
+    _LinearSplitKShadow over the layer inputs the forward stored with a ones column."""
+
+    @staticmethod
+    def forward(ctx, x, fused, splits, *params):
+        mu, val, acts = fused.forward(x.contiguous())
+        ctx.fused, ctx.splits = fused, splits
+        ctx.save_for_backward(*acts)
+        return mu, val
+
+    @staticmethod
+    def backward(ctx, gmu, gval):
+        acts = ctx.saved_tensors
+        fused, S = ctx.fused, ctx.splits
+        if gmu is None:
+            gmu = torch.zeros((acts[0].shape[0], fused.dims[4]), device=acts[0].device, dtype=torch.float16)
+        if gval is None:
+            gval = torch.zeros((acts[0].shape[0], 1), device=acts[0].device, dtype=torch.float16)
+        (g1, g2, g3), gmu, gval = fused.backward(acts, gmu, gval)
+        out = []
+        for gy, xa in ((g1, acts[0]), (g2, acts[1]), (g3, acts[2]), (gmu, acts[3]), (gval, acts[3])):
+            gwb = _split_k_wgrad(gy, xa, S)
+            I = xa.shape[1] - 1
+            out += [gwb[:, :I], gwb[:, I]]
+        return (None, None, None, *out)
+
+
 def linear_train(x: torch.Tensor, layer: nn.Linear, splits: int = 32, shadow=None) -> torch.Tensor:
     """nn.Linear for the learner's minibatch forward (autocast-aware: runs in the autocast dtype
     when autocast is on, as nn.Linear would), with the split-K weight gradient. shadow: the
@@ -259,11 +299,30 @@ class ActorCriticMLP(nn.Module):
                     raise ValueError("shadow_weights: a Linear parameter is not a view of the flat buffer")
                 views[id(p)] = low[o:o + p.numel()].view_as(p)
         self._flat32, self._flat_low, self._low_views = flat, low, views
+        # the fused fp16-MFMA trunk (mi_rl_mlp_train_*) when the layout is compiled; MI_RL_FUSED_MLP=0
+        # or cfg fused_train_mlp: False keeps the per-layer path (A/B)
+        self._train_mlp = None
+        if dtype == torch.float16 and flat.is_cuda and getattr(self, "fused_train_mlp", True):
+            import os
+
+            if os.environ.get("MI_RL_FUSED_MLP", "1") != "0":
+                from .ops import FusedTrainMLP
+                try:
+                    self._train_mlp = FusedTrainMLP(self)
+                except ValueError:
+                    self._train_mlp = None
 
     def heads_train(self, obs: torch.Tensor, splits: int = 32):
         """(mu, value) of the minibatch forward through linear_train (split-K weight grads)."""
         low = getattr(self, "_flat_low", None)
         sh = None
+        fused = getattr(self, "_train_mlp", None)
+        if (fused is not None and low is not None and torch.is_autocast_enabled(obs.device.type)
+                and torch.get_autocast_dtype(obs.device.type) == low.dtype and obs.dtype == torch.float32):
+            fused.pack()                     # f16 operand images of the current masters: one launch
+            params = [p for m in self._linears() for p in (m.weight, m.bias)]
+            with torch.autocast(device_type=obs.device.type, enabled=False):
+                return _FusedMLPTrain.apply(obs, fused, splits, *params)
         if (low is not None and torch.is_autocast_enabled(obs.device.type)
                 and torch.get_autocast_dtype(obs.device.type) == low.dtype):
             low.copy_(self._flat32)          # every layer's low-precision weights: one launch

@@ -78,6 +78,14 @@ def load_library() -> C.CDLL:
         lib.mi_rl_record_step.restype = i32
         lib.mi_rl_record_step.argtypes = [vp, i32, vp, vp, i32, f] + [vp] * 9
         lib.mi_rl_adam_step.restype = i32
+        lib.mi_rl_mlp_train_packed_size.restype = C.c_int64
+        lib.mi_rl_mlp_train_packed_size.argtypes = [C.POINTER(MiRlMlp)]
+        lib.mi_rl_mlp_train_pack.restype = i32
+        lib.mi_rl_mlp_train_pack.argtypes = [C.POINTER(MiRlMlp), vp, vp]
+        lib.mi_rl_mlp_train_fwd.restype = i32
+        lib.mi_rl_mlp_train_fwd.argtypes = [C.POINTER(MiRlMlp), vp, vp, i32, C.POINTER(vp), vp, vp, vp]
+        lib.mi_rl_mlp_train_bwd.restype = i32
+        lib.mi_rl_mlp_train_bwd.argtypes = [C.POINTER(MiRlMlp), vp, C.POINTER(vp), vp, vp, i32, C.POINTER(vp), vp]
         lib.mi_rl_adam_step.argtypes = [C.POINTER(MiRlAdamCfg), vp, vp, vp, vp, C.c_int64, vp, vp, vp, vp, vp,
                                         vp, C.c_int64, vp, vp]
         _LIB = lib
@@ -425,3 +433,74 @@ class FusedAdamStep:
             self.exp_avg_sq.data_ptr(), self.n, self.step_t.data_ptr(), self.lr_t.data_ptr(), _ptr(scale),
             _ptr(tracker), _ptr(kl) if self.cfg.adaptive_lr else None, self.scratch.data_ptr(),
             self.scratch.numel(), self.tickets.data_ptr(), _stream(self.flat)), "mi_rl_adam_step")
+
+
+class FusedTrainMLP:
+    """The PPO update's minibatch network on fp16 MFMA (mi_rl_mlp_train_*): the forward (3 ELU
+    layers + the mu / value heads) and the dgrad chain are one launch each; the weight and bias
+    gradients stay split-K batched GEMMs over the layer inputs the forward stores with a ones
+    column (models._LinearSplitKShadow's scheme). ``net`` is an ActorCriticMLP whose Linear
+    parameters are views of one flat f32 buffer; :meth:`pack` refreshes the f16 operand images
+    from those masters (one launch per minibatch: it replaces the shadow-copy cast)."""
+
+    def __init__(self, net):
+        lin = [m for m in net.actor_mlp if isinstance(m, torch.nn.Linear)]
+        acts = [m for m in net.actor_mlp if not isinstance(m, torch.nn.Linear)]
+        if not net.fixed_sigma or not all(isinstance(a, torch.nn.ELU) for a in acts) or len(lin) != 3:
+            raise ValueError("FusedTrainMLP: fixed-sigma networks of 3 ELU layers only")
+        d = MiRlMlp()
+        d.num_obs, d.num_actions, d.num_hidden = lin[0].in_features, net.mu.out_features, 3
+        self.layers = lin + [net.mu, net.value]
+        for i, m in enumerate(lin):
+            d.units[i] = m.out_features
+        for i, m in enumerate(self.layers):
+            if m.weight.dtype != torch.float32 or not m.weight.is_cuda:
+                raise ValueError("FusedTrainMLP: f32 CUDA weights expected")
+            d.w[i], d.b[i] = m.weight.data_ptr(), m.bias.data_ptr()
+        n = kernels().mi_rl_mlp_train_packed_size(C.byref(d))
+        if n < 0:
+            raise ValueError(f"FusedTrainMLP: layout {d.num_obs}-{list(d.units)[:3]}-{d.num_actions} not compiled")
+        self.desc = d
+        self.dims = (d.num_obs, lin[0].out_features, lin[1].out_features, lin[2].out_features, d.num_actions)
+        self.packed = torch.zeros((int(n),), device=lin[0].weight.device, dtype=torch.float16)
+        self._ptrs = tuple(p.data_ptr() for m in self.layers for p in (m.weight, m.bias))
+
+    def check_views(self) -> None:
+        """The descriptor points at the parameters' storage: fail loudly if it moved."""
+        if tuple(p.data_ptr() for m in self.layers for p in (m.weight, m.bias)) != self._ptrs:
+            raise RuntimeError("FusedTrainMLP: parameter storage moved since construction")
+
+    def pack(self) -> None:
+        _check(kernels().mi_rl_mlp_train_pack(C.byref(self.desc), self.packed.data_ptr(), _stream(self.packed)),
+               "mi_rl_mlp_train_pack")
+
+    def forward(self, x: torch.Tensor):
+        """x [K, O] f32 contiguous -> (mu f16 [K, A], value f16 [K, 1], the 4 layer inputs f16
+        [K, width + 1] with a ones column: views of row-padded buffers)."""
+        O, H1, H2, H3, A = self.dims
+        K = x.shape[0]
+        if x.dtype != torch.float32 or not x.is_contiguous() or x.shape[1] != O:
+            raise ValueError(f"FusedTrainMLP.forward: x {tuple(x.shape)} {x.dtype}")
+        f16 = torch.float16
+        # row stride padded to 8 halfs (mi_rl.h): the kernel's 8-byte accesses stay aligned; the
+        # [K, width + 1] views are what the split-K weight gradients read
+        acts = [torch.empty((K, (w + 1 + 7) & ~7), device=x.device, dtype=f16)[:, :w + 1] for w in (O, H1, H2, H3)]
+        mu = torch.empty((K, A), device=x.device, dtype=f16)
+        val = torch.empty((K, 1), device=x.device, dtype=f16)
+        ptrs = (C.c_void_p * 4)(*[a.data_ptr() for a in acts])
+        _check(kernels().mi_rl_mlp_train_fwd(C.byref(self.desc), self.packed.data_ptr(), x.data_ptr(), K, ptrs,
+                                             mu.data_ptr(), val.data_ptr(), _stream(x)), "mi_rl_mlp_train_fwd")
+        return mu, val, acts
+
+    def backward(self, acts, gmu: torch.Tensor, gval: torch.Tensor):
+        """(gradients w.r.t. the 3 hidden pre-activations, f16 [K, width])."""
+        O, H1, H2, H3, A = self.dims
+        K = gmu.shape[0]
+        gmu = gmu.to(torch.float16).contiguous()
+        gval = gval.to(torch.float16).contiguous()
+        gs = [torch.empty((K, w), device=gmu.device, dtype=torch.float16) for w in (H1, H2, H3)]
+        aptr = (C.c_void_p * 4)(*[a.data_ptr() for a in acts])
+        gptr = (C.c_void_p * 3)(*[g.data_ptr() for g in gs])
+        _check(kernels().mi_rl_mlp_train_bwd(C.byref(self.desc), self.packed.data_ptr(), aptr, gmu.data_ptr(),
+                                             gval.data_ptr(), K, gptr, _stream(gmu)), "mi_rl_mlp_train_bwd")
+        return gs, gmu, gval
