@@ -838,10 +838,12 @@ __global__ void k_mlp_train_pack(mi_rl_mlp m, _Float16* __restrict__ out) {
 
 // this wave's accumulators of one product: acc[t] = sum_s A(s, t) . B[s]; the workgroup stages
 // each k-step's weight chunk (T tiles) into LDS (double buffer, 2 x T x 1 KB)
-template <int T, int KS>
+template <int T, int KS, int TT = T>
 __device__ __forceinline__ void mlp_mm(const _Float16* __restrict__ Ap, const h8 (&B)[KS], mf4 (&acc)[T],
                                        _Float16* lds, int tid, int lane) {
-    constexpr int CH = T * kMlpChunk;                 // halfs per chunk
+    // tiles [T0, T0 + T) of a product with TT tiles per k-step chunk: Ap points at tile T0 of
+    // chunk 0, the k-steps are TT x 1 KB apart
+    constexpr int CH = T * kMlpChunk;                 // halfs per (partial) chunk staged
     constexpr int PER = (CH / 8 + 255) / 256;         // 16-B pieces per thread
 #pragma unroll
     for (int t = 0; t < T; ++t) acc[t] = mf4{0.0f, 0.0f, 0.0f, 0.0f};
@@ -866,7 +868,7 @@ __device__ __forceinline__ void mlp_mm(const _Float16* __restrict__ Ap, const h8
 #pragma unroll
             for (int q = 0; q < PER; ++q) {
                 const int o = (tid + 256 * q) * 8;
-                if (o < CH) stg[q] = *(const h8*)(Ap + (size_t)(s + 1) * CH + o);
+                if (o < CH) stg[q] = *(const h8*)(Ap + (size_t)(s + 1) * TT * kMlpChunk + o);
             }
         }
 #pragma unroll
@@ -885,33 +887,45 @@ __device__ __forceinline__ void mlp_mm(const _Float16* __restrict__ Ap, const h8
     }
 }
 
-__device__ __forceinline__ float mlp_elu(float v) { return v > 0.0f ? v : expm1f(v); }
+// ELU without branches (rounded to f16 by the caller): v > 0: v; otherwise expm1(v), as a degree-6
+// Taylor polynomial for |v| < 1/4 (truncation < 2e-6 relative) and exp(v) - 1 by v_exp_f32 below
+// (no cancellation there: exp(v) <= 0.78). Both are far inside the f16 rounding of the result;
+// libm's expm1f branched per element (the epilogue's 180 divergent sections per wave).
+__device__ __forceinline__ float mlp_elu(float v) {
+    const float p = v * (1.0f + v * (0.5f + v * (1.0f / 6.0f + v * (1.0f / 24.0f + v * (1.0f / 120.0f + v * (1.0f / 720.0f))))));
+    const float e = __builtin_amdgcn_exp2f(v * 1.44269504088896341f) - 1.0f;
+    const float m = v > -0.25f ? p : e;
+    return v > 0.0f ? v : m;
+}
 
 // hidden-layer epilogue (forward): y = f16(elu(f16(acc + b))) stored to act [rows][N + 1] (the ones
 // column at N: the bias column of the split-K weight gradient), and the next product's B
 // fragments (features >= N are 0)
-template <int T, int N>
+template <int T, int N, int T0 = 0, int BN = T / 2>
 __device__ __forceinline__ void mlp_fwd_epi(const mf4 (&acc)[T], const _Float16* __restrict__ bias,
                                             _Float16* __restrict__ act, int row, bool live, int lane,
-                                            h8 (&Bn)[T / 2]) {
+                                            h8 (&Bn)[BN]) {
+    // acc holds tiles T0 .. T0 + T - 1 of the layer (T0 > 0: the second half of a split layer)
     static_assert(N % 4 == 0, "whole groups of 4 features");
     constexpr int LD = mlp_act_ld(N);
     const int h = lane >> 4;
 #pragma unroll
-    for (int t = 0; t < T; ++t) {
+    for (int tl = 0; tl < T; ++tl) {
+        const int t = T0 + tl;
         const int f0 = 16 * t + 4 * h;
-        const h4 b4 = *(const h4*)(bias + f0);
+        const bool in = 16 * (t + 1) <= N || f0 < N;   // compile-time true below the last tile
+        const h4 b4 = *(const h4*)(bias + f0);          // (the padded bias is 0 past N)
         h4 y4;
 #pragma unroll
         for (int i = 0; i < 4; ++i) {
-            const _Float16 z = (_Float16)(acc[t][i] + (float)b4[i]);
+            const _Float16 z = (_Float16)(acc[tl][i] + (float)b4[i]);
             const _Float16 y = (_Float16)mlp_elu((float)z);
-            y4[i] = f0 < N ? y : (_Float16)0.0f;
+            y4[i] = in ? y : (_Float16)0.0f;
             Bn[t >> 1][4 * (t & 1) + i] = y4[i];
         }
-        if (live && f0 < N) *(h4*)(act + (size_t)row * LD + f0) = y4;
+        if (live && in) *(h4*)(act + (size_t)row * LD + f0) = y4;
     }
-    if (live && h == 0) act[(size_t)row * LD + N] = (_Float16)1.0f;   // the ones column
+    if (T0 == 0 && live && h == 0) act[(size_t)row * LD + N] = (_Float16)1.0f;   // the ones column
 }
 
 template <class S>
@@ -940,10 +954,16 @@ __global__ __launch_bounds__(256) void k_mlp_train_fwd(const _Float16* __restric
     if (live && h == 0) xa[(size_t)row * mlp_act_ld(S::O) + S::O] = (_Float16)1.0f;   // the ones column
     const _Float16* bias = pk + S::BIAS;
     h8 B1[S::T1 / 2];
-    {
-        mf4 acc[S::T1];
-        mlp_mm<S::T1, S::KS0>(pk + S::F1, B0, acc, mlp_lds, tid, lane);
-        mlp_fwd_epi<S::T1, S::H1>(acc, bias, h1a, row, live, lane, B1);
+    {   // the widest layer in two halves of its output tiles (half the accumulators live at once)
+        constexpr int HA = S::T1 / 2, HB = S::T1 - HA;
+        {
+            mf4 acc[HA];
+            mlp_mm<HA, S::KS0, S::T1>(pk + S::F1, B0, acc, mlp_lds, tid, lane);
+            mlp_fwd_epi<HA, S::H1, 0, S::T1 / 2>(acc, bias, h1a, row, live, lane, B1);
+        }
+        mf4 acc[HB];
+        mlp_mm<HB, S::KS0, S::T1>(pk + S::F1 + HA * kMlpChunk, B0, acc, mlp_lds, tid, lane);
+        mlp_fwd_epi<HB, S::H1, HA, S::T1 / 2>(acc, bias, h1a, row, live, lane, B1);
     }
     h8 B2[S::T2 / 2];
     {
@@ -976,23 +996,24 @@ __global__ __launch_bounds__(256) void k_mlp_train_fwd(const _Float16* __restric
 
 // backward epilogue: g = f16(f16(acc) * elu'(h)), h the stored activation of this layer
 // (act [rows][N + 1]); stored to g [rows][N] and, when chaining on, the next product's B
-template <int T, int N, bool NEXT>
+template <int T, int N, bool NEXT, int T0 = 0, int BN = T / 2 + 1>
 __device__ __forceinline__ void mlp_bwd_epi(const mf4 (&acc)[T], const _Float16* __restrict__ act,
                                             _Float16* __restrict__ g, int row, bool live, int lane,
-                                            h8 (&Bn)[T / 2]) {
+                                            h8 (&Bn)[BN]) {
     static_assert(N % 4 == 0, "whole groups of 4 features");
     constexpr int LD = mlp_act_ld(N);
     const int h = lane >> 4;
 #pragma unroll
-    for (int t = 0; t < T; ++t) {
+    for (int tl = 0; tl < T; ++tl) {
+        const int t = T0 + tl;
         const int f0 = 16 * t + 4 * h;
         h4 g4 = {(_Float16)0.0f, (_Float16)0.0f, (_Float16)0.0f, (_Float16)0.0f};
-        if (live && f0 < N) {
+        if (live && (16 * (t + 1) <= N || f0 < N)) {   // the second test only in the last tile
             const h4 a4 = *(const h4*)(act + (size_t)row * LD + f0);
 #pragma unroll
             for (int i = 0; i < 4; ++i) {
                 const float hv = (float)a4[i];
-                const float d = (float)(_Float16)acc[t][i];
+                const float d = (float)(_Float16)acc[tl][i];
                 g4[i] = (_Float16)(d * (hv > 0.0f ? 1.0f : hv + 1.0f));
             }
             *(h4*)(g + (size_t)row * N + f0) = g4;
@@ -1033,18 +1054,25 @@ __global__ __launch_bounds__(256) void k_mlp_train_bwd(const _Float16* __restric
     {
         mf4 acc[S::T3];
         mlp_mm<S::T3, 1>(pk + S::BH, BH, acc, mlp_lds, tid, lane);
-        mlp_bwd_epi<S::T3, S::H3, true>(acc, h3a, g3, row, live, lane, B3);
+        mlp_bwd_epi<S::T3, S::H3, true, 0, S::T3 / 2>(acc, h3a, g3, row, live, lane, B3);
     }
     h8 B2[S::T2 / 2];
     {
         mf4 acc[S::T2];
         mlp_mm<S::T2, S::T3 / 2>(pk + S::B3, B3, acc, mlp_lds, tid, lane);
-        mlp_bwd_epi<S::T2, S::H2, true>(acc, h2a, g2, row, live, lane, B2);
+        mlp_bwd_epi<S::T2, S::H2, true, 0, S::T2 / 2>(acc, h2a, g2, row, live, lane, B2);
     }
-    mf4 acc[S::T1];
-    mlp_mm<S::T1, S::T2 / 2>(pk + S::B2, B2, acc, mlp_lds, tid, lane);
-    h8 none[S::T1 / 2];
-    mlp_bwd_epi<S::T1, S::H1, false>(acc, h1a, g1, row, live, lane, none);
+    // the widest product in two halves of its output tiles
+    constexpr int HA = S::T1 / 2, HB = S::T1 - HA;
+    h8 none[1];
+    {
+        mf4 acc[HA];
+        mlp_mm<HA, S::T2 / 2, S::T1>(pk + S::B2, B2, acc, mlp_lds, tid, lane);
+        mlp_bwd_epi<HA, S::H1, false, 0, 1>(acc, h1a, g1, row, live, lane, none);
+    }
+    mf4 acc[HB];
+    mlp_mm<HB, S::T2 / 2, S::T1>(pk + S::B2 + HA * kMlpChunk, B2, acc, mlp_lds, tid, lane);
+    mlp_bwd_epi<HB, S::H1, false, HA, 1>(acc, h1a, g1, row, live, lane, none);
 }
 
 template <class S>

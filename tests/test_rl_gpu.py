@@ -152,7 +152,10 @@ def test_fused_loss_matches_torch_loss(gpu, mixed):
     tol = 2e-2 if mixed else 1e-4
     for x, y in ((a_f, a_t.item()), (c_f, c_t.item()), (e_f, e_t.item()), (kl_f, kl_t.item()), (b_f, b_t.item())):
         assert math.isclose(x, y, rel_tol=tol, abs_tol=1e-6), (x, y)
-    torch.testing.assert_close(mb_f["mu"], cmu, rtol=tol, atol=1e-5)
+    # mixed: the fused trunk (mi_rl_mlp_train_fwd) and the per-layer autocast path sum in a
+    # different order, so mu agrees to a few f16 ulps of the head's magnitude, not to 1e-5
+    mu_atol = 4.0 * 2.0 ** -10 * cmu.abs().max().item() if mixed else 1e-5
+    torch.testing.assert_close(mb_f["mu"], cmu, rtol=tol, atol=mu_atol)
     torch.testing.assert_close(mb_f["sigma"], csig, rtol=1e-6, atol=1e-7)
     for (name, _), gf, gt in zip(ag.model.named_parameters(), g_f, g_t):
         # the fused path sums weight / bias gradients in fp32 (models._LinearSplitKShadow); the
