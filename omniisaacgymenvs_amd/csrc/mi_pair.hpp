@@ -153,6 +153,9 @@ constexpr int kWideScratchRows = MI_PAIR_WIDE_MFMA ? 64 + 32 : 64 - MI_PAIR_WIDE
 #ifndef MI_PAIR_WIDE_AP
 #define MI_PAIR_WIDE_AP 8   // Delassus rows streamed ahead of the wide sweeps' chain
 #endif
+#ifndef MI_PAIR_SWEEP_FMA
+#define MI_PAIR_SWEEP_FMA 1   // PGS row step as two FMAs around the projection (0: l0 + (b - v) / A_rr, v + A (ln - l0))
+#endif
 #ifndef MI_PAIR_WIDE_UPF
 #define MI_PAIR_WIDE_UPF 1   // wide u update: next group's W column loaded ahead (0: in order)
 #endif
@@ -782,12 +785,23 @@ MI_D void pair_artic_substep(const DevModel& m, const WaveTabs& t, const DevStat
                     const float l0 = lamv[rr];
                     const bool fric = kd == 1 || kd == 2;
                     const float lim = mu * lamn;
+#if MI_PAIR_SWEEP_FMA
+                    // x = (l0 + b / A_rr) - v / A_rr and v + A (ln - l0) = (v - A l0) + A ln: the
+                    // l0 terms come off the chain, which is then fma -> med3 -> broadcast -> fma
+                    const float x = __builtin_fmaf(-v, ia, __builtin_fmaf(b, ia, l0));
+#else
+                    const float x = l0 + (b - v) * ia;
+#endif
                     // one med3: max(., lo) then, for friction, min(., lim) (lo <= hi: lamn >= 0)
-                    const float mine = __builtin_amdgcn_fmed3f(l0 + (b - v) * ia, fric ? -lim : 0.0f,
+                    const float mine = __builtin_amdgcn_fmed3f(x, fric ? -lim : 0.0f,
                                                                fric ? lim : __builtin_huge_valf());
                     const float ln = pbcc<rr>(mine);
                     if constexpr (rr % 3 == 0) lamn = rr < nnorm ? ln : lamn;
+#if MI_PAIR_SWEEP_FMA
+                    v = __builtin_fmaf(Ar[rr], ln, __builtin_fmaf(-Ar[rr], l0, v));
+#else
                     v += Ar[rr] * (ln - l0);
+#endif
                     lamv[rr] = ln;
                 }
             });
@@ -1004,6 +1018,9 @@ MI_D void pair_artic_substep(const DevModel& m, const WaveTabs& t, const DevStat
                 int nrow_it = nrh;
                 asm volatile("" : "+s"(nrow_it));
                 float lamn = 0.0f;
+#if MI_PAIR_SWEEP_FMA
+                const float tl = __builtin_fmaf(b, ia, lam);   // lane = row: lam changes at its own row only
+#endif
                 // rows rr .. rr + PA - 1 of A in flight. The scratch is NOT zeroed (no memset at
                 // creation): correctness rests on the invariant that the set-up writes every row
                 // of every group of four it processes ((rr & ~3) < nrh, the sweeps' condition),
@@ -1035,6 +1052,19 @@ MI_D void pair_artic_substep(const DevModel& m, const WaveTabs& t, const DevStat
                         }
                         const bool fric = kd == 1 || kd == 2;
                         const float lim = mu * lamn;
+#if MI_PAIR_SWEEP_FMA
+                        // the narrow sweeps' arithmetic (bit for bit: an env's result does not
+                        // depend on the path its partner sends the wave down): the new lambda
+                        // and the row's old one leave the owner by v_readlane (the old one off
+                        // the chain), v_writelane stores the new one in the owner lane
+                        const float mine = __builtin_amdgcn_fmed3f(__builtin_fmaf(-v, ia, tl), fric ? -lim : 0.0f,
+                                                                   fric ? lim : __builtin_huge_valf());
+                        const float ln = readlane(mine, rr), l0 = readlane(lam, rr);
+                        if constexpr (rr % 3 == 0) lamn = rr < nnh ? ln : lamn;
+                        v = __builtin_fmaf(arr, ln, __builtin_fmaf(-arr, l0, v));
+                        asm("v_writelane_b32 %0, %1, %2" : "+v"(lam) : "s"(ln), "i"(rr));
+                        (void)lw;
+#else
                         const float mine = __builtin_amdgcn_fmed3f(lam + (b - v) * ia, fric ? -lim : 0.0f,
                                                                    fric ? lim : __builtin_huge_valf());
                         // the owner forms the lambda change itself (mine - lam there is exactly
@@ -1045,6 +1075,7 @@ MI_D void pair_artic_substep(const DevModel& m, const WaveTabs& t, const DevStat
                         if constexpr (rr % 3 == 0) lamn = rr < nnh ? readlane(mine, rr) : lamn;
                         v += arr * dl;
                         lam = lw == rr ? mine : lam;
+#endif
                     }
                 });
                 if constexpr (TP::kTgs) {
