@@ -649,7 +649,9 @@ static void proj_margin(ws_t* w, int r, float x, float lo, float hi, int two_sid
  * bias comes from the row's separation plus h x its carried velocity after each earlier
  * sub-step (friction rows: bias 0; velocity iterations: speculative bias only); the owner's
  * step is x = lambda + (b - v_r) / A_rr with the reciprocal formed once, projected onto
- * [0, inf) or +-mu lambda_n. At the end u = u* + sum_r W_r lambda_r and the positions'
+ * [0, inf) or +-mu lambda_n (the device fuses the row step into two FMAs around the projection,
+ * x = (lambda + b / A_rr) - v_r / A_rr and v_c = (v_c - A lambda_old) + A lambda_new: the same
+ * statement rounded differently, within the conditioning allowance). At the end u = u* + sum_r W_r lambda_r and the positions'
  * velocity u-bar = u* + sum_r W_r (sum_k lambda_r^(k) / iters), each summed in row order per
  * DOF. Mathematically the u-space statement (u-bar = the sub-steps' mean velocity); in
  * rounding it is the device's path — the carried v drifts by the rounding of every A dl, which
