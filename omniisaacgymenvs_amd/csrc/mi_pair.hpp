@@ -225,47 +225,63 @@ MI_D lds_cf lds_ptr(const float* p) { return (lds_cf)p; }
 typedef float pv4 __attribute__((ext_vector_type(4)));
 typedef const pv4 __attribute__((address_space(3)))* lds_cf4;
 MI_D int pw_idx(int r, int c, int nv) { return (r & ~3) * nv + 4 * c + (r & 3); }
-MI_D lds_cf4 pw_group(const WaveTabs& t, const float* sm, int g0, int nv) {
-    return (lds_cf4)(sm + t.s_W + g0 * nv);
-}
 // The env's global W slab (rows >= w_rows_lds, up to MI_MAX_ROWS) uses the same 4-row groups,
 // WNV (32) columns: entry (r, c) at (r & ~3) WNV + 4 c + (r & 3), so a slab group is one
 // global_load_dwordx4 per DOF as well (column WNV - 1 is the fallback sweeps' lambda slot)
 MI_D size_t pair_sidx(int r, int c) { return (size_t)(r & ~3) * WNV + 4 * c + (r & 3); }
 typedef const pv4* glb_cf4;
 
+// The W-row sources of one env for a PGS phase, read from the parameter block ONCE: through
+// WaveTabs every 4-row group re-read w_rows_lds / s_W with a scalar load and waited for it
+// before its first W load (a serial round trip per group in the set-up and the u update).
+// kLds: the narrow path, whose rows are all LDS rows (host-checked: w_rows_lds >= kLamRows).
+struct WSrc {
+    lds_cf W;          // the env's LDS W rows
+    const float* gW;   // the env's slab (rows >= nl)
+    int nl;            // LDS rows
+};
+MI_D WSrc make_wsrc(const WaveTabs& t, const float* sm, const float* gW) {
+    WSrc w;
+    w.W = lds_ptr(sm + t.s_W);
+    int nl = t.w_rows_lds;
+    asm volatile("" : "+s"(nl));   // kept (or spilled to a lane), not re-read from memory
+    w.nl = nl;
+    w.gW = gW;
+    return w;
+}
+
 // Delassus entries A[r][g0 + q] = J_r . W_{g0+q}, q < 4, of this lane's row r (the PGS set-up of
 // both widths), the loads of DOF c + PD issued before DOF c's FMAs (a ring indexed at compile
 // time, see sdof_loop). The env has n rows; group rows past them are 0 (they hold stale data,
 // finite or not, and the sweeps only ever scale them by a zero lambda change).
-template <class TP, int PD>
-MI_D void pair_dgroup(const WaveTabs& t, const float* sm, const float* gW, int g0, int n,
-                      const float (&Jr)[TP::nvc], float (&a)[4]) {
+// (W rows from a WSrc: LDS rows [0, nl), the slab beyond; kLds: LDS rows only)
+template <class TP, int PD, bool kLds>
+MI_D void pair_dgroup_w(const WSrc& ws, int g0, int n, const float (&Jr)[TP::nvc], float (&a)[4]) {
     constexpr int NV = TP::nv, NB = PD + 1;
     float a0 = 0.0f, a1 = 0.0f, a2 = 0.0f, a3 = 0.0f;
-    if (g0 + 3 < t.w_rows_lds) {   // uniform: the group in LDS, one ds_read_b128 per DOF
-        const lds_cf4 W = pw_group(t, sm, g0, NV);
+    auto acc = [&](auto C, const pv4& w) {
+        a0 += Jr[C] * w.x;
+        a1 += Jr[C] * w.y;
+        a2 += Jr[C] * w.z;
+        a3 += Jr[C] * w.w;
+    };
+    if (kLds || g0 + 3 < ws.nl) {
+        const lds_cf4 W = (lds_cf4)(ws.W + g0 * NV);
         pv4 wb[NB];
         sfor<0, (PD < NV ? PD : NV)>([&](auto C) { wb[C % NB] = W[C]; });
         sfor<0, NV>([&](auto C) {
             constexpr int c = C;
             if constexpr (c + PD < NV) wb[(c + PD) % NB] = W[c + PD];
-            a0 += Jr[C] * wb[c % NB].x;
-            a1 += Jr[C] * wb[c % NB].y;
-            a2 += Jr[C] * wb[c % NB].z;
-            a3 += Jr[C] * wb[c % NB].w;
+            acc(C, wb[c % NB]);
         });
-    } else {                       // the slab: one global_load_dwordx4 per DOF
-        const glb_cf4 W = (glb_cf4)(gW + (size_t)g0 * WNV);
+    } else {
+        const glb_cf4 W = (glb_cf4)(ws.gW + (size_t)g0 * WNV);
         pv4 wb[NB];
         sfor<0, (PD < NV ? PD : NV)>([&](auto C) { wb[C % NB] = W[C]; });
         sfor<0, NV>([&](auto C) {
             constexpr int c = C;
             if constexpr (c + PD < NV) wb[(c + PD) % NB] = W[c + PD];
-            a0 += Jr[C] * wb[c % NB].x;
-            a1 += Jr[C] * wb[c % NB].y;
-            a2 += Jr[C] * wb[c % NB].z;
-            a3 += Jr[C] * wb[c % NB].w;
+            acc(C, wb[c % NB]);
         });
     }
     a[0] = g0 < n ? a0 : 0.0f;
@@ -273,15 +289,15 @@ MI_D void pair_dgroup(const WaveTabs& t, const float* sm, const float* gW, int g
     a[2] = g0 + 2 < n ? a2 : 0.0f;
     a[3] = g0 + 3 < n ? a3 : 0.0f;
 }
-
 // W entries of rows g0..g0+3 at this lane's DOF kc (the u update of both PGS widths; rows past
 // the env's count are read but never used: the caller selects them away)
-MI_D void pair_wcol(const WaveTabs& t, const float* sm, const float* gW, int g0, int kc, int nv,
-                    float (&wq)[4]) {
-    const pv4 w = g0 + 3 < t.w_rows_lds ? pw_group(t, sm, g0, nv)[kc]
-                                        : ((glb_cf4)(gW + (size_t)g0 * WNV))[kc];
+template <bool kLds>
+MI_D void pair_wcol_w(const WSrc& ws, int g0, int kc, int nv, float (&wq)[4]) {
+    const pv4 w = (kLds || g0 + 3 < ws.nl) ? ((lds_cf4)(ws.W + g0 * nv))[kc]
+                                           : ((glb_cf4)(ws.gW + (size_t)g0 * WNV))[kc];
     wq[0] = w.x; wq[1] = w.y; wq[2] = w.z; wq[3] = w.w;
 }
+
 
 // One articulated substep of the env of this lane's half (env i, LDS region sm, W slab gW).
 template <class TP>
@@ -737,12 +753,13 @@ MI_D void pair_artic_substep(const DevModel& m, const WaveTabs& t, const DevStat
         float v = 0.0f;
         sfor<0, NV>([&](auto C) { v += Jr[C] * us[C]; });
         STAMP(24);
+        const WSrc wsn = make_wsrc(t, sm, gW);
         float Ar[RMAX];
         static_assert(RMAX % 4 == 0, "Delassus rows are built four at a time");
         sfor<0, RMAX / 4>([&](auto G) {
             constexpr int g0 = 4 * G;
             float a[4] = {0.0f, 0.0f, 0.0f, 0.0f};
-            if (g0 < nrows_max) pair_dgroup<TP, MI_PAIR_SDOF_PD>(t, sm, gW, g0, nrows, Jr, a);
+            if (g0 < nrows_max) pair_dgroup_w<TP, MI_PAIR_SDOF_PD, true>(wsn, g0, nrows, Jr, a);
             Ar[g0] = a[0]; Ar[g0 + 1] = a[1]; Ar[g0 + 2] = a[2]; Ar[g0 + 3] = a[3];
         });
         STAMP(25);
@@ -824,7 +841,7 @@ MI_D void pair_artic_substep(const DevModel& m, const WaveTabs& t, const DevStat
             constexpr int g0 = 4 * G;
             if (g0 < nrows_max) {
                 float wq[4];
-                pair_wcol(t, sm, gW, g0, kc, NV, wq);
+                pair_wcol_w<true>(wsn, g0, kc, NV, wq);
 #pragma unroll
                 for (int q = 0; q < 4; ++q) u = g0 + q < nrows ? u + wq[q] * lamv[g0 + q] : u;
                 if constexpr (TP::kTgs) {
@@ -888,6 +905,7 @@ MI_D void pair_artic_substep(const DevModel& m, const WaveTabs& t, const DevStat
             // the env of half h: its slab (the pair need not be adjacent envs: pairing by load)
             const int ih = __builtin_amdgcn_readlane(i, 32 * h);
             const float* gWh = gW + (ptrdiff_t)(ih - i) * (ptrdiff_t)t.g_row_stride;
+            const WSrc wsh = make_wsrc(t, smh, gWh);
             const int rl = l64 < nrh ? l64 : 0;
             float Jr[TP::nvc];
             pair_jrow<TP>(mc, t, smh, rl, nr, Jr);
@@ -987,7 +1005,7 @@ MI_D void pair_artic_substep(const DevModel& m, const WaveTabs& t, const DevStat
                 constexpr int g0 = 4 * G;
                 float a[4] = {0.0f, 0.0f, 0.0f, 0.0f};
                 if (g0 < nrh) {
-                    pair_dgroup<TP, MI_PAIR_WIDE_PD>(t, smh, gWh, g0, nrh, Jr, a);
+                    pair_dgroup_w<TP, MI_PAIR_WIDE_PD, false>(wsh, g0, nrh, Jr, a);
                     if constexpr (g0 >= AR) {
 #pragma unroll
                         for (int q = 0; q < 4; ++q)
@@ -1020,6 +1038,8 @@ MI_D void pair_artic_substep(const DevModel& m, const WaveTabs& t, const DevStat
                 float lamn = 0.0f;
 #if MI_PAIR_SWEEP_FMA
                 const float tl = __builtin_fmaf(b, ia, lam);   // lane = row: lam changes at its own row only
+                float muv = mu, lov = 0.0f, hiv = 0.0f;        // mu in a VGPR: mu lambda_n in one v_mul
+                asm volatile("" : "+v"(muv));
 #endif
                 // rows rr .. rr + PA - 1 of A in flight. The scratch is NOT zeroed (no memset at
                 // creation): correctness rests on the invariant that the set-up writes every row
@@ -1050,21 +1070,30 @@ MI_D void pair_artic_substep(const DevModel& m, const WaveTabs& t, const DevStat
                             arr = ab[(rr - AR) % PA];
                             if constexpr (rr + PA < 64) ab[(rr - AR) % PA] = ald(rr + PA);
                         }
-                        const bool fric = kd == 1 || kd == 2;
-                        const float lim = mu * lamn;
 #if MI_PAIR_SWEEP_FMA
                         // the narrow sweeps' arithmetic (bit for bit: an env's result does not
                         // depend on the path its partner sends the wave down): the new lambda
                         // and the row's old one leave the owner by v_readlane (the old one off
-                        // the chain), v_writelane stores the new one in the owner lane
-                        const float mine = __builtin_amdgcn_fmed3f(__builtin_fmaf(-v, ia, tl), fric ? -lim : 0.0f,
-                                                                   fric ? lim : __builtin_huge_valf());
+                        // the chain), v_writelane stores the new one in the owner lane. Row
+                        // kinds are wave-uniform here (lane = row of one env): rows 3c are
+                        // normal or limit rows, [0, inf); rows 3c + 1, 3c + 2 friction rows
+                        // (+-mu lambda_3c, one v_mul per contact) below nnh, limit rows past it
+                        const float xr = __builtin_fmaf(-v, ia, tl);
+                        const float mine = rr % 3 == 0 ? __builtin_amdgcn_fmed3f(xr, 0.0f, __builtin_huge_valf())
+                                                       : __builtin_amdgcn_fmed3f(xr, lov, hiv);
                         const float ln = readlane(mine, rr), l0 = readlane(lam, rr);
-                        if constexpr (rr % 3 == 0) lamn = rr < nnh ? ln : lamn;
+                        if constexpr (rr % 3 == 0) {   // the next two rows' bounds (uniform select)
+                            const float lm = muv * ln;
+                            const bool fr = rr + 1 < nnh;
+                            hiv = fr ? lm : __builtin_huge_valf();
+                            lov = fr ? -lm : 0.0f;
+                        }
                         v = __builtin_fmaf(arr, ln, __builtin_fmaf(-arr, l0, v));
                         asm("v_writelane_b32 %0, %1, %2" : "+v"(lam) : "s"(ln), "i"(rr));
                         (void)lw;
 #else
+                        const bool fric = kd == 1 || kd == 2;
+                        const float lim = mu * lamn;
                         const float mine = __builtin_amdgcn_fmed3f(lam + (b - v) * ia, fric ? -lim : 0.0f,
                                                                    fric ? lim : __builtin_huge_valf());
                         // the owner forms the lambda change itself (mine - lam there is exactly
@@ -1091,7 +1120,7 @@ MI_D void pair_artic_substep(const DevModel& m, const WaveTabs& t, const DevStat
             // the next group's W column is loaded before this group's FMAs (rows past the LDS
             // ones come from the slab: one L2 round trip per group on the chain otherwise)
             float wn[4] = {0.0f, 0.0f, 0.0f, 0.0f};
-            pair_wcol(t, smh, gWh, 0, kc, NV, wn);
+            pair_wcol_w<false>(wsh, 0, kc, NV, wn);
 #endif
             sfor<0, 16>([&](auto G) {
                 constexpr int g0 = 4 * G;
@@ -1101,9 +1130,9 @@ MI_D void pair_artic_substep(const DevModel& m, const WaveTabs& t, const DevStat
 #pragma unroll
                     for (int q = 0; q < 4; ++q) wq[q] = wn[q];
                     if constexpr (g0 + 4 < 64)
-                        if (g0 + 4 < nrh) pair_wcol(t, smh, gWh, g0 + 4, kc, NV, wn);
+                        if (g0 + 4 < nrh) pair_wcol_w<false>(wsh, g0 + 4, kc, NV, wn);
 #else
-                    pair_wcol(t, smh, gWh, g0, kc, NV, wq);
+                    pair_wcol_w<false>(wsh, g0, kc, NV, wq);
 #endif
 #pragma unroll
                     for (int q = 0; q < 4; ++q) {

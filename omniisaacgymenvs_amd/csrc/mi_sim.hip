@@ -1479,6 +1479,10 @@ int mi_sim_create(const mi_model_desc* md, const mi_sim_params* prm, int32_t N, 
         if (s->pair && ((self_on && t.s_seg < 0) || s->lds_bytes > 163840))
             return cleanup(fail(MI_E_STATE, "paired wave layout does not fit (%zu B of LDS per workgroup)",
                                 s->lds_bytes));
+        // the paired kernels' narrow PGS reads its W rows from LDS only (mi_pair.hpp WSrc)
+        if (s->pair && t.w_rows_lds < lam_rows)
+            return cleanup(fail(MI_E_STATE, "paired wave layout: %d LDS W rows < %d Delassus rows",
+                                t.w_rows_lds, lam_rows));
     }
     s->lower.assign(md->lower, md->lower + L);
     s->upper.assign(md->upper, md->upper + L);
