@@ -37,7 +37,11 @@ struct SimP {
 // row stores its bias). TGS: over the sub-step h from the row's current separation; position
 // iterations correct a penetration (erp), velocity iterations only keep the speculative part.
 MI_D float row_bias(const SimP& p, float e, float step, bool correct) {
-    float b = e >= 0.0f ? -e / step : (correct ? -p.erp * e / step : 0.0f);
+    // e >= 0 ? -e / step : (correct ? -erp e / step : 0), with ONE division: the numerator is
+    // selected first (same roundings; a lane-divergent select ran both divisions' ~10-op
+    // sequences under exec masks, once per sweep in the TGS sweeps)
+    const float num = e >= 0.0f ? -e : (correct ? -p.erp * e : 0.0f);
+    const float b = num / step;
     return b > p.max_depen ? p.max_depen : b;
 }
 
