@@ -223,6 +223,10 @@ MI_D lds_cf lds_ptr(const float* p) { return (lds_cf)p; }
 // wave) and the u update's four rows of the lane's DOF — instead of four ds_read_b32.
 // w_rows_lds is a multiple of 4 (host), so a group is wholly in LDS or wholly in the slab.
 typedef float pv4 __attribute__((ext_vector_type(4)));
+typedef float pv2 __attribute__((ext_vector_type(2)));
+#ifndef MI_PK_FMA
+#define MI_PK_FMA 1   // Delassus set-up on packed FP32 FMAs (v_pk_fma_f32)
+#endif
 typedef const pv4 __attribute__((address_space(3)))* lds_cf4;
 MI_D int pw_idx(int r, int c, int nv) { return (r & ~3) * nv + 4 * c + (r & 3); }
 // The env's global W slab (rows >= w_rows_lds, up to MI_MAX_ROWS) uses the same 4-row groups,
@@ -258,6 +262,16 @@ MI_D WSrc make_wsrc(const WaveTabs& t, const float* sm, const float* gW) {
 template <class TP, int PD, bool kLds>
 MI_D void pair_dgroup_w(const WSrc& ws, int g0, int n, const float (&Jr)[TP::nvc], float (&a)[4]) {
     constexpr int NV = TP::nv, NB = PD + 1;
+#if MI_PK_FMA
+    // two rows' chains per v_pk_fma_f32 (the same fused multiply-add per element, half the
+    // VALU instructions)
+    pv2 a01 = {0.0f, 0.0f}, a23 = {0.0f, 0.0f};
+    auto acc = [&](auto C, const pv4& w) {
+        const pv2 j = {Jr[C], Jr[C]};
+        a01 = __builtin_elementwise_fma(j, w.xy, a01);
+        a23 = __builtin_elementwise_fma(j, w.zw, a23);
+    };
+#else
     float a0 = 0.0f, a1 = 0.0f, a2 = 0.0f, a3 = 0.0f;
     auto acc = [&](auto C, const pv4& w) {
         a0 += Jr[C] * w.x;
@@ -265,6 +279,7 @@ MI_D void pair_dgroup_w(const WSrc& ws, int g0, int n, const float (&Jr)[TP::nvc
         a2 += Jr[C] * w.z;
         a3 += Jr[C] * w.w;
     };
+#endif
     if (kLds || g0 + 3 < ws.nl) {
         const lds_cf4 W = (lds_cf4)(ws.W + g0 * NV);
         pv4 wb[NB];
@@ -284,6 +299,9 @@ MI_D void pair_dgroup_w(const WSrc& ws, int g0, int n, const float (&Jr)[TP::nvc
             acc(C, wb[c % NB]);
         });
     }
+#if MI_PK_FMA
+    const float a0 = a01.x, a1 = a01.y, a2 = a23.x, a3 = a23.y;
+#endif
     a[0] = g0 < n ? a0 : 0.0f;
     a[1] = g0 + 1 < n ? a1 : 0.0f;
     a[2] = g0 + 2 < n ? a2 : 0.0f;
