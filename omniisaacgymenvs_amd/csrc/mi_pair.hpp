@@ -175,10 +175,23 @@ constexpr int kWideScratchRows = MI_PAIR_WIDE_MFMA ? 64 + 32 : 64 - MI_PAIR_WIDE
 // S_c . f for DOF c: the free root's six DOFs have unit subspaces (linear x, y, z then angular
 // x, y, z: the P1 set-up below), so their dot product is one component of f (what dot6 with a
 // unit vector returns, up to the sign of a zero); the joint DOFs' from S_c in LDS
+typedef float pv2 __attribute__((ext_vector_type(2)));
+// dot6 as two packed-FP32 chains (even / odd terms, v_pk_mul + 2 v_pk_fma + one add: 4 VALU
+// ops instead of 6); the summation order is (a0 b0 + a2 b2 + a4 b4) + (a1 b1 + a3 b3 + a5 b5)
+MI_D float dot6p(const float (&a)[6], const float (&b)[6]) {
+    pv2 p = pv2{a[0], a[1]} * pv2{b[0], b[1]};
+    p = __builtin_elementwise_fma(pv2{a[2], a[3]}, pv2{b[2], b[3]}, p);
+    p = __builtin_elementwise_fma(pv2{a[4], a[5]}, pv2{b[4], b[5]}, p);
+    return p.x + p.y;
+}
 template <class TP, int c>
 MI_D float sdot(const float (&sv)[6], const float (&f)[6]) {
     if constexpr (TP::nr == 6 && c < 6) return f[c < 3 ? 3 + c : c - 3];
+#if MI_PK_DOT
+    else return dot6p(sv, f);
+#else
     else return dot6(sv, f);
+#endif
 }
 constexpr int sdof_first_loaded(int nr) { return nr == 6 ? 6 : 0; }
 
@@ -223,9 +236,11 @@ MI_D lds_cf lds_ptr(const float* p) { return (lds_cf)p; }
 // wave) and the u update's four rows of the lane's DOF — instead of four ds_read_b32.
 // w_rows_lds is a multiple of 4 (host), so a group is wholly in LDS or wholly in the slab.
 typedef float pv4 __attribute__((ext_vector_type(4)));
-typedef float pv2 __attribute__((ext_vector_type(2)));
 #ifndef MI_PK_FMA
 #define MI_PK_FMA 1   // Delassus set-up on packed FP32 FMAs (v_pk_fma_f32)
+#endif
+#ifndef MI_PK_DOT
+#define MI_PK_DOT 1   // S_c . f (J rows, CRBA columns) as two packed-FP32 chains
 #endif
 typedef const pv4 __attribute__((address_space(3)))* lds_cf4;
 MI_D int pw_idx(int r, int c, int nv) { return (r & ~3) * nv + 4 * c + (r & 3); }
