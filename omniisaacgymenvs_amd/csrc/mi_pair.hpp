@@ -373,18 +373,18 @@ MI_D void pair_artic_substep(const DevModel& m, const WaveTabs& t, const DevStat
     // ---- P2: composite inertia / force
     float* aux = sm + t.s_X;
     {
-        const float4* recs = reinterpret_cast<const float4*>(sm + t.s_F);
+        // native 4-vectors: each record sum is two v_pk_add_f32 per float4 (the same adds)
+        const pv4* recs = reinterpret_cast<const pv4*>(sm + t.s_F);
         for (int l = lane; l < L; l += 32) {
-            float4 a0 = recs[4 * l], a1 = recs[4 * l + 1], a2 = recs[4 * l + 2], a3 = recs[4 * l + 3];
+            pv4 a0 = recs[4 * l], a1 = recs[4 * l + 1], a2 = recs[4 * l + 2], a3 = recs[4 * l + 3];
             for (int di = mc.desc_start(l); di < mc.desc_start(l + 1); ++di) {
                 const int d = mc.desc(di);
-                const float4 b0 = recs[4 * d], b1 = recs[4 * d + 1], b2 = recs[4 * d + 2], b3 = recs[4 * d + 3];
-                a0.x += b0.x; a0.y += b0.y; a0.z += b0.z; a0.w += b0.w;
-                a1.x += b1.x; a1.y += b1.y; a1.z += b1.z; a1.w += b1.w;
-                a2.x += b2.x; a2.y += b2.y; a2.z += b2.z; a2.w += b2.w;
-                a3.x += b3.x; a3.y += b3.y; a3.z += b3.z; a3.w += b3.w;
+                a0 += recs[4 * d];
+                a1 += recs[4 * d + 1];
+                a2 += recs[4 * d + 2];
+                a3 += recs[4 * d + 3];
             }
-            float4* o = reinterpret_cast<float4*>(aux) + 4 * l;
+            pv4* o = reinterpret_cast<pv4*>(aux) + 4 * l;
             o[0] = a0; o[1] = a1; o[2] = a2; o[3] = a3;
         }
     }
