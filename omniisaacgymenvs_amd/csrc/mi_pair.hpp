@@ -184,6 +184,25 @@ MI_D float dot6p(const float (&a)[6], const float (&b)[6]) {
     p = __builtin_elementwise_fma(pv2{a[4], a[5]}, pv2{b[4], b[5]}, p);
     return p.x + p.y;
 }
+// J_r . u over the NV DOFs (u in LDS, uniform per half) as two packed-FP32 chains (even / odd
+// DOFs), then their sum: the narrow and the wide PGS form v_r the same way
+template <int NV, int NVC>
+MI_D float pk_jdot(const float (&J)[NVC], const float* u) {
+#if MI_PK_DOT
+    pv2 p = {0.0f, 0.0f};
+    sfor<0, NV / 2>([&](auto H) {
+        constexpr int c = 2 * H;
+        p = __builtin_elementwise_fma(pv2{J[c], J[c + 1]}, pv2{u[c], u[c + 1]}, p);
+    });
+    float v = p.x + p.y;
+    if constexpr (NV % 2) v += J[NV - 1] * u[NV - 1];
+    return v;
+#else
+    float v = 0.0f;
+    sfor<0, NV>([&](auto C) { v += J[C] * u[C]; });
+    return v;
+#endif
+}
 template <class TP, int c>
 MI_D float sdot(const float (&sv)[6], const float (&f)[6]) {
     if constexpr (TP::nr == 6 && c < 6) return f[c < 3 ? 3 + c : c - 3];
@@ -783,8 +802,7 @@ MI_D void pair_artic_substep(const DevModel& m, const WaveTabs& t, const DevStat
             if (nrows > 0) pair_jrow<TP>(mc, t, sm, lane < nrows ? lane : 0, nr, Jr);
             else sfor<0, NV>([&](auto C) { Jr[C] = 0.0f; });
         }
-        float v = 0.0f;
-        sfor<0, NV>([&](auto C) { v += Jr[C] * us[C]; });
+        float v = pk_jdot<NV>(Jr, us);
         STAMP(24);
         const WSrc wsn = make_wsrc(t, sm, gW);
         float Ar[RMAX];
@@ -943,8 +961,7 @@ MI_D void pair_artic_substep(const DevModel& m, const WaveTabs& t, const DevStat
             float Jr[TP::nvc];
             pair_jrow<TP>(mc, t, smh, rl, nr, Jr);
             const float* ush = smh + t.s_us;
-            float v = 0.0f;
-            sfor<0, NV>([&](auto C) { v += Jr[C] * ush[C]; });
+            float v = pk_jdot<NV>(Jr, ush);
             STAMP(30);
             float Ar[AR > 0 ? AR : 1];
 #if MI_PAIR_WIDE_MFMA
