@@ -562,9 +562,13 @@ static size_t post_pipe_lds(int es, int A, int O, int D, int S, int te = 32) {
     return sizeof(float) * (size_t)(te * g.P + 4 + te * O + 2 * te + 4);
 }
 
+#ifndef MI_PIPE_ROT
+#define MI_PIPE_ROT 1   // rotated pipeline with fixed-count stores (0: loads consumed at the loop head)
+#endif
+// NO4: obs float4s per lane per tile (>= TE O / 256, host-checked).
 // TE envs per tile (32, or 16: half the LDS and prefetch registers per workgroup, so more
 // workgroups stay resident; lanes e + 16 then repeat env e's root / reward chains, writing nothing)
-template <int TE, int NR4, int NS4>
+template <int TE, int NR4, int NS4, int NO4>
 __global__ __launch_bounds__(64) void k_loco_post_pipe(const KParams* __restrict__ kp_arg,
                                                       const float* __restrict__ actions,
                                                       float* obs, float* rew, int64_t* reset_buf,
@@ -621,6 +625,116 @@ __global__ __launch_bounds__(64) void k_loco_post_pipe(const KParams* __restrict
     const float dof_hi = dof_lane ? kp->m.upper[dof_j + 1] : 1.0f;
     const int sen_pe = ns > 0 ? 64 / ns : 0, sen_le = ns > 0 ? lane / ns : 0, sen_c = lane - sen_le * ns;
     const bool sen_lane = ns > 0 && sen_le < sen_pe;
+#if MI_PIPE_ROT
+    // Rotated pipeline: tile t + G's loads are issued after tile t's first barrier and moved
+    // into LDS at the END of iteration t, after tile t's stores. Every memory op between the two
+    // is an unconditional store of a fixed count (per-env outputs from all 64 lanes, NO4 obs
+    // float4s + one tail dword per lane, indices clamped: lanes past the tile re-store the
+    // tile's last element with the same data), so the wait for the loads is vmcnt(<that count>)
+    // and tile t's stores stay in flight. (With the loads consumed at the loop head, the
+    // variable-count store loops made the compiler wait for all but two of the tile's stores
+    // before each next tile: store acknowledgements on the chain of every tile.)
+    int64_t c_progress = 0, c_rb = 0;
+    int c_nflag = 0;
+#define MI_PIPE_STAGE(T)                                                                         \
+    do {                                                                                        \
+        _Pragma("unroll") for (int r = 0; r < NR4; ++r) {                                        \
+            const int kk = lane + 64 * r, e = div_small(kk, mag_ne);                            \
+            srec4[kk < TE * g.ne4 ? e * g.P4 + (kk - e * g.ne4) : spare4] = rr[r];               \
+        }                                                                                       \
+        _Pragma("unroll") for (int r = 0; r < NS4; ++r) {                                        \
+            const int kk = lane + 64 * r, e = div_small(kk, mag_ns);                            \
+            srec4[kk < TE * g.ns4 ? e * g.P4 + g.ne4 + (kk - e * g.ns4) : spare4] = rsn[r];      \
+        }                                                                                       \
+        _Pragma("unroll") for (int r = 0; r < MI_PIPE_A; ++r) {                                  \
+            const int kk = lane + 64 * r, e = div_small(kk, mag_a);                             \
+            sobs[kk < TE * A ? e * O + ka + (kk - e * A) : trash_o] = ra[r];                    \
+        }                                                                                       \
+        c_progress = pg + 1;                  /* rl_task.py:242 */                              \
+        c_rb = rs;                                                                              \
+        c_nflag = nf;                                                                           \
+        if (lane < TE) spot[lane] = pt;                                                         \
+    } while (0)
+    int t = blockIdx.x;
+    if (t < ntiles) {
+        MI_PIPE_ISSUE(kp, t);
+        MI_PIPE_STAGE(t);
+    }
+    for (; t < ntiles; t += gridDim.x) {
+        const KParams* k = opaque_kp(kp_arg);
+        const int e0 = t * TE, n = min(TE, N - e0);
+        const int64_t progress = c_progress, rb = c_rb;
+        const int nflag = c_nflag;
+        __syncthreads();
+        if (nflag && lane < n) {              // nan_guard bookkeeping, ahead of the next loads
+            k->st.nan_flag[e0 + lane] = 0;
+            atomicAdd(k->st.nan_total, 1ull);
+        }
+        const bool more = t + (int)gridDim.x < ntiles;
+        if (more) MI_PIPE_ISSUE(k, t + (int)gridDim.x);   // in flight during the math and stores
+        if (dof_lane) {
+            const float vs = k->tp.dof_vel_scale;
+            for (int e = dof_le; e < n; e += dof_pe) {
+                const float* r = srec + e * g.P;
+                float* o = sobs + e * O;
+                o[12 + dof_j] = ref_unscale(r[13 + dof_j], dof_lo, dof_hi);
+                o[12 + D + dof_j] = r[13 + D + dof_j] * vs;
+            }
+        }
+        if (sen_lane) {
+            const float cs = k->tp.contact_force_scale;
+            for (int e = sen_le; e < n; e += sen_pe)
+                sobs[e * O + 12 + 2 * D + sen_c] = srec[e * g.P + g.s0 + sen_c] * cs;
+        }
+        __syncthreads();
+        const int pl = TE == 32 ? lane : ((lane & 15) | (lane & 32));
+        const bool pw = TE == 32 || (lane & 16) == 0;
+        {
+            const DevTask& tp = k->tp;
+            const int e = pl & 31;
+            float* R = sobs + (size_t)e * O;
+            loco_obs_root_pair(srec + e * g.P, tp, pl, R, spot, sprev, e < n && pw);
+        }
+        const LocoTerms lt = loco_reward_terms_pair(k->tp, D, sobs + (size_t)(pl & 31) * O,
+                                                    sobs + (size_t)(pl & 31) * O + ka, pl);
+        {
+            // per-env outputs: computed on each lane for slot lane & (TE - 1) (valid where the
+            // lower half holds that env), then every lane stores env el's values from lane el
+            const DevTask& tp = k->tp;
+            const int sl = lane & (TE - 1);
+            const float* R = sobs + (size_t)sl * O;
+            const float rv = loco_reward_total(tp, R[0], R[10], R[11], spot[sl], sprev[sl], lt);
+            const int64_t d = nflag ? 1 : loco_done(tp, R[0], rb, progress);
+            const int el = min(sl, n - 1), i = e0 + el;
+            const float rew_v = __shfl(rv, el);
+            const int d_v = __shfl((int)d, el);
+            const uint32_t pr_lo = (uint32_t)__shfl((int)(uint32_t)progress, el);
+            const uint32_t pr_hi = (uint32_t)__shfl((int)(uint32_t)((uint64_t)progress >> 32), el);
+            rew[i] = rew_v;
+            pot[i] = spot[el];
+            prev[i] = sprev[el];
+            reset_buf[i] = (int64_t)d_v;
+            progress_buf[i] = (int64_t)(((uint64_t)pr_hi << 32) | pr_lo);
+        }
+        __syncthreads();
+        {
+            float* dst = obs + (size_t)e0 * O;   // 16-B aligned (host-checked), e0 * O * 4 B = 128 B multiples
+            const int cnt = n * O, n4 = cnt >> 2;
+#pragma unroll
+            for (int r = 0; r < NO4; ++r) {
+                const int kk = min(lane + 64 * r, n4 - 1);
+                __builtin_nontemporal_store(reinterpret_cast<const v4f*>(sobs)[kk], reinterpret_cast<v4f*>(dst) + kk);
+            }
+            const int kt = min(4 * n4 + lane, cnt - 1);   // ragged tail (< 4 floats), else a re-store
+            dst[kt] = sobs[kt];
+        }
+        __syncthreads();                    // the next tile overwrites the LDS tiles
+        if (more) MI_PIPE_STAGE(t + (int)gridDim.x);
+    }
+#undef MI_PIPE_STAGE
+#undef MI_PIPE_ISSUE
+}
+#else
     int t = blockIdx.x;
     if (t < ntiles) MI_PIPE_ISSUE(kp, t);
     for (; t < ntiles; t += gridDim.x) {
@@ -709,6 +823,7 @@ __global__ __launch_bounds__(64) void k_loco_post_pipe(const KParams* __restrict
     }
 #undef MI_PIPE_ISSUE
 }
+#endif
 
 // register budget of the wave kernels: TopoCT::kWaves waves per SIMD
 #define MI_WAVE_OCC __attribute__((amdgpu_waves_per_eu(T::kWaves, T::kWaves)))
@@ -1996,14 +2111,15 @@ int mi_task_post_step(mi_sim* s, const float* actions, float* obs, float* rew, i
         if (s->tp.kind != MI_TASK_CARTPOLE && s->wave && s->kp_dev && s->ds.fs == 1 && es % 32 == 0 &&
             s->ds.sfs == 1 && s->ds.ses == ns && ns % 4 == 0 && combo &&
             s->tp.A >= 1 && s->tp.A <= 32 && s->dm.D >= 1 && s->dm.D <= 64 &&
-            ns <= 64 && tile <= 64 * 1024) {
+            ns <= 64 && tile <= 64 * 1024 && s->tp.O >= 4 && (((uintptr_t)obs) & 15) == 0 &&
+            (pte * s->tp.O + 255) / 256 <= (combo == 1 ? 11 : combo == 2 ? 8 : combo == 3 ? 6 : 4)) {
             if (s->num_cu <= 0)
                 HIP_TRY(hipDeviceGetAttribute(&s->num_cu, hipDeviceAttributeMultiprocessorCount, s->device));
             const int ntiles = (s->N + pte - 1) / pte;
-            const void* fn = combo == 1 ? (const void*)k_loco_post_pipe<32, 7, 2>
-                           : combo == 2 ? (const void*)k_loco_post_pipe<32, 4, 3>
-                           : combo == 3 ? (const void*)k_loco_post_pipe<16, 4, 1>
-                                        : (const void*)k_loco_post_pipe<16, 2, 2>;
+            const void* fn = combo == 1 ? (const void*)k_loco_post_pipe<32, 7, 2, 11>
+                           : combo == 2 ? (const void*)k_loco_post_pipe<32, 4, 3, 8>
+                           : combo == 3 ? (const void*)k_loco_post_pipe<16, 4, 1, 6>
+                                        : (const void*)k_loco_post_pipe<16, 2, 2, 4>;
             // one resident round: workgroups per CU as registers and LDS allow together
             int per_cu = 0;
             HIP_TRY(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, fn, 64, tile));
@@ -2017,15 +2133,15 @@ int mi_task_post_step(mi_sim* s, const float* actions, float* obs, float* rew, i
             const KParams* kp = (const KParams*)s->kp_dev;
             hipEvent_t ev0 = nullptr, ev1 = nullptr;
             HIP_TRY(timed_launch(s, stream, &ev0, &ev1));
-#define POST_PIPE(T, R, Q) do { if (ev0) hipExtLaunchKernelGGL((k_loco_post_pipe<T, R, Q>), dim3(grid), dim3(64), (uint32_t)tile, \
+#define POST_PIPE(T, R, Q, W) do { if (ev0) hipExtLaunchKernelGGL((k_loco_post_pipe<T, R, Q, W>), dim3(grid), dim3(64), (uint32_t)tile, \
             STREAM(stream), ev0, ev1, 0, kp, actions, obs, rew, reset_buf, progress_buf, potentials, prev_potentials); \
-            else hipLaunchKernelGGL((k_loco_post_pipe<T, R, Q>), dim3(grid), dim3(64), tile, STREAM(stream), kp, \
+            else hipLaunchKernelGGL((k_loco_post_pipe<T, R, Q, W>), dim3(grid), dim3(64), tile, STREAM(stream), kp, \
             actions, obs, rew, reset_buf, progress_buf, potentials, prev_potentials); } while (0)
             switch (combo) {
-                case 1: POST_PIPE(32, 7, 2); break;
-                case 2: POST_PIPE(32, 4, 3); break;
-                case 3: POST_PIPE(16, 4, 1); break;
-                default: POST_PIPE(16, 2, 2); break;
+                case 1: POST_PIPE(32, 7, 2, 11); break;
+                case 2: POST_PIPE(32, 4, 3, 8); break;
+                case 3: POST_PIPE(16, 4, 1, 6); break;
+                default: POST_PIPE(16, 2, 2, 4); break;
             }
 #undef POST_PIPE
             LAUNCH_CHECK();
